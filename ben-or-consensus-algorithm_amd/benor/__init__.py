@@ -1,0 +1,341 @@
+"""Python mirror of the reference's public surface, over libbenor.so (C ABI).
+
+The reference (viviendbk/ben-or-consensus-algorithm) exposes, in TypeScript:
+
+    launchNetwork(N, F, initialValues, faultyList)   src/index.ts:4-14
+    startConsensus(N) / stopConsensus(N)             src/nodes/consensus.ts:3-15
+    GET /status, /getState on port 3000 + i          src/nodes/node.ts:33-39, :197-199
+    getNodesState(N), reachedFinality(states)        __test__/tests/utils.ts:14-24
+
+The same names, argument meanings and errors are provided here (the
+JavaScript mirror for Node lives in ../js/).  As in the reference, one network
+is "listening" at a time: startConsensus(N) / stopConsensus(N) / getNodesState(N)
+address the network most recently launched.  Consensus itself runs as one HIP
+kernel on the current device; there is no CPU fallback -- without the built
+library or a gfx950 device every compute call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import secrets
+from typing import Sequence
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libbenor.so")
+
+BO_OK = 0
+BO_ERR_ARRAYS_DONT_MATCH = 1
+BO_ERR_FAULTY_COUNT = 2
+BO_ERR_INVALID_ARGUMENT = 3
+BO_ERR_NO_DEVICE = 4
+BO_ERR_HIP = 5
+BO_ERR_OUT_OF_RANGE = 6
+BO_ERR_UNSUPPORTED = 7
+BO_MODE_LOCKSTEP = 0
+BO_INIT_RANDOM = 0
+BO_INIT_FIXED = 1
+BO_MAX_N = 4096
+BO_MAX_K = 1024
+
+BASE_NODE_PORT = 3000          # src/config.ts:1 (kept for the HTTP-shaped helpers)
+DEFAULT_K_MAX = 64             # round cap; the reference runs until /stop
+
+# Symbols the C ABI exports (include/benor.h); checked by tests.
+EXPORTED_SYMBOLS = (
+    "bo_network_create", "bo_consensus_start", "bo_consensus_stop", "bo_node_stop",
+    "bo_get_state", "bo_status", "bo_network_size", "bo_network_destroy", "bo_hist_len",
+    "bo_plan_create", "bo_plan_launch", "bo_plan_run", "bo_plan_popc_words_per_node_round",
+    "bo_plan_live_nodes", "bo_plan_destroy", "bo_run_trials", "bo_run_trial_states",
+    "bo_popc_peak", "bo_last_error", "bo_abi_version",
+)
+
+
+class Error(Exception):
+    """The reference's `new Error(message)` (launchNodes.ts:11,13)."""
+
+
+class NodeStateC(ctypes.Structure):
+    _fields_ = [("killed", ctypes.c_int8), ("x", ctypes.c_int8), ("decided", ctypes.c_int8),
+                ("pad", ctypes.c_int8), ("k", ctypes.c_int32)]
+
+
+class TrialsCfgC(ctypes.Structure):
+    _fields_ = [("N", ctypes.c_uint32), ("F", ctypes.c_uint32), ("k_max", ctypes.c_uint32),
+                ("init_mode", ctypes.c_uint32), ("mode", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+                ("seed", ctypes.c_uint64), ("faulty", ctypes.POINTER(ctypes.c_uint8)),
+                ("init", ctypes.POINTER(ctypes.c_int8))]
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libbenor.so; raises if it was not built (no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libbenor.so not built at {LIB_PATH}: run __graft_entry__.build()")
+    L = ctypes.CDLL(LIB_PATH)
+    P = ctypes.POINTER
+    L.bo_network_create.argtypes = [ctypes.c_uint32, ctypes.c_uint32, P(ctypes.c_int8), ctypes.c_uint32,
+                                    P(ctypes.c_uint8), ctypes.c_uint32, P(ctypes.c_void_p)]
+    L.bo_consensus_start.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32]
+    L.bo_consensus_stop.argtypes = [ctypes.c_void_p]
+    L.bo_node_stop.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+    L.bo_get_state.argtypes = [ctypes.c_void_p, ctypes.c_uint32, P(NodeStateC)]
+    L.bo_status.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+    L.bo_network_size.argtypes = [ctypes.c_void_p]
+    L.bo_network_size.restype = ctypes.c_uint32
+    L.bo_network_destroy.argtypes = [ctypes.c_void_p]
+    L.bo_network_destroy.restype = None
+    L.bo_hist_len.argtypes = [ctypes.c_uint32]
+    L.bo_hist_len.restype = ctypes.c_uint32
+    L.bo_plan_create.argtypes = [P(TrialsCfgC), P(ctypes.c_void_p)]
+    L.bo_plan_launch.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
+                                 ctypes.c_void_p]
+    L.bo_plan_run.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, P(ctypes.c_uint64)]
+    L.bo_plan_popc_words_per_node_round.argtypes = [ctypes.c_void_p]
+    L.bo_plan_popc_words_per_node_round.restype = ctypes.c_uint64
+    L.bo_plan_live_nodes.argtypes = [ctypes.c_void_p]
+    L.bo_plan_live_nodes.restype = ctypes.c_uint32
+    L.bo_plan_destroy.argtypes = [ctypes.c_void_p]
+    L.bo_plan_destroy.restype = None
+    L.bo_run_trials.argtypes = [P(TrialsCfgC), ctypes.c_uint64, ctypes.c_uint64, P(ctypes.c_uint64)]
+    L.bo_run_trial_states.argtypes = [P(TrialsCfgC), ctypes.c_uint64, P(NodeStateC), P(ctypes.c_uint32)]
+    L.bo_popc_peak.argtypes = [ctypes.c_uint32]
+    L.bo_popc_peak.restype = ctypes.c_double
+    L.bo_last_error.restype = ctypes.c_char_p
+    L.bo_abi_version.restype = ctypes.c_int
+    _lib = L
+    return L
+
+
+def last_error() -> str:
+    return lib().bo_last_error().decode()
+
+
+def _check(rc: int) -> None:
+    if rc != BO_OK:
+        msg = last_error()
+        if rc in (BO_ERR_ARRAYS_DONT_MATCH, BO_ERR_FAULTY_COUNT):
+            raise Error(msg)
+        raise RuntimeError(f"libbenor error {rc}: {msg}")
+
+
+_VAL = {0: 0, 1: 1, "?": 2}
+_UNVAL = {-1: None, 0: 0, 1: 1, 2: "?"}
+
+
+def _state_dict(s: NodeStateC) -> dict:
+    """NodeState (src/types.ts:1-8)."""
+    return {"killed": bool(s.killed), "x": _UNVAL[s.x],
+            "decided": None if s.decided < 0 else bool(s.decided),
+            "k": None if s.k < 0 else int(s.k)}
+
+
+class Node:
+    """Stands in for one of the `http.Server` objects launchNetwork returns:
+    the caller may close() it (benorconsensus.test.ts:14-29); the node's
+    routes are getState() / status()."""
+
+    def __init__(self, net: "Network", node_id: int):
+        self._net, self.node_id = net, node_id
+        self.port = BASE_NODE_PORT + node_id
+
+    def close(self, cb=None):
+        if cb is not None:
+            cb()
+
+    def closeAllConnections(self):
+        return None
+
+    def getState(self) -> dict:
+        return self._net.get_state(self.node_id)
+
+    def status(self) -> tuple[int, str]:
+        return self._net.status(self.node_id)
+
+
+class Network:
+    """Owns one bo_network handle (host-side node state)."""
+
+    def __init__(self, N: int, F: int, initialValues: Sequence, faultyList: Sequence[bool]):
+        L = lib()
+        n_init, n_f = len(initialValues), len(faultyList)
+        init = (ctypes.c_int8 * max(1, n_init))(*[_VAL.get(v, -2) for v in initialValues])
+        fl = (ctypes.c_uint8 * max(1, n_f))(*[1 if v is True else 0 for v in faultyList])
+        h = ctypes.c_void_p()
+        _check(L.bo_network_create(N, F, init, n_init, fl, n_f, ctypes.byref(h)))
+        self._h = h
+        self.N, self.F = N, F
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and _lib is not None:
+            _lib.bo_network_destroy(h)
+            self._h = None
+
+    def start(self, seed: int | None = None, k_max: int = DEFAULT_K_MAX) -> None:
+        if seed is None:
+            seed = secrets.randbits(64)        # the reference's coin is Math.random()
+        _check(lib().bo_consensus_start(self._h, seed, k_max))
+
+    def stop(self) -> None:
+        _check(lib().bo_consensus_stop(self._h))
+
+    def stop_node(self, i: int) -> None:
+        _check(lib().bo_node_stop(self._h, i))
+
+    def get_state(self, i: int) -> dict:
+        s = NodeStateC()
+        _check(lib().bo_get_state(self._h, i, ctypes.byref(s)))
+        return _state_dict(s)
+
+    def status(self, i: int) -> tuple[int, str]:
+        """GET /status (node.ts:33-39): (500, "faulty") or (200, "live")."""
+        code = lib().bo_status(self._h, i)
+        if code < 0:
+            _check(-code)
+        return (500, "faulty") if code == 500 else (200, "live")
+
+
+_current: Network | None = None
+
+
+def launchNetwork(N: int, F: int, initialValues: Sequence, faultyList: Sequence[bool]) -> list[Node]:
+    """src/index.ts:4-14 -> launchNodes.ts:4-44.  Raises Error("Arrays don't
+    match") / Error("faultyList doesnt have F faulties") like the reference."""
+    global _current
+    net = Network(N, F, initialValues, faultyList)
+    _current = net
+    return [Node(net, i) for i in range(N)]
+
+
+def _net(N: int) -> Network:
+    if _current is None or _current.N != N:
+        raise RuntimeError(f"no launched network of size {N}")
+    return _current
+
+
+def startConsensus(N: int, seed: int | None = None, k_max: int = DEFAULT_K_MAX) -> None:
+    """src/nodes/consensus.ts:3-8: GET /start on every node, then the round
+    loop (node.ts:43-163) on the GPU until every live node decided or k_max."""
+    if N == 0:
+        return
+    _net(N).start(seed, k_max)
+
+
+def stopConsensus(N: int) -> None:
+    """src/nodes/consensus.ts:10-15: GET /stop on every node."""
+    if N == 0:
+        return
+    _net(N).stop()
+
+
+def getNodeState(nodeId: int) -> dict:
+    """__test__/tests/utils.ts:4-12 (GET /getState)."""
+    if _current is None:
+        raise RuntimeError("no launched network")
+    return _current.get_state(nodeId)
+
+
+def getNodesState(N: int) -> list[dict]:
+    """__test__/tests/utils.ts:14-20."""
+    net = _net(N)
+    return [net.get_state(i) for i in range(N)]
+
+
+def getStatus(nodeId: int) -> tuple[int, str]:
+    if _current is None:
+        raise RuntimeError("no launched network")
+    return _current.status(nodeId)
+
+
+def reachedFinality(states: Sequence[dict]) -> bool:
+    """__test__/tests/utils.ts:22-24."""
+    return all(s["decided"] is not False for s in states)
+
+
+# ------------------------------------------------------------------ batches
+def hist_len(k_max: int) -> int:
+    return (k_max + 1) * 3 + 1
+
+
+class TrialsPlan:
+    """Many independent trials of one (N, F, faulty) network shape on the
+    current device (bo_plan_*)."""
+
+    def __init__(self, N: int, F: int, faulty: Sequence[bool] | None = None, *, seed: int = 0,
+                 k_max: int = DEFAULT_K_MAX, initial_values: Sequence | None = None):
+        if faulty is None:                       # start.ts:7-18 placement: the first F nodes
+            faulty = [i < F for i in range(N)]
+        self.N, self.F, self.k_max, self.seed = N, F, k_max, seed
+        self._fl = (ctypes.c_uint8 * max(1, N))(*[1 if v else 0 for v in faulty])
+        if initial_values is None:
+            self._init = (ctypes.c_int8 * max(1, N))()
+            mode = BO_INIT_RANDOM
+        else:
+            self._init = (ctypes.c_int8 * max(1, N))(*[_VAL[v] for v in initial_values])
+            mode = BO_INIT_FIXED
+        self._cfg = TrialsCfgC(N, F, k_max, mode, BO_MODE_LOCKSTEP, 0, seed,
+                               ctypes.cast(self._fl, ctypes.POINTER(ctypes.c_uint8)),
+                               ctypes.cast(self._init, ctypes.POINTER(ctypes.c_int8)))
+        h = ctypes.c_void_p()
+        _check(lib().bo_plan_create(ctypes.byref(self._cfg), ctypes.byref(h)))
+        self._h = h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and _lib is not None:
+            _lib.bo_plan_destroy(h)
+            self._h = None
+
+    @property
+    def live_nodes(self) -> int:
+        return lib().bo_plan_live_nodes(self._h)
+
+    @property
+    def popc_words_per_node_round(self) -> int:
+        return lib().bo_plan_popc_words_per_node_round(self._h)
+
+    @property
+    def hist_len(self) -> int:
+        return hist_len(self.k_max)
+
+    def launch(self, trial_begin: int, trial_count: int, hist_dev_ptr: int, stream_ptr: int = 0) -> None:
+        """Asynchronous; adds into the device histogram at hist_dev_ptr."""
+        _check(lib().bo_plan_launch(self._h, trial_begin, trial_count, ctypes.c_void_p(hist_dev_ptr),
+                                    ctypes.c_void_p(stream_ptr)))
+
+    def run(self, trial_begin: int, trial_count: int):
+        import numpy as np
+
+        h = np.zeros(self.hist_len, dtype=np.uint64)
+        _check(lib().bo_plan_run(self._h, trial_begin, trial_count,
+                                 h.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))))
+        return h
+
+
+def run_trial_states(N: int, F: int, faulty: Sequence[bool], *, seed: int = 0, trial: int = 0,
+                     k_max: int = DEFAULT_K_MAX, initial_values: Sequence | None = None):
+    """Per-node final states of one trial: (rounds, [NodeState dict] * N)."""
+    fl = (ctypes.c_uint8 * max(1, N))(*[1 if v else 0 for v in faulty])
+    if initial_values is None:
+        init = (ctypes.c_int8 * max(1, N))()
+        mode = BO_INIT_RANDOM
+    else:
+        init = (ctypes.c_int8 * max(1, N))(*[_VAL[v] for v in initial_values])
+        mode = BO_INIT_FIXED
+    cfg = TrialsCfgC(N, F, k_max, mode, BO_MODE_LOCKSTEP, 0, seed,
+                     ctypes.cast(fl, ctypes.POINTER(ctypes.c_uint8)),
+                     ctypes.cast(init, ctypes.POINTER(ctypes.c_int8)))
+    st = (NodeStateC * max(1, N))()
+    rounds = ctypes.c_uint32(0)
+    _check(lib().bo_run_trial_states(ctypes.byref(cfg), trial, st, ctypes.byref(rounds)))
+    return int(rounds.value), [_state_dict(st[i]) for i in range(N)]
+
+
+def popc_peak(iters: int = 20) -> float:
+    return float(lib().bo_popc_peak(iters))

@@ -1,0 +1,54 @@
+// benor_internal.h -- launch-side contract between the C-ABI runtime
+// (benor_runtime.cpp) and the gfx950 kernels (benor_kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "benor.h"
+
+namespace benor {
+
+// Philox counter-stream tags (top byte of counter word 3).  Must match
+// oracle/benor_oracle.c (the checker) -- DESIGN.md §3.
+constexpr uint32_t kStreamCoin = 0u;
+constexpr uint32_t kStreamInit = 1u;
+
+constexpr int kWavesPerBlock = 4;          // 256-thread workgroups, one trial per wave
+constexpr uint32_t kMaxW = BO_MAX_N / 64;  // u64 words per bit plane at N = 4096
+
+struct KParams {
+  uint32_t N, F;            // network size, fault parameter
+  uint32_t m;               // live (non-crashed) nodes = senders = receivers
+  uint32_t W;               // u64 words per plane = ceil(m / 64) = receiver groups
+  uint32_t G;               // receiver groups per tally block (template parameter)
+  uint32_t nblocks;         // ceil(W / G)
+  uint32_t k_max;
+  uint32_t init_mode;       // BO_INIT_RANDOM / BO_INIT_FIXED
+  uint32_t hist_len;        // (k_max + 1) * 3 + 1
+  uint32_t lds_bytes;       // dynamic LDS per workgroup
+  uint32_t wave_bytes;      // per-wave LDS region
+  uint32_t hist_bytes;      // LDS histogram bytes (16-aligned)
+  uint64_t seed;
+  uint64_t trial_begin;
+  uint64_t trial_count;
+  const uint32_t *live_ids;        // [m] compact index -> node id (device)
+  const uint4 *init_plane;         // [W] {X0lo, X0hi, X1lo, X1hi} (device; fixed init)
+  unsigned long long *hist;        // [hist_len] (device, accumulated)
+  bo_node_state *node_out;         // [N] (device) or nullptr; only with trial_count == 1
+  uint32_t *rounds_out;            // (device) or nullptr
+};
+
+// Pick the tally block size G and fill nblocks / LDS sizes.
+void plan_geometry(KParams &p);
+
+hipError_t launch_lockstep(const KParams &p, int grid_blocks, hipStream_t stream);
+
+// Grid size that fills the current device for this configuration.
+int lockstep_grid(const KParams &p, int device);
+
+// v_bcnt_u32_b32 microbenchmark: popcount words executed per launch.
+hipError_t launch_popc_peak(uint32_t *sink, int grid_blocks, int iters, hipStream_t stream,
+                            double *words_per_launch);
+
+}  // namespace benor

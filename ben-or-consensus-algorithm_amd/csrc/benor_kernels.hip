@@ -1,0 +1,341 @@
+// benor_kernels.hip -- gfx950 (MI355X) kernels for the Ben-Or round loop.
+//
+// Replaces the reference's per-node POST /message handler
+// (viviendbk/ben-or-consensus-algorithm src/nodes/node.ts:43-163) for a batch
+// of independent trials.  Design:
+//
+//   * one wave64 = one trial (a whole simulated network), so the
+//     all-to-all message exchange of a phase never leaves the wave: there are
+//     no barriers, no inter-wave traffic and no HBM traffic in the round loop;
+//   * lane l of receiver group j is live node c = 64 j + l (compact order of
+//     live node ids); crashed nodes (node.ts:45,171) own no lane and no bit;
+//   * a phase's messages are two bit planes over the m live senders,
+//     {is0, is1}, produced by wave ballots and kept in the wave's LDS slice as
+//     16-byte records {is0.lo, is0.hi, is1.lo, is1.hi} per 64 senders;
+//   * every live receiver tallies its own inbox with v_bcnt_u32_b32
+//     (popcount + accumulate, one VALU op per 32 senders per count), reading
+//     each record once per wave with a broadcast ds_read_b128 and applying it
+//     to G receiver groups per lane;
+//   * per-node coins (node.ts:111) and random initial values come from
+//     Philox4x32-10 keyed by (seed, global trial id, node id, round);
+//   * each trial's outcome is one increment of an LDS histogram, flushed to
+//     HBM with one atomic per non-zero bin per workgroup.
+//
+// Per-receiver tallies are the simulated unit (SURVEY §7 "symmetry trap"):
+// in lockstep mode all receivers of a trial see the same inbox, so a compiler
+// would legitimately merge their identical popcounts.  The tally is therefore
+// an opaque `v_bcnt_u32_b32` and each receiver group's chain starts from a
+// distinct constant (subtracted afterwards) so that every live node's count is
+// executed by its own lane, as the reference executes it in its own handler.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "benor_internal.h"
+
+namespace benor {
+
+// ------------------------------------------------------------------ Philox
+__device__ __forceinline__ uint4 philox4x32_10(uint32_t k0, uint32_t k1, uint4 c) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t lo0 = 0xD2511F53u * c.x;
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c.x);
+    const uint32_t lo1 = 0xCD9E8D57u * c.z;
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z);
+    c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// One receiver's tally step: acc + popcount(word).  Opaque on purpose (see
+// the header comment): the per-receiver count must execute per receiver.
+__device__ __forceinline__ uint32_t tally(uint32_t word, uint32_t acc) {
+  uint32_t r;
+  asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(word), "v"(acc));
+  return r;
+}
+
+__device__ __forceinline__ uint64_t group_mask(uint32_t j, uint32_t m) {
+  const uint32_t lo = j * 64u;
+  if (lo >= m) return 0ull;
+  const uint32_t n = m - lo;
+  return n >= 64u ? ~0ull : ((1ull << n) - 1ull);
+}
+
+__device__ __forceinline__ uint4 rec(uint64_t is0, uint64_t is1) {
+  return make_uint4((uint32_t)is0, (uint32_t)(is0 >> 32), (uint32_t)is1, (uint32_t)(is1 >> 32));
+}
+
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+
+// Tally of one block of G receiver groups against a plane of W records.
+// a0[g] / a1[g] receive the counts of 0s / 1s (node.ts:56-62, :92-98).
+template <int G>
+__device__ __forceinline__ void tally_block(const uint4 *__restrict__ plane, uint32_t W,
+                                            uint32_t (&a0)[G], uint32_t (&a1)[G]) {
+#pragma unroll
+  for (int g = 0; g < G; ++g) { a0[g] = (uint32_t)g; a1[g] = (uint32_t)g; }
+  uint32_t w = 0;
+  for (; w + 1 < W; w += 2) {
+    const uint4 q = plane[w];
+    const uint4 s = plane[w + 1];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      a0[g] = tally(q.x, a0[g]);
+      a1[g] = tally(q.z, a1[g]);
+      a0[g] = tally(q.y, a0[g]);
+      a1[g] = tally(q.w, a1[g]);
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      a0[g] = tally(s.x, a0[g]);
+      a1[g] = tally(s.z, a1[g]);
+      a0[g] = tally(s.y, a0[g]);
+      a1[g] = tally(s.w, a1[g]);
+    }
+  }
+  if (w < W) {
+    const uint4 q = plane[w];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      a0[g] = tally(q.x, a0[g]);
+      a1[g] = tally(q.z, a1[g]);
+      a0[g] = tally(q.y, a0[g]);
+      a1[g] = tally(q.w, a1[g]);
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < G; ++g) { a0[g] -= (uint32_t)g; a1[g] -= (uint32_t)g; }
+}
+
+// ------------------------------------------------------------ the kernel
+template <int G>
+__global__ void __launch_bounds__(256) benor_lockstep_kernel(KParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = threadIdx.x >> 6;
+  const uint32_t W = p.W, m = p.m, F = p.F;
+
+  uint32_t *lhist = reinterpret_cast<uint32_t *>(smem);
+  unsigned char *wbase = smem + p.hist_bytes + wv * p.wave_bytes;
+  uint4 *X = reinterpret_cast<uint4 *>(wbase);          // x planes      [W]
+  uint4 *P = X + W;                                      // proposal planes [W]
+  uint32_t *D = reinterpret_cast<uint32_t *>(P + W);    // decided bits  [nblocks][64]
+
+  for (uint32_t i = threadIdx.x; i < p.hist_len; i += blockDim.x) lhist[i] = 0u;
+  __syncthreads();
+
+  const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
+  const uint64_t waves_total = (uint64_t)gridDim.x * kWavesPerBlock;
+  const uint32_t nb = p.nblocks;
+
+  for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + wv; t < p.trial_count; t += waves_total) {
+    const uint64_t trial = p.trial_begin + t;
+    const uint32_t tlo = (uint32_t)trial, thi = (uint32_t)(trial >> 32);
+
+    // ---- /start (node.ts:167-188): round-1 x planes of the live nodes.
+    if (p.init_mode == BO_INIT_RANDOM) {
+      const uint32_t nphil = (W + 1u) >> 1;   // one Philox block = two u64 plane words
+      if (lane < nphil) {
+        const uint4 r = philox4x32_10(k0, k1, make_uint4(tlo, thi, lane, kStreamInit << 24));
+        const uint32_t w0 = 2u * lane, w1 = w0 + 1u;
+        const uint64_t v0 = group_mask(w0, m), v1 = group_mask(w1, m);
+        const uint64_t x1a = ((uint64_t)r.y << 32 | r.x) & v0;
+        X[w0] = rec(v0 & ~x1a, x1a);
+        if (w1 < W) {
+          const uint64_t x1b = ((uint64_t)r.w << 32 | r.z) & v1;
+          X[w1] = rec(v1 & ~x1b, x1b);
+        }
+      }
+    } else {
+      for (uint32_t w = lane; w < W; w += 64u) X[w] = p.init_plane[w];
+    }
+    for (uint32_t b = 0; b < nb; ++b) D[b * 64u + lane] = 0u;
+
+    uint32_t R = 0;
+    bool all_dec = false;
+    for (uint32_t r = 1; r <= p.k_max; ++r) {
+      // ---- R-phase ("proposal phase", node.ts:46-82): tally x, propose.
+      for (uint32_t b = 0; b < nb; ++b) {
+        uint32_t a0[G], a1[G];
+        tally_block<G>(X, W, a0, a1);
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const uint32_t j = b * G + g;
+          if (j < W) {
+            const uint64_t vm = group_mask(j, m);
+            const uint64_t p0 = ballot(a0[g] > a1[g]) & vm;   // node.ts:63-64
+            const uint64_t p1 = ballot(a1[g] > a0[g]) & vm;   // node.ts:65-66 (else "?")
+            if (lane == 0) P[j] = rec(p0, p1);
+          }
+        }
+      }
+      // ---- P-phase ("voting phase", node.ts:83-158): tally proposals,
+      //      decide on > F, adopt the strict majority, else flip a coin.
+      bool lane_done = true;
+      for (uint32_t b = 0; b < nb; ++b) {
+        uint32_t a0[G], a1[G];
+        tally_block<G>(P, W, a0, a1);
+        uint32_t db = D[b * 64u + lane];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const uint32_t j = b * G + g;
+          if (j < W) {
+            const uint64_t vm = group_mask(j, m);
+            const bool d0l = a0[g] > F;                          // node.ts:99
+            const bool d1l = a1[g] > F;                          // node.ts:102
+            const uint64_t d0 = ballot(d0l) & vm;
+            const uint64_t d1 = ballot(d1l) & vm & ~d0;
+            const uint64_t rest = vm & ~(d0 | d1);
+            const uint64_t ad0 = ballot(a0[g] > a1[g]) & rest;   // node.ts:106-107
+            const uint64_t ad1 = ballot(a1[g] > a0[g]) & rest;   // node.ts:108-109
+            const uint64_t tie = rest & ~(ad0 | ad1);
+            uint64_t x1 = d1 | ad1;
+            if (tie) {                                           // node.ts:111
+              bool c1 = false;
+              if ((tie >> lane) & 1ull) {
+                const uint32_t node = p.live_ids[j * 64u + lane];
+                const uint4 rr = philox4x32_10(k0, k1, make_uint4(tlo, thi, node, (r & 0x00FFFFFFu) | (kStreamCoin << 24)));
+                c1 = !(rr.x > 0x80000000u);                      // Math.random() > 0.5 ? 0 : 1
+              }
+              x1 |= ballot(c1) & tie;
+            }
+            if (lane == 0) X[j] = rec(vm & ~x1, x1);
+            if (d0l || d1l) db |= (1u << g);
+            const bool valid = (j * 64u + lane) < m;
+            lane_done = lane_done && (!valid || ((db >> g) & 1u));
+          }
+        }
+        D[b * 64u + lane] = db;
+      }
+      R = r;                                                    // node.ts:147  k = r + 1
+      all_dec = __all(lane_done);                               // all-decided auto-stop (node.ts:116-145)
+      if (all_dec) break;
+    }
+
+    // ---- outcome: common final x (agreement check) and histogram bin.
+    bool any0 = false, any1 = false;
+    for (uint32_t w = lane; w < W; w += 64u) {
+      const uint4 q = X[w];
+      any0 = any0 || ((q.x | q.y) != 0u);
+      any1 = any1 || ((q.z | q.w) != 0u);
+    }
+    const bool g0 = __any(any0), g1 = __any(any1);
+    const uint32_t v = (g0 && g1) ? 2u : (g1 ? 1u : 0u);
+    if (lane == 0) {
+      const uint32_t bin = all_dec ? (R * 3u + v) : v;
+      atomicAdd(&lhist[bin], 1u);
+      if (all_dec && v == 2u) atomicAdd(&lhist[p.hist_len - 1u], 1u);
+      if (p.rounds_out) *p.rounds_out = all_dec ? R : 0u;
+    }
+    if (p.node_out) {                                           // GET /getState (node.ts:197-199)
+      for (uint32_t c = lane; c < m; c += 64u) {
+        const uint4 q = X[c >> 6];
+        const uint64_t x1 = (uint64_t)q.w << 32 | q.z;
+        const uint32_t db = D[((c >> 6) / G) * 64u + (c & 63u)];
+        bo_node_state s;
+        s.killed = 0;
+        s.x = (int8_t)((x1 >> (c & 63u)) & 1ull);
+        s.decided = (int8_t)((db >> ((c >> 6) % G)) & 1u);
+        s.pad = 0;
+        s.k = (int32_t)R + 1;
+        p.node_out[p.live_ids[c]] = s;
+      }
+    }
+  }
+
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < p.hist_len; i += blockDim.x) {
+    const uint32_t c = lhist[i];
+    if (c) atomicAdd(&p.hist[i], (unsigned long long)c);
+  }
+}
+
+// --------------------------------------------------- popcount peak probe
+// Eight independent v_bcnt_u32_b32 chains per lane; the roofline's `peak`
+// is the spec VALU rate, this probe says what the part sustains.
+__global__ void __launch_bounds__(256) popc_peak_kernel(uint32_t *sink, int iters) {
+  uint32_t a[8];
+  const uint32_t x = threadIdx.x * 2654435761u + blockIdx.x;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[i] = x + (uint32_t)i;
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) asm volatile("v_bcnt_u32_b32 %0, %1, %0" : "+v"(a[i]) : "v"(x));
+    }
+  }
+  uint32_t s = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s ^= a[i];
+  if (s == 0x12345678u) sink[blockIdx.x] = s;
+}
+
+// ------------------------------------------------------------ host side
+void plan_geometry(KParams &p) {
+  const uint32_t W = p.W;
+  const uint32_t nb = (W + 15u) / 16u;           // blocks of at most 16 groups
+  const uint32_t G = (W + nb - 1u) / nb;         // balanced: padding < nb groups
+  p.G = G;
+  p.nblocks = (W + G - 1u) / G;
+  p.hist_len = (p.k_max + 1u) * 3u + 1u;
+  p.hist_bytes = ((p.hist_len * 4u) + 15u) & ~15u;
+  p.wave_bytes = W * 32u + p.nblocks * 256u;
+  p.lds_bytes = p.hist_bytes + kWavesPerBlock * p.wave_bytes;
+}
+
+template <int G>
+static hipError_t launch_g(const KParams &p, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(benor_lockstep_kernel<G>, dim3(grid), dim3(64 * kWavesPerBlock), p.lds_bytes, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_lockstep(const KParams &p, int grid, hipStream_t s) {
+  switch (p.G) {
+    case 1: return launch_g<1>(p, grid, s);
+    case 2: return launch_g<2>(p, grid, s);
+    case 3: return launch_g<3>(p, grid, s);
+    case 4: return launch_g<4>(p, grid, s);
+    case 5: return launch_g<5>(p, grid, s);
+    case 6: return launch_g<6>(p, grid, s);
+    case 7: return launch_g<7>(p, grid, s);
+    case 8: return launch_g<8>(p, grid, s);
+    case 9: return launch_g<9>(p, grid, s);
+    case 10: return launch_g<10>(p, grid, s);
+    case 11: return launch_g<11>(p, grid, s);
+    case 12: return launch_g<12>(p, grid, s);
+    case 13: return launch_g<13>(p, grid, s);
+    case 14: return launch_g<14>(p, grid, s);
+    case 15: return launch_g<15>(p, grid, s);
+    case 16: return launch_g<16>(p, grid, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+int lockstep_grid(const KParams &p, int device) {
+  int cus = 256;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+  // 8 workgroups (32 waves) per CU when registers and LDS allow it.
+  const uint64_t waves_needed = p.trial_count;
+  const uint64_t blocks_needed = (waves_needed + kWavesPerBlock - 1) / kWavesPerBlock;
+  uint64_t per_cu = 8;
+  if (p.lds_bytes > 0) {
+    const uint64_t lds_fit = (160u * 1024u) / p.lds_bytes;
+    if (lds_fit < per_cu) per_cu = lds_fit ? lds_fit : 1;
+  }
+  uint64_t grid = (uint64_t)cus * per_cu;
+  if (blocks_needed < grid) grid = blocks_needed;
+  if (grid < 1) grid = 1;
+  return (int)grid;
+}
+
+hipError_t launch_popc_peak(uint32_t *sink, int grid, int iters, hipStream_t s, double *words) {
+  hipLaunchKernelGGL(popc_peak_kernel, dim3(grid), dim3(256), 0, s, sink, iters);
+  if (words) *words = (double)grid * 256.0 * (double)iters * 64.0;
+  return hipGetLastError();
+}
+
+}  // namespace benor

@@ -1,0 +1,384 @@
+// benor_runtime.cpp -- C ABI (include/benor.h) over the gfx950 kernels.
+//
+// Host-side mirror of the reference's network layer:
+//   launchNetwork / launchNodes   src/index.ts:4-14, src/nodes/launchNodes.ts:4-44
+//   startConsensus / stopConsensus src/nodes/consensus.ts:3-15
+//   GET /status, /start, /stop, /getState   src/nodes/node.ts:33-39, :167-199
+// The POST /message round loop (node.ts:43-163) runs on the device
+// (benor_kernels.hip).  There is no CPU fallback: without a gfx950 device
+// every compute entry point returns BO_ERR_NO_DEVICE.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "benor.h"
+#include "benor_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+  g_err = msg;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char *what) {
+  g_err = std::string(what) + ": " + hipGetErrorString(e);
+  return BO_ERR_HIP;
+}
+
+#define HIP_TRY(expr)                                  \
+  do {                                                 \
+    hipError_t e_ = (expr);                            \
+    if (e_ != hipSuccess) return hip_fail(e_, #expr);  \
+  } while (0)
+
+// The product runs only on a gfx950 device.
+int check_device(int *dev_out) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+    return fail(BO_ERR_NO_DEVICE, "no HIP device visible (libbenor has no CPU fallback)");
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, dev));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(BO_ERR_NO_DEVICE, std::string("device is ") + prop.gcnArchName + ", libbenor targets gfx950");
+  if (dev_out) *dev_out = dev;
+  return BO_OK;
+}
+
+__global__ void add_bin_kernel(unsigned long long *hist, uint32_t bin, unsigned long long n) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) hist[bin] += n;
+}
+
+}  // namespace
+
+struct bo_network {
+  uint32_t N = 0, F = 0;
+  std::vector<bo_node_state> st;
+  std::vector<uint8_t> faulty;
+  uint64_t starts = 0;
+};
+
+struct bo_plan {
+  benor::KParams kp{};
+  bo_trials_cfg cfg{};
+  std::vector<uint32_t> live_ids;
+  uint32_t *d_live = nullptr;
+  uint4 *d_init = nullptr;
+  int device = 0;
+};
+
+extern "C" {
+
+const char *bo_last_error(void) { return g_err.c_str(); }
+int bo_abi_version(void) { return BENOR_ABI_VERSION; }
+uint32_t bo_hist_len(uint32_t k_max) { return (k_max + 1u) * 3u + 1u; }
+
+// ------------------------------------------------------------ network API
+int bo_network_create(uint32_t N, uint32_t F, const int8_t *init, uint32_t n_init,
+                      const uint8_t *faulty, uint32_t n_faulty, bo_network **out) {
+  if (!out) return fail(BO_ERR_INVALID_ARGUMENT, "out is NULL");
+  *out = nullptr;
+  // launchNodes.ts:10-11
+  if (n_init != n_faulty || N != n_init) return fail(BO_ERR_ARRAYS_DONT_MATCH, "Arrays don't match");
+  uint32_t cnt = 0;
+  for (uint32_t i = 0; i < n_faulty; ++i) cnt += faulty[i] ? 1u : 0u;
+  // launchNodes.ts:12-13
+  if (cnt != F) return fail(BO_ERR_FAULTY_COUNT, "faultyList doesnt have F faulties");
+  if (N > BO_MAX_N) return fail(BO_ERR_UNSUPPORTED, "N exceeds BO_MAX_N");
+  for (uint32_t i = 0; i < N; ++i)
+    if (init[i] < 0 || init[i] > 2) return fail(BO_ERR_INVALID_ARGUMENT, "initial value must be 0, 1 or '?'(2)");
+  auto *net = new bo_network();
+  net->N = N;
+  net->F = F;
+  net->st.resize(N);
+  net->faulty.assign(faulty, faulty + N);
+  for (uint32_t i = 0; i < N; ++i) {   // node.ts:21-26
+    const bool f = faulty[i] != 0;
+    net->st[i].killed = f ? 1 : 0;
+    net->st[i].x = f ? -1 : init[i];
+    net->st[i].decided = f ? -1 : 0;
+    net->st[i].pad = 0;
+    net->st[i].k = f ? -1 : 0;
+  }
+  *out = net;
+  return BO_OK;
+}
+
+uint32_t bo_network_size(const bo_network *net) { return net ? net->N : 0u; }
+
+void bo_network_destroy(bo_network *net) { delete net; }
+
+int bo_status(const bo_network *net, uint32_t i) {   // node.ts:33-39
+  if (!net) return -fail(BO_ERR_INVALID_ARGUMENT, "net is NULL");
+  if (i >= net->N) return -fail(BO_ERR_OUT_OF_RANGE, "node index out of range");
+  return net->st[i].killed ? 500 : 200;
+}
+
+int bo_get_state(const bo_network *net, uint32_t i, bo_node_state *out) {   // node.ts:197-199
+  if (!net || !out) return fail(BO_ERR_INVALID_ARGUMENT, "NULL argument");
+  if (i >= net->N) return fail(BO_ERR_OUT_OF_RANGE, "node index out of range");
+  *out = net->st[i];
+  return BO_OK;
+}
+
+int bo_node_stop(bo_network *net, uint32_t i) {   // node.ts:191-194
+  if (!net) return fail(BO_ERR_INVALID_ARGUMENT, "net is NULL");
+  if (i >= net->N) return fail(BO_ERR_OUT_OF_RANGE, "node index out of range");
+  net->st[i].killed = 1;
+  return BO_OK;
+}
+
+int bo_consensus_stop(bo_network *net) {   // consensus.ts:10-15
+  if (!net) return fail(BO_ERR_INVALID_ARGUMENT, "net is NULL");
+  for (auto &s : net->st) s.killed = 1;
+  return BO_OK;
+}
+
+int bo_consensus_start(bo_network *net, uint64_t seed, uint32_t k_max) {   // consensus.ts:3-8
+  if (!net) return fail(BO_ERR_INVALID_ARGUMENT, "net is NULL");
+  if (k_max < 1 || k_max > BO_MAX_K) return fail(BO_ERR_INVALID_ARGUMENT, "k_max out of range");
+  const uint32_t N = net->N;
+  // Nodes that run: not killed (faulty from launch, or stopped).  They send
+  // and receive; killed nodes do neither (node.ts:45, :171).
+  std::vector<uint32_t> active;
+  for (uint32_t i = 0; i < N; ++i)
+    if (!net->st[i].killed) active.push_back(i);
+  const uint64_t trial = net->starts++;
+  if (active.empty()) return BO_OK;
+  for (uint32_t i : active) net->st[i].k = 1;   // node.ts:172
+  const int64_t quorum = (int64_t)N - (int64_t)net->F;
+  // Fewer running senders than the quorum: no R-phase ever triggers
+  // (node.ts:52), every running node stays at k = 1, undecided.
+  if ((int64_t)active.size() < quorum) return BO_OK;
+  int dev = 0;
+  int rc = check_device(&dev);
+  if (rc) return rc;
+
+  bo_trials_cfg cfg{};
+  cfg.N = N;
+  cfg.F = net->F;
+  cfg.k_max = k_max;
+  cfg.init_mode = BO_INIT_FIXED;
+  cfg.mode = BO_MODE_LOCKSTEP;
+  cfg.seed = seed;
+  std::vector<uint8_t> crashed(N);
+  std::vector<int8_t> x(N);
+  for (uint32_t i = 0; i < N; ++i) {
+    crashed[i] = net->st[i].killed ? 1 : 0;
+    x[i] = net->st[i].killed ? 0 : net->st[i].x;
+  }
+  cfg.faulty = crashed.data();
+  cfg.init = x.data();
+  // Launch-time validation is already done; here the crashed set is the
+  // killed set, which has exactly N - quorum = F members at this point.
+  std::vector<bo_node_state> states(N);
+  uint32_t rounds = 0;
+  rc = bo_run_trial_states(&cfg, trial, states.data(), &rounds);
+  if (rc) return rc;
+  for (uint32_t i : active) net->st[i] = states[i];
+  return BO_OK;
+}
+
+// -------------------------------------------------------------- batch API
+int bo_plan_create(const bo_trials_cfg *cfg, bo_plan **out) {
+  if (!cfg || !out) return fail(BO_ERR_INVALID_ARGUMENT, "NULL argument");
+  *out = nullptr;
+  if (cfg->N < 1 || cfg->N > BO_MAX_N) return fail(BO_ERR_UNSUPPORTED, "N must be in [1, 4096]");
+  if (cfg->k_max < 1 || cfg->k_max > BO_MAX_K) return fail(BO_ERR_INVALID_ARGUMENT, "k_max must be in [1, 1024]");
+  if (cfg->mode != BO_MODE_LOCKSTEP) return fail(BO_ERR_UNSUPPORTED, "unknown delivery mode");
+  if (cfg->init_mode != BO_INIT_RANDOM && cfg->init_mode != BO_INIT_FIXED)
+    return fail(BO_ERR_INVALID_ARGUMENT, "unknown init_mode");
+  if (!cfg->faulty) return fail(BO_ERR_INVALID_ARGUMENT, "faulty is NULL");
+  if (cfg->init_mode == BO_INIT_FIXED && !cfg->init) return fail(BO_ERR_INVALID_ARGUMENT, "init is NULL");
+  uint32_t f = 0;
+  for (uint32_t i = 0; i < cfg->N; ++i) f += cfg->faulty[i] ? 1u : 0u;
+  // Lockstep = the reference's admissible inputs: exactly F crash faults
+  // (launchNodes.ts:12-13).
+  if (f != cfg->F) return fail(BO_ERR_FAULTY_COUNT, "faultyList doesnt have F faulties");
+  int dev = 0;
+  int rc = check_device(&dev);
+  if (rc) return rc;
+
+  auto *pl = new bo_plan();
+  pl->cfg = *cfg;
+  pl->cfg.faulty = nullptr;
+  pl->cfg.init = nullptr;
+  pl->device = dev;
+  for (uint32_t i = 0; i < cfg->N; ++i)
+    if (!cfg->faulty[i]) pl->live_ids.push_back(i);
+  const uint32_t m = (uint32_t)pl->live_ids.size();
+  benor::KParams &kp = pl->kp;
+  kp.N = cfg->N;
+  kp.F = cfg->F;
+  kp.m = m;
+  kp.W = (m + 63u) / 64u;
+  kp.k_max = cfg->k_max;
+  kp.init_mode = cfg->init_mode;
+  kp.seed = cfg->seed;
+  if (m > 0) {
+    benor::plan_geometry(kp);
+    std::vector<uint4> plane(kp.W, make_uint4(0, 0, 0, 0));
+    if (cfg->init_mode == BO_INIT_FIXED) {
+      for (uint32_t c = 0; c < m; ++c) {
+        const int8_t v = cfg->init[pl->live_ids[c]];
+        if (v < 0 || v > 2) { delete pl; return fail(BO_ERR_INVALID_ARGUMENT, "initial value must be 0, 1 or '?'(2)"); }
+        const uint32_t w = c >> 6, b = c & 63u;
+        uint32_t *r = reinterpret_cast<uint32_t *>(&plane[w]);
+        if (v == 0) r[b >> 5] |= 1u << (b & 31u);
+        if (v == 1) r[2 + (b >> 5)] |= 1u << (b & 31u);
+      }
+    }
+    hipError_t e = hipMalloc(&pl->d_live, sizeof(uint32_t) * m);
+    if (e == hipSuccess) e = hipMalloc(&pl->d_init, sizeof(uint4) * kp.W);
+    if (e == hipSuccess) e = hipMemcpy(pl->d_live, pl->live_ids.data(), sizeof(uint32_t) * m, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(pl->d_init, plane.data(), sizeof(uint4) * kp.W, hipMemcpyHostToDevice);
+    if (e != hipSuccess) { bo_plan_destroy(pl); return hip_fail(e, "plan upload"); }
+    kp.live_ids = pl->d_live;
+    kp.init_plane = pl->d_init;
+  } else {
+    kp.hist_len = bo_hist_len(cfg->k_max);
+  }
+  *out = pl;
+  return BO_OK;
+}
+
+void bo_plan_destroy(bo_plan *pl) {
+  if (!pl) return;
+  if (pl->d_live) (void)hipFree(pl->d_live);
+  if (pl->d_init) (void)hipFree(pl->d_init);
+  delete pl;
+}
+
+uint32_t bo_plan_live_nodes(const bo_plan *pl) { return pl ? pl->kp.m : 0u; }
+
+uint64_t bo_plan_popc_words_per_node_round(const bo_plan *pl) {
+  if (!pl) return 0;
+  return 4ull * ((pl->kp.m + 31ull) / 32ull);
+}
+
+static int plan_launch_impl(bo_plan *pl, uint64_t trial_begin, uint64_t trial_count, uint64_t *hist_dev,
+                            bo_node_state *node_out, uint32_t *rounds_out, hipStream_t s) {
+  if (trial_count == 0) return BO_OK;
+  benor::KParams kp = pl->kp;
+  if (kp.m == 0) {   // no live node: every trial lands in bin (0, 2)
+    hipLaunchKernelGGL(add_bin_kernel, dim3(1), dim3(64), 0, s,
+                       reinterpret_cast<unsigned long long *>(hist_dev), 2u, (unsigned long long)trial_count);
+    HIP_TRY(hipGetLastError());
+    return BO_OK;
+  }
+  kp.trial_begin = trial_begin;
+  kp.trial_count = trial_count;
+  kp.hist = reinterpret_cast<unsigned long long *>(hist_dev);
+  kp.node_out = node_out;
+  kp.rounds_out = rounds_out;
+  const int grid = benor::lockstep_grid(kp, pl->device);
+  HIP_TRY(benor::launch_lockstep(kp, grid, s));
+  return BO_OK;
+}
+
+int bo_plan_launch(bo_plan *pl, uint64_t trial_begin, uint64_t trial_count, uint64_t *hist_dev, void *stream) {
+  if (!pl || !hist_dev) return fail(BO_ERR_INVALID_ARGUMENT, "NULL argument");
+  return plan_launch_impl(pl, trial_begin, trial_count, hist_dev, nullptr, nullptr,
+                          reinterpret_cast<hipStream_t>(stream));
+}
+
+int bo_plan_run(bo_plan *pl, uint64_t trial_begin, uint64_t trial_count, uint64_t *hist_host) {
+  if (!pl || !hist_host) return fail(BO_ERR_INVALID_ARGUMENT, "NULL argument");
+  const uint32_t H = bo_hist_len(pl->cfg.k_max);
+  uint64_t *d = nullptr;
+  HIP_TRY(hipMalloc(&d, sizeof(uint64_t) * H));
+  hipError_t e = hipMemset(d, 0, sizeof(uint64_t) * H);
+  int rc = BO_OK;
+  if (e == hipSuccess) rc = plan_launch_impl(pl, trial_begin, trial_count, d, nullptr, nullptr, nullptr);
+  std::vector<uint64_t> h(H);
+  if (e == hipSuccess && rc == BO_OK) e = hipMemcpy(h.data(), d, sizeof(uint64_t) * H, hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (e != hipSuccess) return hip_fail(e, "bo_plan_run");
+  if (rc) return rc;
+  for (uint32_t i = 0; i < H; ++i) hist_host[i] += h[i];
+  return BO_OK;
+}
+
+int bo_run_trials(const bo_trials_cfg *cfg, uint64_t trial_begin, uint64_t trial_count, uint64_t *hist_host) {
+  bo_plan *pl = nullptr;
+  int rc = bo_plan_create(cfg, &pl);
+  if (rc) return rc;
+  rc = bo_plan_run(pl, trial_begin, trial_count, hist_host);
+  bo_plan_destroy(pl);
+  return rc;
+}
+
+int bo_run_trial_states(const bo_trials_cfg *cfg, uint64_t trial, bo_node_state *nodes_out, uint32_t *rounds_out) {
+  if (!cfg || !nodes_out) return fail(BO_ERR_INVALID_ARGUMENT, "NULL argument");
+  bo_plan *pl = nullptr;
+  int rc = bo_plan_create(cfg, &pl);
+  if (rc) return rc;
+  const uint32_t N = cfg->N, H = bo_hist_len(cfg->k_max);
+  // Host-side initial states (node.ts:21-26); live entries are overwritten
+  // by the kernel.
+  std::vector<bo_node_state> st(N);
+  for (uint32_t i = 0; i < N; ++i) {
+    const bool f = cfg->faulty[i] != 0;
+    st[i].killed = f ? 1 : 0;
+    st[i].x = f ? -1 : (cfg->init_mode == BO_INIT_FIXED ? cfg->init[i] : -1);
+    st[i].decided = f ? -1 : 0;
+    st[i].pad = 0;
+    st[i].k = f ? -1 : 0;
+  }
+  bo_node_state *d_st = nullptr;
+  uint64_t *d_h = nullptr;
+  uint32_t *d_r = nullptr;
+  hipError_t e = hipMalloc(&d_st, sizeof(bo_node_state) * N);
+  if (e == hipSuccess) e = hipMalloc(&d_h, sizeof(uint64_t) * H);
+  if (e == hipSuccess) e = hipMalloc(&d_r, sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemcpy(d_st, st.data(), sizeof(bo_node_state) * N, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemset(d_h, 0, sizeof(uint64_t) * H);
+  if (e == hipSuccess) e = hipMemset(d_r, 0, sizeof(uint32_t));
+  if (e == hipSuccess) rc = plan_launch_impl(pl, trial, 1, d_h, d_st, d_r, nullptr);
+  uint32_t rounds = 0;
+  if (e == hipSuccess && rc == BO_OK) e = hipMemcpy(nodes_out, d_st, sizeof(bo_node_state) * N, hipMemcpyDeviceToHost);
+  if (e == hipSuccess && rc == BO_OK) e = hipMemcpy(&rounds, d_r, sizeof(uint32_t), hipMemcpyDeviceToHost);
+  if (d_st) (void)hipFree(d_st);
+  if (d_h) (void)hipFree(d_h);
+  if (d_r) (void)hipFree(d_r);
+  bo_plan_destroy(pl);
+  if (e != hipSuccess) return hip_fail(e, "bo_run_trial_states");
+  if (rc) return rc;
+  if (rounds_out) *rounds_out = rounds;
+  return BO_OK;
+}
+
+double bo_popc_peak(uint32_t iters) {
+  if (check_device(nullptr)) return 0.0;
+  int dev = 0, cus = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  uint32_t *sink = nullptr;
+  if (hipMalloc(&sink, sizeof(uint32_t) * cus * 8) != hipSuccess) return 0.0;
+  const int grid = cus * 8, inner = 2048;
+  double words = 0;
+  hipEvent_t a, b;
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  (void)benor::launch_popc_peak(sink, grid, inner, nullptr, &words);   // warm-up
+  (void)hipEventRecord(a, nullptr);
+  for (uint32_t i = 0; i < iters; ++i) (void)benor::launch_popc_peak(sink, grid, inner, nullptr, &words);
+  (void)hipEventRecord(b, nullptr);
+  (void)hipEventSynchronize(b);
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, a, b);
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  (void)hipFree(sink);
+  if (ms <= 0) return 0.0;
+  return words * iters / (ms * 1e-3);
+}
+
+}  // extern "C"

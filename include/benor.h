@@ -1,0 +1,170 @@
+/*
+ * benor.h -- C ABI of the MI355X-native Ben-Or consensus simulator (libbenor.so).
+ *
+ * This is the drop-in boundary for the reference's hot path
+ * (viviendbk/ben-or-consensus-algorithm, src/nodes/node.ts:43-163, the
+ * POST /message round loop).  Each entry point names the reference interface
+ * it replaces.  Plain C types only: pointers, sizes, integers.  No torch or
+ * HIP types appear in any signature; streams are passed as `void*`
+ * (a hipStream_t, NULL = default stream).
+ *
+ * Value encoding (src/types.ts:1-8, `Value = 0 | 1 | "?"`):
+ *     int8  0 -> 0,  1 -> 1,  2 -> "?",  -1 -> null (faulty node's x)
+ * `decided`: -1 -> null, 0 -> false, 1 -> true;  `k`: -1 -> null.
+ *
+ * Threading: every function may be called from any host thread, but calls on
+ * one bo_network handle must not overlap (the reference is single-threaded:
+ * one Node event loop).  bo_plan_launch is asynchronous on its stream; all
+ * other calls are synchronous.
+ */
+#ifndef BENOR_H
+#define BENOR_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BENOR_ABI_VERSION 1
+
+/* Return codes.  The first two are the reference's two launch errors. */
+enum {
+    BO_OK = 0,
+    BO_ERR_ARRAYS_DONT_MATCH = 1,   /* launchNodes.ts:10-11  Error("Arrays don't match") */
+    BO_ERR_FAULTY_COUNT = 2,        /* launchNodes.ts:12-13  Error("faultyList doesnt have F faulties") */
+    BO_ERR_INVALID_ARGUMENT = 3,
+    BO_ERR_NO_DEVICE = 4,           /* no gfx950 device visible: the product never falls back to CPU */
+    BO_ERR_HIP = 5,
+    BO_ERR_OUT_OF_RANGE = 6,        /* node index >= N */
+    BO_ERR_UNSUPPORTED = 7          /* configuration outside what this build simulates */
+};
+
+/* Delivery model.  LOCKSTEP is the reference's semantics for its admissible
+ * inputs (exactly F crash faults, launchNodes.ts:12-13): every live node
+ * receives every live node's message in every phase. */
+enum { BO_MODE_LOCKSTEP = 0 };
+
+enum { BO_INIT_RANDOM = 0, BO_INIT_FIXED = 1 };
+
+/* Largest network simulated per trial (N <= 4096 live + faulty nodes). */
+#define BO_MAX_N 4096u
+/* Largest round cap. */
+#define BO_MAX_K 1024u
+
+/* NodeState (src/types.ts:1-8), as served by GET /getState (node.ts:197-199). */
+typedef struct bo_node_state {
+    int8_t killed;    /* 0/1 */
+    int8_t x;         /* -1 null, 0, 1, 2 '?' */
+    int8_t decided;   /* -1 null, 0, 1 */
+    int8_t pad;
+    int32_t k;        /* -1 null */
+} bo_node_state;
+
+typedef struct bo_network bo_network;
+
+/* ---- network API: one simulated network, the reference's public surface ---- */
+
+/* launchNetwork(N, F, initialValues, faultyList)  (src/index.ts:4-14)
+ *   -> launchNodes (src/nodes/launchNodes.ts:4-44).
+ * Performs the reference's two validations in its order and returns their
+ * codes; on success *out owns host-side node state (node.ts:21-26):
+ * faulty -> {killed:1, x:null, decided:null, k:null}; live -> {0, init, 0, 0}.
+ * init values: 0, 1 or 2 ('?').  No GPU work happens here. */
+int bo_network_create(uint32_t N, uint32_t F,
+                      const int8_t *initial_values, uint32_t n_initial_values,
+                      const uint8_t *faulty_list, uint32_t n_faulty_list,
+                      bo_network **out);
+
+/* startConsensus(N)  (src/nodes/consensus.ts:3-8) -> GET /start on every node
+ * (node.ts:167-188), then the POST /message round loop (node.ts:43-163) until
+ * every live node has decided or k_max rounds ran -- one HIP kernel launch on
+ * the calling thread's current device, synchronous.  `seed` keys the
+ * per-node coins (node.ts:111).  Nodes already stopped act as crashed. */
+int bo_consensus_start(bo_network *net, uint64_t seed, uint32_t k_max);
+
+/* stopConsensus(N)  (consensus.ts:10-15) -> GET /stop on every node (node.ts:191-194). */
+int bo_consensus_stop(bo_network *net);
+
+/* GET /stop on one node (node.ts:191-194): killed = true. */
+int bo_node_stop(bo_network *net, uint32_t node);
+
+/* GET /getState (node.ts:197-199). */
+int bo_get_state(const bo_network *net, uint32_t node, bo_node_state *out);
+
+/* GET /status (node.ts:33-39): returns 500 ("faulty") or 200 ("live"), or a
+ * negative BO_ERR_* code. */
+int bo_status(const bo_network *net, uint32_t node);
+
+uint32_t bo_network_size(const bo_network *net);
+
+/* server.close() for every server (benorconsensus.test.ts:14-29). */
+void bo_network_destroy(bo_network *net);
+
+/* ---- batch API: many independent trials of one network shape ---- */
+
+typedef struct bo_trials_cfg {
+    uint32_t N, F;            /* network size; fault parameter (quorum N-F, decide on > F) */
+    uint32_t k_max;           /* round cap, 1..BO_MAX_K */
+    uint32_t init_mode;       /* BO_INIT_RANDOM: iid Bernoulli(1/2) per live node; BO_INIT_FIXED */
+    uint32_t mode;            /* BO_MODE_LOCKSTEP */
+    uint32_t reserved;
+    uint64_t seed;            /* Philox4x32-10 key */
+    const uint8_t *faulty;    /* host [N]; exactly F set in LOCKSTEP mode */
+    const int8_t *init;       /* host [N]; used when init_mode == BO_INIT_FIXED */
+} bo_trials_cfg;
+
+/* Histogram length for a round cap: (k_max + 1) * 3 + 1 uint64 bins.
+ *   bin[R*3 + v], 1 <= R <= k_max : every live node decided after round R, common x = v
+ *                                   (v = 2: decided values differ)
+ *   bin[0*3 + v]                  : not every live node decided within k_max rounds;
+ *                                   v = common x, or 2 if they differ
+ *   bin[(k_max+1)*3]              : trials whose decided values differ (agreement violations) */
+uint32_t bo_hist_len(uint32_t k_max);
+
+typedef struct bo_plan bo_plan;
+
+/* Validate a trial configuration and upload its tables to the current device. */
+int bo_plan_create(const bo_trials_cfg *cfg, bo_plan **out);
+
+/* Run global trial ids [trial_begin, trial_begin + trial_count) and ADD their
+ * outcomes into hist_dev (device pointer, bo_hist_len(k_max) uint64).
+ * Asynchronous on `stream` (hipStream_t or NULL). */
+int bo_plan_launch(bo_plan *plan, uint64_t trial_begin, uint64_t trial_count,
+                   uint64_t *hist_dev, void *stream);
+
+/* Same, blocking, host histogram (added into hist_host). */
+int bo_plan_run(bo_plan *plan, uint64_t trial_begin, uint64_t trial_count, uint64_t *hist_host);
+
+/* Work of one launch in the roofline's algorithmic unit: VALU popcount words
+ * that the per-receiver tallies of one live node-round need (2 phases x
+ * 2 counts x ceil(m/32) words, m = live nodes). */
+uint64_t bo_plan_popc_words_per_node_round(const bo_plan *plan);
+uint32_t bo_plan_live_nodes(const bo_plan *plan);
+
+void bo_plan_destroy(bo_plan *plan);
+
+/* One-shot convenience: create plan, run trial ids [trial_begin, +trial_count), destroy. */
+int bo_run_trials(const bo_trials_cfg *cfg, uint64_t trial_begin, uint64_t trial_count,
+                  uint64_t *hist_host);
+
+/* Per-node final states of one trial (trial id `trial`), nodes_out[N]. */
+int bo_run_trial_states(const bo_trials_cfg *cfg, uint64_t trial, bo_node_state *nodes_out,
+                        uint32_t *rounds_out);
+
+/* ---- diagnostics ---- */
+
+/* Time the v_bcnt_u32_b32 peak microbenchmark: returns popcount words/s
+ * measured on the current device over `iters` launches (0 on error). */
+double bo_popc_peak(uint32_t iters);
+
+/* Message of the last error on this thread ("" if none). */
+const char *bo_last_error(void);
+
+int bo_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BENOR_H */

@@ -1,0 +1,420 @@
+/*
+ * benor_oracle.c -- CPU restatement of the reference Ben-Or round loop.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load this library, and only as the checker
+ * (or as the timed CPU baseline).  The product path (libbenor.so) never links
+ * or calls anything in oracle/.
+ *
+ * Reference: viviendbk/ben-or-consensus-algorithm (TypeScript, Express).  The
+ * reference cannot be executed in this image (Node 12 has no global fetch and
+ * no optional chaining; express / ts-node / jest are absent, no network), so
+ * this file restates its algorithm in C.  Parity of this restatement is
+ * pinned by the reference's own known-answer tests
+ * (__test__/tests/benorconsensus.test.ts:133-486, fixtures in
+ * tests/golden/reference_cases.json) and by the exact analytic law of SURVEY
+ * §8c (oracle/analytic.py).
+ *
+ * Two restatements that cross-check each other:
+ *   (i)  oracle_message_sim  -- message-level: per-node inbox arrays keyed by
+ *        round, literal `>= N-F` triggers, seeded delivery order
+ *        (src/nodes/node.ts:43-163, :167-188, :191-194).
+ *   (ii) oracle_run_trials   -- round-level bit planes + popcount, the same
+ *        semantics the HIP kernel implements; also the timed CPU baseline.
+ *
+ * Shared conventions (identical in the HIP kernel):
+ *   Philox4x32-10, key = {seed_lo, seed_hi}.
+ *   coin(trial, node, round) = ctr {trial_lo, trial_hi, node, round | 0<<24},
+ *       word 0 = w; coin = (w > 0x80000000) ? 0 : 1, i.e. the reference's
+ *       `Math.random() > 0.5 ? 0 : 1` (node.ts:111) with u = w * 2^-32.
+ *   random initial value of the c-th live node (ascending node id):
+ *       bit (c & 31) of word c>>5, word j = philox(ctr {trial_lo, trial_hi,
+ *       j>>2, 1<<24})[j & 3].
+ *   halting: the network stops after the round in which every live node has
+ *       decided (the reference's all-decided auto-stop, node.ts:116-145,
+ *       without its F>0 `decided:null` defect), else after k_max rounds.
+ *       A live node's k is then (rounds run) + 1 (node.ts:147).
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define ORC_STREAM_COIN 0u
+#define ORC_STREAM_INIT 1u
+#define ORC_STREAM_ORDER 3u
+
+/* ---------------------------------------------------------------- Philox */
+/* Philox4x32-10 (Salmon et al., SC'11; Random123 reference constants). */
+static inline void orc_mulhilo(uint32_t a, uint32_t b, uint32_t *hi, uint32_t *lo) {
+    uint64_t p = (uint64_t)a * (uint64_t)b;
+    *hi = (uint32_t)(p >> 32);
+    *lo = (uint32_t)p;
+}
+
+void oracle_philox4x32_10(const uint32_t key_in[2], const uint32_t ctr_in[4], uint32_t out[4]) {
+    uint32_t k0 = key_in[0], k1 = key_in[1];
+    uint32_t c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
+    for (int r = 0; r < 10; ++r) {
+        uint32_t hi0, lo0, hi1, lo1;
+        orc_mulhilo(0xD2511F53u, c0, &hi0, &lo0);
+        orc_mulhilo(0xCD9E8D57u, c2, &hi1, &lo1);
+        uint32_t n0 = hi1 ^ c1 ^ k0;
+        uint32_t n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+static inline uint32_t orc_philox_word(uint64_t seed, uint64_t trial, uint32_t c2, uint32_t c3, int idx) {
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    uint32_t ctr[4] = {(uint32_t)trial, (uint32_t)(trial >> 32), c2, c3};
+    uint32_t out[4];
+    oracle_philox4x32_10(key, ctr, out);
+    return out[idx];
+}
+
+/* node.ts:111  `Math.random() > 0.5 ? 0 : 1` with u = w * 2^-32. */
+int oracle_coin(uint64_t seed, uint64_t trial, uint32_t node, uint32_t round) {
+    uint32_t w = orc_philox_word(seed, trial, node, (round & 0x00FFFFFFu) | (ORC_STREAM_COIN << 24), 0);
+    return (w > 0x80000000u) ? 0 : 1;
+}
+
+/* Random initial value (0/1) of the c-th live node. */
+int oracle_random_init(uint64_t seed, uint64_t trial, uint32_t c) {
+    uint32_t j = c >> 5;
+    uint32_t w = orc_philox_word(seed, trial, j >> 2, ORC_STREAM_INIT << 24, (int)(j & 3));
+    return (int)((w >> (c & 31)) & 1u);
+}
+
+/* ---------------------------------------------------- launch validation */
+/* launchNodes.ts:10-13.  Returns 0 ok, 1 "Arrays don't match",
+ * 2 "faultyList doesnt have F faulties". */
+int oracle_validate(int64_t N, int64_t F, int64_t n_init, int64_t n_faulty, const uint8_t *faulty) {
+    if (n_init != n_faulty || N != n_init) return 1;
+    int64_t cnt = 0;
+    for (int64_t i = 0; i < n_faulty; ++i) cnt += faulty[i] ? 1 : 0;
+    if (cnt != F) return 2;
+    return 0;
+}
+
+/* ------------------------------------------------------------ node state */
+/* NodeState (src/types.ts:1-8): x -1=null,0,1,2='?'; decided -1=null,0,1; k -1=null */
+typedef struct {
+    int8_t killed;
+    int8_t x;
+    int8_t decided;
+    int8_t pad;
+    int32_t k;
+} orc_node_state;
+
+/* ===================================================================== */
+/* (i) message-level restatement of node.ts:43-163                        */
+/* ===================================================================== */
+typedef struct { int32_t k; int8_t x; uint8_t phase; uint32_t to; } orc_msg;   /* {k, x, messageType} */
+typedef struct { int8_t *v; int32_t len, cap; } orc_vec;                       /* Value[] */
+
+static void vec_push(orc_vec *a, int8_t x) {
+    if (a->len == a->cap) {
+        a->cap = a->cap ? a->cap * 2 : 8;
+        a->v = (int8_t *)realloc(a->v, (size_t)a->cap);
+    }
+    a->v[a->len++] = x;
+}
+
+typedef struct { uint64_t s; } orc_rng;
+static inline uint64_t orc_splitmix(orc_rng *r) {
+    uint64_t z = (r->s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+/*
+ * One network run at message granularity.
+ *   init[i] in {0,1,2('?')}, faulty[i] in {0,1}; state_out[N].
+ *   order_mode 0: FIFO delivery; k >= 1: seeded uniformly random pick from
+ *   the pending pool (the "fixed seeded order" of the north star), k salts
+ *   the order stream.
+ * Returns rounds run R (>=0), or -1 if every live node decided is never
+ * reached within k_max (state then reflects k_max rounds).  *stalled is set
+ * when the pool drained without a halt (fewer than N-F live senders).
+ */
+int oracle_message_sim(uint32_t N, uint32_t F, const int8_t *init, const uint8_t *faulty,
+                       uint64_t seed, uint64_t trial, uint32_t k_max, int order_mode,
+                       orc_node_state *state_out, int *stalled) {
+    /* node.ts:21-26 */
+    orc_node_state *st = state_out;
+    uint32_t live = 0;
+    for (uint32_t i = 0; i < N; ++i) {
+        st[i].killed = faulty[i] ? 1 : 0;
+        st[i].x = faulty[i] ? -1 : init[i];
+        st[i].decided = faulty[i] ? -1 : 0;
+        st[i].k = faulty[i] ? -1 : 0;
+        st[i].pad = 0;
+        live += faulty[i] ? 0 : 1;
+    }
+    if (stalled) *stalled = 0;
+    const int64_t quorum = (int64_t)N - (int64_t)F;
+    const uint32_t KR = k_max + 2;
+    /* proposals / votes: Map<k, Value[]> per node (node.ts:29-30) */
+    orc_vec *prop = (orc_vec *)calloc((size_t)N * KR, sizeof(orc_vec));
+    orc_vec *vote = (orc_vec *)calloc((size_t)N * KR, sizeof(orc_vec));
+    uint8_t *pdone = (uint8_t *)calloc((size_t)N * KR, 1);   /* first P trigger seen */
+    uint32_t *completed = (uint32_t *)calloc(KR, sizeof(uint32_t));
+
+    size_t pcap = (size_t)N * N * 2 + 16, plen = 0;
+    orc_msg *pool = (orc_msg *)malloc(pcap * sizeof(orc_msg));
+    orc_rng rng;
+    rng.s = ((uint64_t)orc_philox_word(seed, trial, 0, ORC_STREAM_ORDER << 24, 0) << 32) |
+            orc_philox_word(seed, trial, 0, ORC_STREAM_ORDER << 24, 1);
+    rng.s ^= (uint64_t)order_mode * 0xD1B54A32D192ED03ull;   /* order_mode >= 1 salts the order */
+
+#define BCAST(KK, XX, PH)                                                        \
+    do {                                                                         \
+        for (uint32_t to_ = 0; to_ < N; ++to_) {                                 \
+            if (plen == pcap) { pcap *= 2; pool = (orc_msg *)realloc(pool, pcap * sizeof(orc_msg)); } \
+            pool[plen].k = (KK); pool[plen].x = (XX); pool[plen].phase = (PH);   \
+            pool[plen].to = to_; ++plen;                                         \
+        }                                                                        \
+    } while (0)
+
+    /* /start (node.ts:167-188), called for every node by startConsensus */
+    for (uint32_t i = 0; i < N; ++i) {
+        if (!st[i].killed) {
+            st[i].k = 1;
+            BCAST(1, st[i].x, 0);
+        }
+    }
+    int rounds = 0, halted = 0;
+    size_t head = 0;
+    while (!halted && head < plen) {
+        size_t pick;
+        if (order_mode >= 1) {
+            size_t avail = plen - head;
+            pick = head + (size_t)(orc_splitmix(&rng) % avail);
+            orc_msg t = pool[pick]; pool[pick] = pool[head]; pool[head] = t;
+        }
+        pick = head++;
+        orc_msg m = pool[pick];
+        uint32_t i = m.to;
+        if (st[i].killed) continue;                         /* node.ts:45 */
+        if (m.k < 0 || (uint32_t)m.k >= KR) continue;
+        if (m.phase == 0) {                                 /* "proposal phase" node.ts:46-82 */
+            orc_vec *a = &prop[(size_t)i * KR + (uint32_t)m.k];
+            vec_push(a, m.x);
+            if ((int64_t)a->len >= quorum) {
+                int c0 = 0, c1 = 0;
+                for (int32_t j = 0; j < a->len; ++j) {
+                    if (a->v[j] == 0) c0++;
+                    else if (a->v[j] == 1) c1++;
+                }
+                int8_t v = (c0 > c1) ? 0 : (c1 > c0) ? 1 : 2;
+                BCAST(m.k, v, 1);                           /* node.ts:72-80 */
+            }
+        } else {                                            /* "voting phase" node.ts:83-158 */
+            orc_vec *a = &vote[(size_t)i * KR + (uint32_t)m.k];
+            vec_push(a, m.x);
+            if ((int64_t)a->len >= quorum) {
+                int c0 = 0, c1 = 0;
+                for (int32_t j = 0; j < a->len; ++j) {
+                    if (a->v[j] == 0) c0++;
+                    else if (a->v[j] == 1) c1++;
+                }
+                if (c0 > (int)F) { st[i].x = 0; st[i].decided = 1; }
+                else if (c1 > (int)F) { st[i].x = 1; st[i].decided = 1; }
+                else {
+                    if (c0 + c1 > 0 && c0 > c1) st[i].x = 0;
+                    else if (c0 + c1 > 0 && c0 < c1) st[i].x = 1;
+                    else st[i].x = (int8_t)oracle_coin(seed, trial, i, (uint32_t)m.k);
+                }
+                st[i].k = m.k + 1;                          /* node.ts:147 */
+                uint8_t *pd = &pdone[(size_t)i * KR + (uint32_t)m.k];
+                int first = !*pd;
+                *pd = 1;
+                /* halting rule (all-decided auto-stop, node.ts:116-145): once
+                 * every live node has completed round k, stop if all decided
+                 * or k == k_max. */
+                if (first) {
+                    completed[m.k]++;
+                    if (completed[m.k] == live) {
+                        int all = 1;
+                        for (uint32_t j = 0; j < N; ++j)
+                            if (!faulty[j] && st[j].decided != 1) { all = 0; break; }
+                        rounds = m.k;
+                        if (all || (uint32_t)m.k >= k_max) { halted = all ? 2 : 1; break; }
+                    }
+                }
+                BCAST(m.k + 1, st[i].x, 0);                 /* node.ts:149-157 */
+            }
+        }
+    }
+#undef BCAST
+    if (!halted && stalled) *stalled = 1;
+    for (size_t j = 0; j < (size_t)N * KR; ++j) { free(prop[j].v); free(vote[j].v); }
+    free(prop); free(vote); free(pdone); free(completed); free(pool);
+    if (halted == 2) return rounds;
+    return -1;
+}
+
+/* ===================================================================== */
+/* (ii) round-level bit-plane restatement (same semantics as the kernel)  */
+/* ===================================================================== */
+typedef struct {
+    uint32_t N, F;            /* network size, fault parameter (quorum N-F, decide > F) */
+    uint32_t k_max;           /* round cap (>= 1) */
+    uint32_t init_mode;       /* 0 = random Bernoulli(1/2) per live node, 1 = fixed */
+    uint64_t seed;
+    uint64_t trial_begin;
+    uint64_t trial_count;
+    const uint8_t *faulty;    /* [N] crash-faulty (never send, never receive) */
+    const int8_t *init;       /* [N] 0/1/2('?'), used when init_mode == 1 */
+    int32_t threads;          /* <=0: all available */
+} orc_trials_cfg;
+
+static inline int popc64(uint64_t v) { return __builtin_popcountll(v); }
+
+/* Histogram layout (shared with the kernel):
+ *   hist[(R * 3) + v], R in [1, k_max]: all live decided after round R, common x = v (2 = differ)
+ *   hist[0 * 3 + v]: not all decided after k_max rounds; v = common x or 2
+ *   hist[(k_max + 1) * 3]: count of trials where all decided but values differ */
+static void run_one(const orc_trials_cfg *cfg, const uint32_t *live_ids, uint32_t m,
+                    uint64_t trial, uint64_t *x0, uint64_t *x1, uint64_t *p0, uint64_t *p1,
+                    uint64_t *dec, uint64_t *hist, orc_node_state *node_out) {
+    const uint32_t W = (m + 63) / 64;
+    const uint32_t F = cfg->F;
+    const int64_t quorum = (int64_t)cfg->N - (int64_t)cfg->F;
+    const size_t H = (size_t)(cfg->k_max + 1) * 3;
+    if (m == 0) { hist[2]++; return; }
+    /* initial planes (compact live order) */
+    for (uint32_t w = 0; w < W; ++w) { x0[w] = x1[w] = 0; dec[w] = 0; }
+    for (uint32_t c = 0; c < m; ++c) {
+        int v = cfg->init_mode == 1 ? cfg->init[live_ids[c]] : oracle_random_init(cfg->seed, trial, c);
+        if (v == 0) x0[c >> 6] |= 1ull << (c & 63);
+        else if (v == 1) x1[c >> 6] |= 1ull << (c & 63);
+        if (node_out) node_out[live_ids[c]].x = (int8_t)v;
+    }
+    if ((int64_t)m < quorum) {          /* fewer live senders than the quorum: no trigger ever fires */
+        if (node_out) {
+            for (uint32_t c = 0; c < m; ++c) { node_out[live_ids[c]].k = 1; }
+        }
+        hist[2]++;
+        return;
+    }
+    uint32_t R = 0;
+    int all_dec = 0;
+    for (uint32_t r = 1; r <= cfg->k_max; ++r) {
+        /* R-phase (node.ts:52-69): every live receiver tallies all m live senders. */
+        for (uint32_t w = 0; w < W; ++w) { p0[w] = p1[w] = 0; }
+        for (uint32_t c = 0; c < m; ++c) {
+            const uint64_t *a0 = x0, *a1 = x1;
+            __asm__ volatile("" : "+r"(a0), "+r"(a1));   /* per-receiver tally: no hoisting */
+            int c0 = 0, c1 = 0;
+            for (uint32_t w = 0; w < W; ++w) { c0 += popc64(a0[w]); c1 += popc64(a1[w]); }
+            if (c0 > c1) p0[c >> 6] |= 1ull << (c & 63);
+            else if (c1 > c0) p1[c >> 6] |= 1ull << (c & 63);
+        }
+        /* P-phase (node.ts:88-113) */
+        uint64_t nx0[64], nx1[64];
+        for (uint32_t w = 0; w < W; ++w) { nx0[w] = nx1[w] = 0; }
+        for (uint32_t c = 0; c < m; ++c) {
+            const uint64_t *a0 = p0, *a1 = p1;
+            __asm__ volatile("" : "+r"(a0), "+r"(a1));
+            int c0 = 0, c1 = 0;
+            for (uint32_t w = 0; w < W; ++w) { c0 += popc64(a0[w]); c1 += popc64(a1[w]); }
+            int x;
+            uint64_t bit = 1ull << (c & 63);
+            if (c0 > (int)F) { x = 0; dec[c >> 6] |= bit; }
+            else if (c1 > (int)F) { x = 1; dec[c >> 6] |= bit; }
+            else if (c0 + c1 > 0 && c0 > c1) x = 0;
+            else if (c0 + c1 > 0 && c0 < c1) x = 1;
+            else x = oracle_coin(cfg->seed, trial, live_ids[c], r);
+            if (x) nx1[c >> 6] |= bit; else nx0[c >> 6] |= bit;
+        }
+        for (uint32_t w = 0; w < W; ++w) { x0[w] = nx0[w]; x1[w] = nx1[w]; }
+        R = r;
+        all_dec = 1;
+        for (uint32_t w = 0; w < W; ++w) {
+            uint32_t lo = w * 64, n = (m - lo) < 64 ? (m - lo) : 64;
+            uint64_t vm = n == 64 ? ~0ull : ((1ull << n) - 1);
+            if ((dec[w] & vm) != vm) { all_dec = 0; break; }
+        }
+        if (all_dec) break;
+    }
+    /* common value */
+    int any0 = 0, any1 = 0;
+    for (uint32_t w = 0; w < W; ++w) { any0 |= x0[w] != 0; any1 |= x1[w] != 0; }
+    int v = (any0 && any1) ? 2 : any1 ? 1 : 0;
+    if (all_dec) {
+        hist[(size_t)R * 3 + (size_t)v]++;
+        if (v == 2) hist[H]++;
+    } else {
+        hist[v]++;
+    }
+    if (node_out) {
+        for (uint32_t c = 0; c < m; ++c) {
+            orc_node_state *s = &node_out[live_ids[c]];
+            uint64_t bit = 1ull << (c & 63);
+            s->x = (x1[c >> 6] & bit) ? 1 : 0;
+            s->decided = (dec[c >> 6] & bit) ? 1 : 0;
+            s->k = (int32_t)R + 1;
+        }
+    }
+}
+
+/* Batch of independent trials; hist has (k_max+1)*3+1 entries (accumulated).
+ * node_out (optional, only when trial_count == 1): per-node final state.
+ * Returns 0, or -1 on bad config. */
+int oracle_run_trials(const orc_trials_cfg *cfg, uint64_t *hist, orc_node_state *node_out) {
+    if (cfg->k_max < 1 || cfg->N > 4096) return -1;
+    uint32_t *live_ids = (uint32_t *)malloc(sizeof(uint32_t) * (cfg->N + 1));
+    uint32_t m = 0;
+    for (uint32_t i = 0; i < cfg->N; ++i) if (!cfg->faulty[i]) live_ids[m++] = i;
+    /* this restatement covers the reference's admissible inputs: the number of
+     * crash-faulty nodes is exactly F (launchNodes.ts:12-13), or fewer live
+     * nodes than the quorum (stall).  f < F needs the random-delivery model. */
+    if ((int64_t)m > (int64_t)cfg->N - (int64_t)cfg->F) { free(live_ids); return -2; }
+    if (node_out) {
+        for (uint32_t i = 0; i < cfg->N; ++i) {
+            int f = cfg->faulty[i] != 0;
+            node_out[i].killed = (int8_t)f;
+            node_out[i].x = f ? -1 : (cfg->init_mode == 1 ? cfg->init[i] : -1);
+            node_out[i].decided = f ? -1 : 0;
+            node_out[i].k = f ? -1 : 0;
+            node_out[i].pad = 0;
+        }
+    }
+    const size_t HS = (size_t)(cfg->k_max + 1) * 3 + 1;
+    int nthreads = 1;
+#ifdef _OPENMP
+    nthreads = cfg->threads > 0 ? cfg->threads : omp_get_max_threads();
+#endif
+    if (node_out) nthreads = 1;
+    uint64_t *hl = (uint64_t *)calloc((size_t)nthreads * HS, sizeof(uint64_t));
+#ifdef _OPENMP
+#pragma omp parallel num_threads(nthreads)
+#endif
+    {
+        int tid = 0;
+#ifdef _OPENMP
+        tid = omp_get_thread_num();
+#endif
+        uint64_t x0[64], x1[64], p0[64], p1[64], dec[64];
+        uint64_t *h = hl + (size_t)tid * HS;
+#ifdef _OPENMP
+#pragma omp for schedule(static)
+#endif
+        for (int64_t t = 0; t < (int64_t)cfg->trial_count; ++t)
+            run_one(cfg, live_ids, m, cfg->trial_begin + (uint64_t)t, x0, x1, p0, p1, dec, h,
+                    node_out);
+    }
+    for (int t = 0; t < nthreads; ++t)
+        for (size_t j = 0; j < HS; ++j) hist[j] += hl[(size_t)t * HS + j];
+    free(hl);
+    free(live_ids);
+    return 0;
+}

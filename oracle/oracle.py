@@ -1,0 +1,141 @@
+"""ctypes front-end for the CPU oracle (oracle/benor_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py -- never by the product package.  It restates the
+reference's algorithm (src/nodes/node.ts:43-163, launchNodes.ts:10-13); see the
+C file header for the pinning story.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+
+class NodeState(ctypes.Structure):
+    _fields_ = [("killed", ctypes.c_int8), ("x", ctypes.c_int8), ("decided", ctypes.c_int8),
+                ("pad", ctypes.c_int8), ("k", ctypes.c_int32)]
+
+
+class TrialsCfg(ctypes.Structure):
+    _fields_ = [("N", ctypes.c_uint32), ("F", ctypes.c_uint32), ("k_max", ctypes.c_uint32),
+                ("init_mode", ctypes.c_uint32), ("seed", ctypes.c_uint64),
+                ("trial_begin", ctypes.c_uint64), ("trial_count", ctypes.c_uint64),
+                ("faulty", ctypes.POINTER(ctypes.c_uint8)), ("init", ctypes.POINTER(ctypes.c_int8)),
+                ("threads", ctypes.c_int32)]
+
+
+def build() -> str:
+    """Compile liboracle.so in place (gcc)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        L.oracle_philox4x32_10.argtypes = [ctypes.POINTER(ctypes.c_uint32)] * 3
+        L.oracle_coin.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32]
+        L.oracle_coin.restype = ctypes.c_int
+        L.oracle_random_init.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32]
+        L.oracle_random_init.restype = ctypes.c_int
+        L.oracle_validate.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                      ctypes.POINTER(ctypes.c_uint8)]
+        L.oracle_validate.restype = ctypes.c_int
+        L.oracle_message_sim.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_int8),
+                                         ctypes.POINTER(ctypes.c_uint8), ctypes.c_uint64, ctypes.c_uint64,
+                                         ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(NodeState),
+                                         ctypes.POINTER(ctypes.c_int)]
+        L.oracle_message_sim.restype = ctypes.c_int
+        L.oracle_run_trials.argtypes = [ctypes.POINTER(TrialsCfg), ctypes.POINTER(ctypes.c_uint64),
+                                        ctypes.POINTER(NodeState)]
+        L.oracle_run_trials.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def philox4x32_10(key, ctr):
+    k = (ctypes.c_uint32 * 2)(*key)
+    c = (ctypes.c_uint32 * 4)(*ctr)
+    o = (ctypes.c_uint32 * 4)()
+    lib().oracle_philox4x32_10(k, c, o)
+    return list(o)
+
+
+def coin(seed: int, trial: int, node: int, rnd: int) -> int:
+    return lib().oracle_coin(seed, trial, node, rnd)
+
+
+def random_init(seed: int, trial: int, c: int) -> int:
+    return lib().oracle_random_init(seed, trial, c)
+
+
+VAL_CODE = {0: 0, 1: 1, "?": 2}
+CODE_VAL = {-1: None, 0: 0, 1: 1, 2: "?"}
+
+
+def _states(arr, n):
+    out = []
+    for i in range(n):
+        s = arr[i]
+        out.append({"killed": bool(s.killed), "x": CODE_VAL[s.x],
+                    "decided": None if s.decided < 0 else bool(s.decided),
+                    "k": None if s.k < 0 else int(s.k)})
+    return out
+
+
+def validate(N, F, initial_values, faulty_list) -> int:
+    f = (ctypes.c_uint8 * max(1, len(faulty_list)))(*[1 if v else 0 for v in faulty_list])
+    return lib().oracle_validate(N, F, len(initial_values), len(faulty_list), f)
+
+
+def message_sim(N, F, initial_values, faulty_list, seed=0, trial=0, k_max=64, order_mode=1):
+    """(i) message-level restatement: returns (rounds or -1, stalled, states)."""
+    init = (ctypes.c_int8 * max(1, N))(*[VAL_CODE[v] for v in initial_values])
+    f = (ctypes.c_uint8 * max(1, N))(*[1 if v else 0 for v in faulty_list])
+    st = (NodeState * max(1, N))()
+    stalled = ctypes.c_int(0)
+    r = lib().oracle_message_sim(N, F, init, f, seed, trial, k_max, order_mode, st, ctypes.byref(stalled))
+    return r, bool(stalled.value), _states(st, N)
+
+
+def hist_len(k_max: int) -> int:
+    return (k_max + 1) * 3 + 1
+
+
+@dataclass
+class TrialsResult:
+    hist: np.ndarray
+    states: list | None
+
+
+def run_trials(N, F, faulty_list, *, seed=0, trial_begin=0, trial_count=1, k_max=64,
+               initial_values=None, threads=0, want_states=False) -> TrialsResult:
+    """(ii) round-level bit-plane restatement over a batch of trials."""
+    f = (ctypes.c_uint8 * max(1, N))(*[1 if v else 0 for v in faulty_list])
+    if initial_values is None:
+        init = (ctypes.c_int8 * max(1, N))()
+        mode = 0
+    else:
+        init = (ctypes.c_int8 * max(1, N))(*[VAL_CODE[v] for v in initial_values])
+        mode = 1
+    cfg = TrialsCfg(N, F, k_max, mode, seed, trial_begin, trial_count,
+                    ctypes.cast(f, ctypes.POINTER(ctypes.c_uint8)),
+                    ctypes.cast(init, ctypes.POINTER(ctypes.c_int8)), threads)
+    hist = np.zeros(hist_len(k_max), dtype=np.uint64)
+    st = (NodeState * max(1, N))() if want_states else None
+    rc = lib().oracle_run_trials(ctypes.byref(cfg), hist.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                 st)
+    if rc != 0:
+        raise ValueError(f"oracle_run_trials rc={rc}")
+    return TrialsResult(hist, _states(st, N) if want_states else None)

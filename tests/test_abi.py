@@ -1,0 +1,97 @@
+"""C ABI boundary checks that need no GPU (CPU suite).
+
+* libbenor.so loads and exports every entry point include/benor.h declares.
+* The host-side half of the reference surface behaves like the reference
+  without any device work: launch validation (launchNodes.ts:10-13), initial
+  NodeState (node.ts:21-26), /status (node.ts:33-39), /stop (node.ts:191-194).
+  These are the reference's "Project is setup correctly" tests
+  (benorconsensus.test.ts:45-118), verbatim in intent.
+* Compute entry points fail loudly without a device (no CPU fallback).
+"""
+import os
+import re
+import subprocess
+
+import pytest
+
+import benor
+from conftest import ROOT, check_reference_expectations
+
+HEADER = os.path.join(ROOT, "include", "benor.h")
+
+
+def header_symbols():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:[\w\s\*]+?)\b(bo_\w+)\s*\(", txt, flags=re.M)))
+
+
+def test_header_declares_python_mirror_symbols():
+    assert sorted(benor.EXPORTED_SYMBOLS) == header_symbols()
+
+
+def test_library_exports_every_declared_symbol():
+    out = subprocess.run(["nm", "-D", "--defined-only", benor.LIB_PATH], check=True, capture_output=True,
+                         text=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    missing = [s for s in header_symbols() if s not in exported]
+    assert not missing, missing
+    L = benor.lib()
+    for s in header_symbols():
+        assert hasattr(L, s)
+    assert L.bo_abi_version() == 1
+    assert L.bo_hist_len(64) == 65 * 3 + 1
+
+
+def test_library_targets_gfx950():
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/clang-offload-bundler", "--list", "--type=o",
+                          f"--input={benor.LIB_PATH}"], capture_output=True, text=True)
+    # the offload bundle lives in .hip_fatbin; fall back to scanning the file
+    data = open(benor.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+
+
+def test_launch_errors(reference_cases):
+    for e in reference_cases["launch_errors"]:
+        with pytest.raises(benor.Error, match=re.escape(e["error"])):
+            benor.launchNetwork(e["N"], e["F"], e["init"], e["faulty"])
+
+
+def test_setup_cases_status(reference_cases):
+    for case in reference_cases["cases"]:
+        if case["start"]:
+            continue
+        N = case["N"]
+        servers = benor.launchNetwork(N, sum(case["faulty"]), case["init"], case["faulty"])
+        assert len(servers) == N
+        statuses = [benor.getStatus(i) for i in range(N)]
+        check_reference_expectations(case, benor.getNodesState(N), statuses)
+        benor.stopConsensus(N)
+        assert all(benor.getStatus(i) == (500, "faulty") for i in range(N))   # node.ts:191-194, :33-35
+        for s in servers:
+            s.close(lambda: s.closeAllConnections())
+
+
+def test_initial_state_before_start():
+    fl = [True, False, False, False, False]
+    benor.launchNetwork(5, 1, [1, 0, "?", 1, 0], fl)
+    st = benor.getNodesState(5)
+    assert st[0] == {"killed": True, "x": None, "decided": None, "k": None}
+    assert st[2] == {"killed": False, "x": "?", "decided": False, "k": 0}
+    assert not benor.reachedFinality(st)
+
+
+def test_reference_accepts_what_it_accepts():
+    # F > N/2, '?' initial values, F == N are all accepted (launchNodes.ts:10-13
+    # is the only validation; start.ts:25-29 rejects F > N/2 only in the demo).
+    benor.launchNetwork(4, 3, ["?", 1, 0, 1], [True, True, True, False])
+    benor.launchNetwork(2, 2, [1, 1], [True, True])
+    assert benor.getNodesState(2)[0]["x"] is None
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="a GPU is present: the loud-failure path is not reachable")
+def test_no_silent_cpu_fallback():
+    benor.launchNetwork(5, 0, [1] * 5, [False] * 5)
+    with pytest.raises(RuntimeError, match="libbenor error 4"):
+        benor.startConsensus(5, seed=1)
+    with pytest.raises(RuntimeError, match="libbenor error 4"):
+        benor.TrialsPlan(10, 4)

@@ -1,0 +1,165 @@
+"""Parity of the HIP path (via the C ABI) against the CPU oracle.  GPU only.
+
+Bit-exact integer agreement is required everywhere:
+* per-node final NodeState of every committed golden state case
+  (tests/golden/oracle_vectors.json: every 0/1 input of the reference's
+  shapes, '?' inputs, coin-heavy ties, W > 1 and padded tally blocks);
+* outcome histograms of the committed golden histogram cases;
+* fresh seeded batches against the oracle run live on the same inputs;
+* the reference's own known-answer tests through the network API.
+At BASELINE's full sizes (N=1024, F=341, up to 10^7 trials per launch),
+size-independent properties: sharding invariance (histogram of [0, T) equals
+the sum over any split), R == 1 whenever m is odd, agreement, and the exact
+analytic law by chi-square.
+"""
+import itertools
+
+import numpy as np
+import pytest
+
+import analytic
+import benor
+import oracle
+from conftest import check_reference_expectations
+from make_golden import decode_state
+
+pytestmark = pytest.mark.gpu
+
+
+def first_f(N, F):
+    return [i < F for i in range(N)]
+
+
+def test_golden_states(oracle_vectors):
+    for c in oracle_vectors["states"]:
+        rounds, st = benor.run_trial_states(c["N"], c["F"], c["faulty"], seed=c["seed"], trial=c["trial"],
+                                            k_max=c["k_max"], initial_values=c["init"])
+        assert st == [decode_state(e) for e in c["states"]], c
+
+
+def test_golden_histograms(oracle_vectors):
+    for h in oracle_vectors["hists"]:
+        plan = benor.TrialsPlan(h["N"], h["F"], first_f(h["N"], h["F"]), seed=h["seed"], k_max=h["k_max"])
+        got = plan.run(h["trial_begin"], h["trial_count"])
+        assert {str(i): int(v) for i, v in enumerate(got) if v} == h["hist_nonzero"], (h["N"], h["F"])
+
+
+@pytest.mark.parametrize("N,F,trials,k_max", [
+    (10, 4, 200_000, 24), (10, 5, 50_000, 11), (5, 1, 100_000, 24), (64, 0, 30_000, 32),
+    (70, 2, 20_000, 32), (128, 0, 20_000, 32), (256, 85, 20_000, 16), (1024, 341, 5_000, 16),
+    (1088, 0, 500, 32), (1100, 40, 1_000, 32), (2047, 0, 200, 32), (4096, 0, 100, 16), (4096, 2047, 100, 16),
+    (3, 1, 10_000, 8), (1, 0, 1000, 4), (2, 1, 1000, 4), (33, 16, 5000, 16),
+])
+def test_random_batches_match_oracle(N, F, trials, k_max):
+    seed = 0x9E3779B97F4A7C15 ^ (N * 7919 + F)
+    plan = benor.TrialsPlan(N, F, first_f(N, F), seed=seed, k_max=k_max)
+    got = plan.run(777, trials)
+    ref = oracle.run_trials(N, F, first_f(N, F), seed=seed, trial_begin=777, trial_count=trials, k_max=k_max)
+    np.testing.assert_array_equal(got, ref.hist)
+
+
+@pytest.mark.parametrize("N,F", [(12, 4), (16, 6), (9, 3), (64, 2)])
+def test_random_fault_placement_states(N, F):
+    """Fault placement is arbitrary (faultyList); per-node states must match."""
+    rng = np.random.default_rng(N + 31 * F)
+    for t in range(30):
+        fl = [False] * N
+        for i in rng.choice(N, F, replace=False):
+            fl[i] = True
+        init = [int(v) for v in rng.integers(0, 2, N)]
+        seed = int(rng.integers(0, 2**63))
+        ref = oracle.run_trials(N, F, fl, seed=seed, trial_begin=t, trial_count=1, k_max=20,
+                                initial_values=init, want_states=True).states
+        _, got = benor.run_trial_states(N, F, fl, seed=seed, trial=t, k_max=20, initial_values=init)
+        assert got == ref
+
+
+def test_reference_known_answers_network_api(reference_cases):
+    """benorconsensus.test.ts:133-486 through launchNetwork / startConsensus /
+    getNodesState / stopConsensus -- the reference's call sequence."""
+    for case in reference_cases["cases"]:
+        inits = ([list(b) for b in itertools.product([0, 1], repeat=case["N"])]
+                 if case["init"] == "random01" else [case["init"]])
+        for init in inits:
+            N = case["N"]
+            servers = benor.launchNetwork(N, sum(case["faulty"]), init, case["faulty"])
+            statuses = [benor.getStatus(i) for i in range(N)]
+            if case["start"]:
+                benor.startConsensus(N, seed=0x5EED)
+                states = benor.getNodesState(N)
+                assert benor.reachedFinality(states) or any(s["decided"] is False for s in states)
+                check_reference_expectations(case, states)
+                ref = oracle.run_trials(N, sum(case["faulty"]), case["faulty"], seed=0x5EED, trial_begin=0,
+                                        trial_count=1, k_max=benor.DEFAULT_K_MAX, initial_values=init,
+                                        want_states=True).states
+                assert states == ref
+            else:
+                check_reference_expectations(case, benor.getNodesState(N), statuses)
+            benor.stopConsensus(N)
+            assert all(benor.getStatus(i)[0] == 500 for i in range(N))
+            for s in servers:
+                s.close()
+
+
+def test_stopped_nodes_stall():
+    """A node stopped before start leaves fewer than N-F senders: the round-1
+    R-phase never triggers (node.ts:52), so live nodes sit at k = 1."""
+    servers = benor.launchNetwork(5, 1, [1, 1, 1, 0, 0], [False, False, False, False, True])
+    servers[0]._net.stop_node(0)
+    benor.startConsensus(5, seed=3)
+    st = benor.getNodesState(5)
+    assert st[0]["killed"] and st[0]["k"] == 0
+    assert all(s["k"] == 1 and s["decided"] is False for s in st[1:4])
+
+
+def test_restart_runs_from_current_values():
+    benor.launchNetwork(6, 2, [0, 0, 1, 1, 0, 1], [True, False, False, False, False, True])
+    benor.startConsensus(6, seed=1)
+    a = benor.getNodesState(6)
+    benor.startConsensus(6, seed=1)   # second start: fresh run from the decided x
+    b = benor.getNodesState(6)
+    assert all(s["decided"] for s in b[1:5])
+    assert [s["x"] for s in a] == [s["x"] for s in b]
+
+
+# ------------------------------------------------- full-size properties
+def test_full_size_sharding_invariance_and_law():
+    """N=1024, F=341 (BASELINE metric config): m = 683 is odd, so no round can
+    tie -- every trial decides the live majority in round 1.  The
+    histogram of one launch equals the sum of a split run (global Philox
+    counters), and the decided value is Bernoulli(1/2)."""
+    N, F, k = 1024, 341, 16
+    plan = benor.TrialsPlan(N, F, first_f(N, F), seed=0x243F6A8885A308D3, k_max=k)
+    T = 2_000_000
+    whole = plan.run(0, T)
+    parts = plan.run(0, 600_001) + plan.run(600_001, 1_000_000) + plan.run(1_600_001, T - 1_600_001)
+    np.testing.assert_array_equal(whole, parts)
+    assert whole.sum() == T
+    assert whole[3] + whole[4] == T            # bins (R=1, v=0), (R=1, v=1)
+    assert whole[-1] == 0
+    assert analytic.chi2_pvalue(whole[:-1], analytic.hist_probs(N, F, k)) > 1e-3
+    # a spot-check of the same launch range against the oracle
+    ref = oracle.run_trials(N, F, first_f(N, F), seed=0x243F6A8885A308D3, trial_begin=1_999_000,
+                            trial_count=1000, k_max=k)
+    np.testing.assert_array_equal(plan.run(1_999_000, 1000), ref.hist)
+
+
+@pytest.mark.parametrize("N,F,k_max", [(10, 4, 24), (10, 5, 11), (64, 0, 32), (100, 30, 32)])
+def test_analytic_law_1e6(N, F, k_max):
+    plan = benor.TrialsPlan(N, F, first_f(N, F), seed=0xA11CE + N, k_max=k_max)
+    h = plan.run(0, 1_000_000)
+    assert h.sum() == 1_000_000 and h[-1] == 0
+    assert analytic.chi2_pvalue(h[:-1], analytic.hist_probs(N, F, k_max)) > 1e-3
+
+
+def test_no_decision_case_f_gt_half():
+    """Exceeding Fault Tolerance (benorconsensus.test.ts:292-345) at scale:
+    N=10, F=5 never decides; every trial runs k_max rounds (k = k_max+1 > 10)."""
+    plan = benor.TrialsPlan(10, 5, first_f(10, 5), seed=5, k_max=11)
+    h = plan.run(0, 1_000_000)
+    assert h[:3].sum() == 1_000_000
+
+
+def test_popc_peak_probe_runs():
+    peak = benor.popc_peak(5)
+    assert peak > 1e12

@@ -1,0 +1,148 @@
+"""Pin the CPU oracle before trusting it (CPU only).
+
+* Philox4x32-10 against the Random123 known-answer vectors.
+* The reference's launch validation (launchNodes.ts:10-13).
+* Every known-answer test of the reference suite
+  (__test__/tests/benorconsensus.test.ts:45-486) through both restatements.
+* Message-level (i) == bit-plane (ii) on tie-heavy seeded cases, under FIFO
+  and seeded-random delivery orders.
+* The exact analytic outcome law by chi-square.
+* The committed golden vectors are reproduced.
+"""
+import itertools
+
+import numpy as np
+import pytest
+
+import analytic
+import oracle
+from conftest import check_reference_expectations
+from make_golden import decode_state
+
+# Random123 kat_vectors, philox4x32_10
+PHILOX_KAT = [
+    ([0, 0], [0, 0, 0, 0], [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]),
+    ([0xFFFFFFFF, 0xFFFFFFFF], [0xFFFFFFFF] * 4, [0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD]),
+    ([0xA4093822, 0x299F31D0], [0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344],
+     [0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1]),
+]
+
+
+@pytest.mark.parametrize("key,ctr,out", PHILOX_KAT)
+def test_philox_kat(key, ctr, out):
+    assert oracle.philox4x32_10(key, ctr) == out
+
+
+def test_coin_matches_math_random_rule():
+    # coin = Math.random() > 0.5 ? 0 : 1 with u = w * 2^-32 (node.ts:111)
+    for trial in range(50):
+        for node in range(5):
+            w = oracle.philox4x32_10([0x1234, 0], [trial, 0, node, 3])[0]
+            assert oracle.coin(0x1234, trial, node, 3) == (0 if w / 2**32 > 0.5 else 1)
+
+
+def test_launch_errors(reference_cases):
+    for e in reference_cases["launch_errors"]:
+        code = oracle.validate(e["N"], e["F"], e["init"], e["faulty"])
+        assert code == {"Arrays don't match": 1, "faultyList doesnt have F faulties": 2}[e["error"]]
+
+
+def _run_case_message(case, init, seed=7):
+    N = case["N"]
+    F = sum(case["faulty"])
+    return oracle.message_sim(N, F, init, case["faulty"], seed=seed, trial=0, k_max=64)
+
+
+def _run_case_planes(case, init, seed=7):
+    N = case["N"]
+    F = sum(case["faulty"])
+    return oracle.run_trials(N, F, case["faulty"], seed=seed, trial_begin=0, trial_count=1, k_max=64,
+                             initial_values=init, want_states=True).states
+
+
+def test_reference_known_answers(reference_cases):
+    for case in reference_cases["cases"]:
+        if not case["start"]:
+            continue
+        inits = ([list(b) for b in itertools.product([0, 1], repeat=case["N"])]
+                 if case["init"] == "random01" else [case["init"]])
+        for init in inits:
+            r, stalled, st_i = _run_case_message(case, init)
+            assert not stalled
+            st_ii = _run_case_planes(case, init)
+            assert st_i == st_ii
+            check_reference_expectations(case, st_i)
+
+
+@pytest.mark.parametrize("N,F", [(4, 0), (6, 2), (8, 2), (10, 4), (12, 4), (8, 4), (6, 3), (2, 0), (16, 6)])
+def test_message_level_equals_bitplanes(N, F):
+    """(i) == (ii) per node, including coin rounds: tie-heavy even-m shapes."""
+    rng = np.random.default_rng(N * 100 + F)
+    for t in range(40):
+        faulty = [False] * N
+        for i in rng.choice(N, F, replace=False):
+            faulty[i] = True
+        init = [int(v) for v in rng.integers(0, 2, N)]
+        if t % 7 == 0:
+            init[rng.integers(0, N)] = "?"
+        seed = int(rng.integers(0, 2**63))
+        for order in (0, 1):
+            r, stalled, st_i = oracle.message_sim(N, F, init, faulty, seed=seed, trial=t, k_max=24,
+                                                  order_mode=order)
+            st_ii = oracle.run_trials(N, F, faulty, seed=seed, trial_begin=t, trial_count=1, k_max=24,
+                                      initial_values=init, want_states=True).states
+            assert st_i == st_ii, (N, F, init, faulty, order)
+
+
+def test_delivery_order_independence():
+    """With exactly F crashes every inbox is the full live set, so the seeded
+    delivery order cannot change any outcome."""
+    N, F = 9, 3
+    faulty = [True] * F + [False] * (N - F)
+    init = [0, 0, 0, 1, 1, 1, 0, 1, 0]
+    ref = oracle.message_sim(N, F, init, faulty, seed=11, trial=5, order_mode=0)
+    for salt in range(1, 30):
+        got = oracle.message_sim(N, F, init, faulty, seed=11, trial=5, order_mode=salt)
+        assert got == ref
+
+
+def test_stall_when_fewer_live_than_quorum():
+    # launchNodes accepts only exactly-F faults, but a node stopped before the
+    # run leaves fewer senders than N-F: nothing ever triggers (node.ts:52).
+    N, F = 5, 1
+    r, stalled, st = oracle.message_sim(N, F, [1, 1, 1, 1, 1], [True, True, False, False, False], k_max=8)
+    assert stalled and r == -1
+    assert all(s["k"] == 1 and s["decided"] is False for s in st[2:])
+
+
+@pytest.mark.parametrize("N,F,k_max", [(10, 4, 16), (5, 1, 16), (10, 5, 11), (64, 0, 24), (100, 30, 24),
+                                       (7, 2, 16), (4, 1, 24), (12, 6, 12)])
+def test_analytic_law(N, F, k_max):
+    faulty = [i < F for i in range(N)]
+    r = oracle.run_trials(N, F, faulty, seed=0xC0FFEE + N, trial_count=100000, k_max=k_max)
+    probs = analytic.hist_probs(N, F, k_max)
+    assert r.hist[-1] == 0                              # agreement never violated
+    assert abs(probs.sum() - 1.0) < 1e-9
+    assert analytic.chi2_pvalue(r.hist[:-1], probs) > 1e-3
+
+
+def test_expected_rounds_closed_form():
+    # N=5,F=1 -> q=0.375, E[R]=1.6; N=10,F=4 -> q=0.3125, E[R]=1.4545
+    assert analytic.tie_prob(4) == pytest.approx(0.375)
+    assert analytic.expected_rounds(5, 1) == pytest.approx(1.6)
+    assert analytic.tie_prob(6) == pytest.approx(0.3125)
+    assert analytic.expected_rounds(10, 4) == pytest.approx(1.454545, rel=1e-5)
+    assert analytic.tie_prob(683) == 0.0
+
+
+def test_golden_vectors_reproduce(oracle_vectors):
+    for c in oracle_vectors["states"][::3]:
+        res = oracle.run_trials(c["N"], c["F"], c["faulty"], seed=c["seed"], trial_begin=c["trial"],
+                                trial_count=1, k_max=c["k_max"], initial_values=c["init"], want_states=True)
+        assert res.states == [decode_state(e) for e in c["states"]]
+    for h in oracle_vectors["hists"]:
+        if h["N"] * h["trial_count"] > 2_000_000:
+            continue
+        res = oracle.run_trials(h["N"], h["F"], [i < h["F"] for i in range(h["N"])], seed=h["seed"],
+                                trial_begin=h["trial_begin"], trial_count=h["trial_count"], k_max=h["k_max"])
+        assert {str(i): int(v) for i, v in enumerate(res.hist) if v} == h["hist_nonzero"]
