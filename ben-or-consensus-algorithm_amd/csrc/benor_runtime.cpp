@@ -150,16 +150,19 @@ int bo_consensus_start(bo_network *net, uint64_t seed, uint32_t k_max) {   // co
   std::vector<uint32_t> active;
   for (uint32_t i = 0; i < N; ++i)
     if (!net->st[i].killed) active.push_back(i);
-  const uint64_t trial = net->starts++;
   if (active.empty()) return BO_OK;
-  for (uint32_t i : active) net->st[i].k = 1;   // node.ts:172
   const int64_t quorum = (int64_t)N - (int64_t)net->F;
   // Fewer running senders than the quorum: no R-phase ever triggers
   // (node.ts:52), every running node stays at k = 1, undecided.
-  if ((int64_t)active.size() < quorum) return BO_OK;
+  if ((int64_t)active.size() < quorum) {
+    for (uint32_t i : active) net->st[i].k = 1;   // node.ts:172
+    ++net->starts;
+    return BO_OK;
+  }
   int dev = 0;
   int rc = check_device(&dev);
   if (rc) return rc;
+  const uint64_t trial = net->starts++;
 
   bo_trials_cfg cfg{};
   cfg.N = N;

@@ -1,0 +1,63 @@
+// Type declarations for the JavaScript mirror (index.js).  The reference's
+// types are src/types.ts:1-8; the signatures mirror src/index.ts:4-14 and
+// src/nodes/consensus.ts:3-15.
+
+export type Value = 0 | 1 | "?";
+
+export type NodeState = {
+  killed: boolean;
+  x: Value | null;
+  decided: boolean | null;
+  k: number | null;
+};
+
+export declare const BASE_NODE_PORT: number;
+export declare const DEFAULT_K_MAX: number;
+
+/** Stand-in for the reference's http.Server per node. */
+export interface NodeServer {
+  readonly nodeId: number;
+  readonly port: number;
+  close(cb?: () => void): NodeServer;
+  closeAllConnections(): void;
+}
+
+/** Rejects with Error("Arrays don't match") / Error("faultyList doesnt have F faulties"). */
+export declare function launchNetwork(
+  N: number,
+  F: number,
+  initialValues: Value[],
+  faultyList: boolean[]
+): Promise<NodeServer[]>;
+
+export interface StartOptions {
+  /** Philox key for the per-node coins (default: random, like Math.random()). */
+  seed?: bigint | number;
+  /** Round cap (default 64). */
+  kMax?: number;
+}
+
+export declare function startConsensus(N: number, options?: StartOptions): Promise<void>;
+export declare function stopConsensus(N: number): Promise<void>;
+export declare function stopNode(nodeId: number): Promise<void>;
+export declare function getNodeState(nodeId: number): Promise<NodeState>;
+export declare function getNodesState(N: number): Promise<NodeState[]>;
+export declare function getNodeStatus(nodeId: number): Promise<{ status: 200 | 500; body: "live" | "faulty" }>;
+export declare function reachedFinality(states: NodeState[]): boolean;
+export declare function delay(ms: number): Promise<void>;
+
+export interface TrialsConfig {
+  N: number;
+  F: number;
+  /** default: the first F nodes are crash-faulty */
+  faultyList?: boolean[];
+  /** default: iid Bernoulli(1/2) per live node */
+  initialValues?: Value[];
+  seed?: bigint | number;
+  kMax?: number;
+  trialBegin?: bigint | number;
+  trialCount?: bigint | number;
+}
+
+/** Outcome histogram, (kMax + 1) * 3 + 1 bins (include/benor.h). */
+export declare function runTrials(cfg: TrialsConfig): Promise<BigUint64Array>;

@@ -1,0 +1,94 @@
+'use strict';
+// JavaScript mirror of the reference's public surface, backed by the N-API
+// addon (benor.node) over libbenor.so.  Drop-in for
+//   src/index.ts:4-14            launchNetwork(N, F, initialValues, faultyList)
+//   src/nodes/consensus.ts:3-15  startConsensus(N) / stopConsensus(N)
+//   __test__/tests/utils.ts:4-24 getNodesState(N) / reachedFinality(states)
+// plus what the HTTP routes served: getNodeState(i) (GET /getState,
+// node.ts:197-199) and getNodeStatus(i) (GET /status, node.ts:33-39).
+// As in the reference, one network "listens" at a time (ports 3000 + i there;
+// the most recently launched network here).
+
+const path = require('path');
+const addon = require(path.join(__dirname, 'benor.node'));
+
+const BASE_NODE_PORT = 3000;          // src/config.ts:1
+const DEFAULT_K_MAX = 64;             // round cap: the reference runs until /stop
+
+let current = null;                   // { handle, N }
+
+// Stands in for the http.Server objects launchNetwork returns; the reference
+// test teardown calls server.close(cb) and closeAllConnections()
+// (benorconsensus.test.ts:14-29).
+class NodeServer {
+  constructor(nodeId) { this.nodeId = nodeId; this.port = BASE_NODE_PORT + nodeId; }
+  close(cb) { if (typeof cb === 'function') setImmediate(cb); return this; }
+  closeAllConnections() {}
+}
+
+async function launchNetwork(N, F, initialValues, faultyList) {
+  const handle = addon.networkCreate(N, F, initialValues, faultyList);   // throws the reference's Errors
+  current = { handle, N };
+  const servers = [];
+  for (let i = 0; i < N; i++) servers.push(new NodeServer(i));
+  return servers;
+}
+
+function net(N) {
+  if (!current || (N !== undefined && current.N !== N)) throw new Error(`no launched network of size ${N}`);
+  return current;
+}
+
+function randomSeed() {
+  // the reference's coins come from Math.random(); a fresh 64-bit key per start
+  const hi = BigInt(Math.floor(Math.random() * 2 ** 32));
+  const lo = BigInt(Math.floor(Math.random() * 2 ** 32));
+  return (hi << 32n) | lo;
+}
+
+// Resolves once the round loop has run to completion (all live nodes decided,
+// or kMax rounds).  The reference resolves before consensus finishes and the
+// callers poll getNodesState; polling here sees the final states at once.
+async function startConsensus(N, options = {}) {
+  if (N === 0) return;
+  const seed = options.seed !== undefined ? BigInt(options.seed) : randomSeed();
+  const kMax = options.kMax !== undefined ? options.kMax : DEFAULT_K_MAX;
+  await addon.networkStart(net(N).handle, seed, kMax);
+}
+
+async function stopConsensus(N) {
+  if (N === 0) return;
+  addon.networkStop(net(N).handle);
+}
+
+async function stopNode(nodeId) { addon.nodeStop(net().handle, nodeId); }
+
+async function getNodeState(nodeId) { return addon.getState(net().handle, nodeId); }
+
+async function getNodesState(N) {
+  const h = net(N).handle;
+  const out = [];
+  for (let i = 0; i < N; i++) out.push(addon.getState(h, i));
+  return out;
+}
+
+// GET /status: { status: 500, body: "faulty" } | { status: 200, body: "live" }
+async function getNodeStatus(nodeId) {
+  const code = addon.status(net().handle, nodeId);
+  return { status: code, body: code === 500 ? 'faulty' : 'live' };
+}
+
+function reachedFinality(states) {
+  return states.find((el) => el.decided === false) === undefined;
+}
+
+// Batch of independent trials: resolves to the outcome histogram
+// (BigUint64Array, layout documented in include/benor.h).
+async function runTrials(cfg) { return addon.runTrials(cfg); }
+
+const delay = (ms) => new Promise((res) => setTimeout(res, ms));   // src/utils.ts:1
+
+module.exports = {
+  BASE_NODE_PORT, DEFAULT_K_MAX, launchNetwork, startConsensus, stopConsensus, stopNode,
+  getNodeState, getNodesState, getNodeStatus, reachedFinality, runTrials, delay,
+};
