@@ -88,6 +88,7 @@ def main():
     import torch.distributed as dist
 
     import benor
+    from benor.parallel import merge_histogram, weak_range
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -107,10 +108,9 @@ def main():
 
     def step(s):
         step_hist.zero_()
-        begin = (s * world + rank) * T
-        plan.launch(begin, T, step_hist.data_ptr(), stream.cuda_stream)
-        if world > 1:
-            dist.all_reduce(step_hist)          # RCCL merge of the outcome histograms
+        begin, n = weak_range(s, rank, world, T)
+        plan.launch(begin, n, step_hist.data_ptr(), stream.cuda_stream)
+        merge_histogram(step_hist)              # RCCL merge of the outcome histograms
         hist.add_(step_hist)
 
     for s in range(args.warmup):
@@ -126,12 +126,11 @@ def main():
     for i in range(args.steps):
         s = args.warmup + i
         step_hist.zero_()
-        begin = (s * world + rank) * T
+        begin, n = weak_range(s, rank, world, T)
         ev[i][0].record(stream)
-        plan.launch(begin, T, step_hist.data_ptr(), stream.cuda_stream)
+        plan.launch(begin, n, step_hist.data_ptr(), stream.cuda_stream)
         ev[i][1].record(stream)
-        if world > 1:
-            dist.all_reduce(step_hist)
+        merge_histogram(step_hist)
         hist.add_(step_hist)
     torch.cuda.synchronize()
     if world > 1:
