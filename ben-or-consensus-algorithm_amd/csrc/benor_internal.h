@@ -16,6 +16,7 @@ constexpr uint32_t kStreamInit = 1u;
 
 constexpr int kWavesPerBlock = 4;          // 256-thread workgroups, one trial per wave
 constexpr uint32_t kMaxW = BO_MAX_N / 64;  // u64 words per bit plane at N = 4096
+constexpr int kMaxWSpecialised = 16;       // m <= 1024: fully unrolled W-specialised kernel
 
 struct KParams {
   uint32_t N, F;            // network size, fault parameter
@@ -23,6 +24,7 @@ struct KParams {
   uint32_t W;               // u64 words per plane = ceil(m / 64) = receiver groups
   uint32_t G;               // receiver groups per tally block (template parameter)
   uint32_t nblocks;         // ceil(W / G)
+  uint32_t variant;         // 1: W-specialised kernel (W <= 16), 0: blocked kernel
   uint32_t k_max;
   uint32_t init_mode;       // BO_INIT_RANDOM / BO_INIT_FIXED
   uint32_t hist_len;        // (k_max + 1) * 3 + 1

@@ -30,6 +30,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "benor_internal.h"
 
 namespace benor {
@@ -253,6 +255,220 @@ __global__ void __launch_bounds__(256) benor_lockstep_kernel(KParams p) {
   }
 }
 
+// ------------------------------------------- W-specialised kernel (m <= 1024)
+// For networks of at most 1024 live nodes (W <= 16 receiver groups) the whole
+// round is unrolled at compile time: every receiver group's tally chain is a
+// register, the plane records are read with immediate LDS offsets, a phase's
+// ballots are staged into one VGPR with v_writelane and stored by one
+// ds_write_b32, and the per-group `decided` masks live in SGPRs.  Initial
+// values of TB = 64 / ceil(W/2) consecutive trials of the wave are drawn by
+// one Philox pass (every lane busy) into an LDS ring.
+template <int N, int I = 0>
+struct Unroll {
+  template <class Fn>
+  __device__ __forceinline__ static void run(Fn &&f) {
+    if constexpr (I < N) {
+      f(std::integral_constant<int, I>{});
+      Unroll<N, I + 1>::run(f);
+    }
+  }
+};
+
+// First step of receiver group C's chain: popcount(word) + C.  The distinct
+// immediate per group keeps the groups' (identical, in lockstep) chains from
+// being merged; comparisons are bias-invariant and thresholds add C.
+template <int C>
+__device__ __forceinline__ uint32_t tally_first(uint32_t word) {
+  uint32_t r;
+  asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(word), "i"(C));
+  return r;
+}
+
+template <int W>
+__device__ __forceinline__ void tally_plane(const uint4 *__restrict__ plane, uint32_t (&a0)[W],
+                                            uint32_t (&a1)[W]) {
+  const uint4 q = plane[0];
+  Unroll<W>::run([&](auto gi) {
+    constexpr int g = decltype(gi)::value;
+    a0[g] = tally_first<g>(q.x);
+    a1[g] = tally_first<g>(q.z);
+  });
+#pragma unroll
+  for (int g = 0; g < W; ++g) {
+    a0[g] = tally(q.y, a0[g]);
+    a1[g] = tally(q.w, a1[g]);
+  }
+#pragma unroll
+  for (int w = 1; w < W; ++w) {
+    const uint4 s = plane[w];
+#pragma unroll
+    for (int g = 0; g < W; ++g) {
+      a0[g] = tally(s.x, a0[g]);
+      a1[g] = tally(s.z, a1[g]);
+      a0[g] = tally(s.y, a0[g]);
+      a1[g] = tally(s.w, a1[g]);
+    }
+  }
+}
+
+template <int L>
+__device__ __forceinline__ uint32_t writelane(uint32_t v, uint32_t val) {
+  asm("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(val), "i"(L));
+  return v;
+}
+
+// Stage one group's two ballot words (4 dwords) into lanes 4g..4g+3 of v.
+template <int G>
+__device__ __forceinline__ uint32_t stage4(uint32_t v, uint64_t is0, uint64_t is1) {
+  v = writelane<4 * G + 0>(v, (uint32_t)is0);
+  v = writelane<4 * G + 1>(v, (uint32_t)(is0 >> 32));
+  v = writelane<4 * G + 2>(v, (uint32_t)is1);
+  v = writelane<4 * G + 3>(v, (uint32_t)(is1 >> 32));
+  return v;
+}
+
+template <int W>
+__global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
+  constexpr int NPH = (W + 1) / 2;          // Philox blocks per trial (2 plane words each)
+  constexpr int TB = 64 / NPH;              // trials per init batch
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = threadIdx.x >> 6;
+  const uint32_t m = p.m, F = p.F;
+
+  uint32_t *lhist = reinterpret_cast<uint32_t *>(smem);
+  uint4 *ring = reinterpret_cast<uint4 *>(smem + p.hist_bytes + wv * p.wave_bytes);   // [TB][W]
+  uint4 *X = ring + TB * W;                                                              // [W]
+  uint4 *P = X + W;                                                                      // [W]
+
+  for (uint32_t i = threadIdx.x; i < p.hist_len; i += blockDim.x) lhist[i] = 0u;
+  if (p.init_mode != BO_INIT_RANDOM && lane < (uint32_t)W) ring[lane] = p.init_plane[lane];
+  __syncthreads();
+
+  const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
+  const uint64_t waves_total = (uint64_t)gridDim.x * kWavesPerBlock;
+  const uint64_t tailm = group_mask(W - 1, m);
+  const bool random_init = p.init_mode == BO_INIT_RANDOM;
+
+  for (uint64_t base = (uint64_t)blockIdx.x * kWavesPerBlock + wv; base < p.trial_count;
+       base += waves_total * TB) {
+    // ---- /start (node.ts:167-188): round-1 x planes of TB trials at once.
+    if (random_init) {
+      const uint32_t s = lane / NPH, b = lane - s * NPH;
+      const uint64_t t = base + (uint64_t)s * waves_total;
+      if (s < (uint32_t)TB && t < p.trial_count) {
+        const uint64_t trial = p.trial_begin + t;
+        const uint4 r = philox4x32_10(k0, k1, make_uint4((uint32_t)trial, (uint32_t)(trial >> 32), b, kStreamInit << 24));
+        const uint32_t w0 = 2u * b, w1 = w0 + 1u;
+        const uint64_t v0 = group_mask(w0, m), v1 = group_mask(w1, m);
+        const uint64_t x1a = ((uint64_t)r.y << 32 | r.x) & v0;
+        ring[s * W + w0] = rec(v0 & ~x1a, x1a);
+        if (w1 < (uint32_t)W) {
+          const uint64_t x1b = ((uint64_t)r.w << 32 | r.z) & v1;
+          ring[s * W + w1] = rec(v1 & ~x1b, x1b);
+        }
+      }
+    }
+    for (int s = 0; s < TB; ++s) {
+      const uint64_t t = base + (uint64_t)s * waves_total;
+      if (t >= p.trial_count) break;
+      const uint64_t trial = p.trial_begin + t;
+      const uint32_t tlo = (uint32_t)trial, thi = (uint32_t)(trial >> 32);
+      const uint4 *Xr = random_init ? ring + s * W : ring;
+      uint64_t dec[W];
+#pragma unroll
+      for (int g = 0; g < W; ++g) dec[g] = 0ull;
+      uint32_t R = 0;
+      bool all_dec = false;
+      for (uint32_t r = 1; r <= p.k_max; ++r) {
+        uint32_t a0[W], a1[W];
+        // ---- R-phase ("proposal phase", node.ts:46-82)
+        tally_plane<W>(Xr, a0, a1);
+        uint32_t st = 0;
+        Unroll<W>::run([&](auto gi) {
+          constexpr int g = decltype(gi)::value;
+          const uint64_t vm = (g == W - 1) ? tailm : ~0ull;
+          const uint64_t p0 = ballot(a0[g] > a1[g]) & vm;   // node.ts:63-64
+          const uint64_t p1 = ballot(a1[g] > a0[g]) & vm;   // node.ts:65-66 (else "?")
+          st = stage4<g>(st, p0, p1);
+        });
+        if (lane < 4u * W) reinterpret_cast<uint32_t *>(P)[lane] = st;
+        // ---- P-phase ("voting phase", node.ts:83-158)
+        tally_plane<W>(P, a0, a1);
+        bool done = true;
+        Unroll<W>::run([&](auto gi) {
+          constexpr int g = decltype(gi)::value;
+          const uint64_t vm = (g == W - 1) ? tailm : ~0ull;
+          const uint32_t Fg = F + (uint32_t)g;                        // chain bias g
+          const uint64_t d0 = ballot(a0[g] > Fg) & vm;                 // node.ts:99
+          const uint64_t d1 = ballot(a1[g] > Fg) & vm & ~d0;           // node.ts:102
+          const uint64_t rest = vm & ~(d0 | d1);
+          uint64_t x1 = d1;
+          if (rest) {                                                   // some receiver did not decide
+            const uint64_t ad1 = ballot(a1[g] > a0[g]) & rest;         // node.ts:108-109
+            const uint64_t tie = ballot(a1[g] == a0[g]) & rest;        // node.ts:110-111
+            x1 |= ad1;
+            if (tie) {
+              bool c1 = false;
+              if ((tie >> lane) & 1ull) {
+                const uint32_t node = p.live_ids[g * 64 + lane];
+                const uint4 rr = philox4x32_10(k0, k1, make_uint4(tlo, thi, node, (r & 0x00FFFFFFu) | (kStreamCoin << 24)));
+                c1 = !(rr.x > 0x80000000u);                             // Math.random() > 0.5 ? 0 : 1
+              }
+              x1 |= ballot(c1) & tie;
+            }
+          }
+          st = stage4<g>(st, vm & ~x1, x1);
+          dec[g] |= d0 | d1;
+          done = done && (dec[g] == vm);
+        });
+        if (lane < 4u * W) reinterpret_cast<uint32_t *>(X)[lane] = st;
+        Xr = X;
+        R = r;                                                        // node.ts:147  k = r + 1
+        all_dec = done;                                               // all-decided auto-stop
+        if (all_dec) break;
+      }
+      // ---- outcome
+      bool any0 = false, any1 = false;
+      if (lane < (uint32_t)W) {
+        const uint4 q = Xr[lane];
+        any0 = (q.x | q.y) != 0u;
+        any1 = (q.z | q.w) != 0u;
+      }
+      const bool g0 = __any(any0), g1 = __any(any1);
+      const uint32_t v = (g0 && g1) ? 2u : (g1 ? 1u : 0u);
+      if (lane == 0) {
+        atomicAdd(&lhist[all_dec ? (R * 3u + v) : v], 1u);
+        if (all_dec && v == 2u) atomicAdd(&lhist[p.hist_len - 1u], 1u);
+        if (p.rounds_out) *p.rounds_out = all_dec ? R : 0u;
+      }
+      if (p.node_out) {                                               // GET /getState (node.ts:197-199)
+        Unroll<W>::run([&](auto gi) {
+          constexpr int g = decltype(gi)::value;
+          const uint32_t c = g * 64u + lane;
+          if (c < m) {
+            const uint4 q = Xr[g];
+            const uint64_t x1 = (uint64_t)q.w << 32 | q.z;
+            bo_node_state ns;
+            ns.killed = 0;
+            ns.x = (int8_t)((x1 >> lane) & 1ull);
+            ns.decided = (int8_t)((dec[g] >> lane) & 1ull);
+            ns.pad = 0;
+            ns.k = (int32_t)R + 1;
+            p.node_out[p.live_ids[c]] = ns;
+          }
+        });
+      }
+    }
+  }
+
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < p.hist_len; i += blockDim.x) {
+    const uint32_t c = lhist[i];
+    if (c) atomicAdd(&p.hist[i], (unsigned long long)c);
+  }
+}
+
 // --------------------------------------------------- popcount peak probe
 // Eight independent v_bcnt_u32_b32 chains per lane; the roofline's `peak`
 // is the spec VALU rate, this probe says what the part sustains.
@@ -277,13 +493,23 @@ __global__ void __launch_bounds__(256) popc_peak_kernel(uint32_t *sink, int iter
 // ------------------------------------------------------------ host side
 void plan_geometry(KParams &p) {
   const uint32_t W = p.W;
-  const uint32_t nb = (W + 15u) / 16u;           // blocks of at most 16 groups
-  const uint32_t G = (W + nb - 1u) / nb;         // balanced: padding < nb groups
-  p.G = G;
-  p.nblocks = (W + G - 1u) / G;
   p.hist_len = (p.k_max + 1u) * 3u + 1u;
   p.hist_bytes = ((p.hist_len * 4u) + 15u) & ~15u;
-  p.wave_bytes = W * 32u + p.nblocks * 256u;
+  if (W <= kMaxWSpecialised) {
+    // W-specialised kernel: init ring [TB][W] + X [W] + P [W] records per wave
+    const uint32_t nph = (W + 1u) / 2u, tb = 64u / nph;
+    p.G = W;
+    p.nblocks = 1;
+    p.variant = 1;
+    p.wave_bytes = (tb * W + 2u * W) * 16u;
+  } else {
+    const uint32_t nb = (W + 15u) / 16u;           // blocks of at most 16 groups
+    const uint32_t G = (W + nb - 1u) / nb;         // balanced: padding < nb groups
+    p.G = G;
+    p.nblocks = (W + G - 1u) / G;
+    p.variant = 0;
+    p.wave_bytes = W * 32u + p.nblocks * 256u;
+  }
   p.lds_bytes = p.hist_bytes + kWavesPerBlock * p.wave_bytes;
 }
 
@@ -293,26 +519,29 @@ static hipError_t launch_g(const KParams &p, int grid, hipStream_t s) {
   return hipGetLastError();
 }
 
+template <int W>
+static hipError_t launch_w(const KParams &p, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(benor_lockstep_w_kernel<W>, dim3(grid), dim3(64 * kWavesPerBlock), p.lds_bytes, s, p);
+  return hipGetLastError();
+}
+
+template <int... Is>
+static hipError_t dispatch_w(const KParams &p, int grid, hipStream_t s, std::integer_sequence<int, Is...>) {
+  hipError_t e = hipErrorInvalidValue;
+  ((p.W == (uint32_t)(Is + 1) ? (e = launch_w<Is + 1>(p, grid, s), true) : false) || ...);
+  return e;
+}
+
+template <int... Is>
+static hipError_t dispatch_g(const KParams &p, int grid, hipStream_t s, std::integer_sequence<int, Is...>) {
+  hipError_t e = hipErrorInvalidValue;
+  ((p.G == (uint32_t)(Is + 1) ? (e = launch_g<Is + 1>(p, grid, s), true) : false) || ...);
+  return e;
+}
+
 hipError_t launch_lockstep(const KParams &p, int grid, hipStream_t s) {
-  switch (p.G) {
-    case 1: return launch_g<1>(p, grid, s);
-    case 2: return launch_g<2>(p, grid, s);
-    case 3: return launch_g<3>(p, grid, s);
-    case 4: return launch_g<4>(p, grid, s);
-    case 5: return launch_g<5>(p, grid, s);
-    case 6: return launch_g<6>(p, grid, s);
-    case 7: return launch_g<7>(p, grid, s);
-    case 8: return launch_g<8>(p, grid, s);
-    case 9: return launch_g<9>(p, grid, s);
-    case 10: return launch_g<10>(p, grid, s);
-    case 11: return launch_g<11>(p, grid, s);
-    case 12: return launch_g<12>(p, grid, s);
-    case 13: return launch_g<13>(p, grid, s);
-    case 14: return launch_g<14>(p, grid, s);
-    case 15: return launch_g<15>(p, grid, s);
-    case 16: return launch_g<16>(p, grid, s);
-    default: return hipErrorInvalidValue;
-  }
+  if (p.variant == 1) return dispatch_w(p, grid, s, std::make_integer_sequence<int, kMaxWSpecialised>{});
+  return dispatch_g(p, grid, s, std::make_integer_sequence<int, 16>{});
 }
 
 int lockstep_grid(const KParams &p, int device) {

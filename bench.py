@@ -32,7 +32,11 @@ PKG = os.path.join(ROOT, "ben-or-consensus-algorithm_amd")
 sys.path.insert(0, PKG)
 
 METRIC = "simulated node-rounds/sec at N=1024,F=341, 1–8 GPUs; % of INT/popcount roofline"
-SPEC_PEAK_POPC = 256 * 4 * 32 * 2.4e9      # v_bcnt_u32_b32 lane-ops/s: 256 CU x 4 SIMD32 x 2.4 GHz
+# v_bcnt_u32_b32 issues one wave64 instruction per 4 cycles per SIMD (16 lanes/clk;
+# tools/valu_probe.hip, profiles/r01-v1_valu_probe.txt: 4.15 cyc at full occupancy,
+# vs 2.4-2.5 for v_and_b32 / v_add_u32), so the popcount roofline of the chip is
+# 256 CU x 4 SIMD x 16 lanes x 2.4 GHz.
+SPEC_PEAK_POPC = 256 * 4 * 16 * 2.4e9
 
 
 def parse():
@@ -168,7 +172,7 @@ def main():
         "config": {"workload": f"N={N},F={F} lockstep crash faults, {T} trials per GPU per step, k_max={k_max}",
                    "N": N, "F": F, "live_nodes": m, "trials_per_gpu_per_step": T, "k_max": k_max,
                    "parallelism": f"dp{world} (trial-id sharding, RCCL histogram all-reduce)"},
-        "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": SPEC_PEAK_POPC / 1e12,
+        "roofline": {"bound": "valu (v_bcnt_u32_b32 issue)", "achieved": achieved / 1e12, "peak": SPEC_PEAK_POPC / 1e12,
                      "unit": "Tpopc/s", "frac": achieved / SPEC_PEAK_POPC, "traffic": traffic,
                      "kernel_ms": float(np.mean(kern_ms)), "popc_words_per_node_round": words_per_nr,
                      "peak_probe": (peak_measured / 1e12) if peak_measured else None},

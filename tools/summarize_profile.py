@@ -1,0 +1,77 @@
+"""Summarise a tools/profile.sh run (gpurun_out/prof_<tag>/) into profiles/.
+
+Writes
+  profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (copied)
+  profiles/<tag>_valu_probe.txt     VALU issue-rate probe output (copied)
+  profiles/<tag>_summary.md         PMC counters per launch of the lockstep kernel, derived rates
+  profiles/pmc_traffic.json         HBM bytes per launch (bench.py reads it for roofline.traffic)
+
+HBM bytes follow MI355X_MICROARCH.md §HBM / cdna_hip_programming.md §7:
+FETCH_SIZE and WRITE_SIZE (KiB) come from separate --pmc passes; on gfx950
+FETCH_SIZE reads half the bytes of a wide coalesced stream, so it is doubled
+(an upper bound for this kernel's few narrow reads); WRITE_SIZE is taken as is.
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def pmc_per_dispatch(path, kernel_sub="lockstep"):
+    agg = defaultdict(list)
+    meta = {}
+    for f in glob.glob(os.path.join(path, "pmc*", "*counter_collection.csv")):
+        for r in csv.DictReader(open(f)):
+            if kernel_sub not in r["Kernel_Name"]:
+                continue
+            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+            meta = {k: r[k] for k in ("Kernel_Name", "Grid_Size", "Workgroup_Size", "LDS_Block_Size",
+                                      "VGPR_Count", "SGPR_Count", "Scratch_Size")}
+    return {k: sum(v) / len(v) for k, v in agg.items()}, meta
+
+
+def main(tag, trials, N=1024, F=341):
+    src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    dst = os.path.join(ROOT, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    stats = glob.glob(os.path.join(src, "trace", "*kernel_stats.csv"))
+    if stats:
+        shutil.copy(stats[0], os.path.join(dst, f"{tag}_kernel_stats.csv"))
+    probe = os.path.join(src, "valu_probe.txt")
+    if os.path.exists(probe):
+        shutil.copy(probe, os.path.join(dst, f"{tag}_valu_probe.txt"))
+    c, meta = pmc_per_dispatch(src)
+    m = N - F
+    lines = [f"# Profile {tag}: lockstep kernel, N={N}, F={F}, {trials} trials per launch", ""]
+    lines += [f"- {k}: {v}" for k, v in meta.items()]
+    lines += ["", "| counter | per launch | per trial |", "|---|---|---|"]
+    for k in sorted(c):
+        lines.append(f"| {k} | {c[k]:.6g} | {c[k] / trials:.4g} |")
+    if "SQ_INSTS_VALU" in c:
+        bcnt = 4 * ((m + 31) // 32) * m / 64 * 1.0
+        lines += ["", f"- v_bcnt per trial (algorithmic, 4*ceil(m/32) words x ceil(m/64) groups): "
+                      f"{4 * ((m + 31) // 32) * ((m + 63) // 64)}",
+                  f"- VALU instructions per trial: {c['SQ_INSTS_VALU'] / trials:.1f}"]
+    if "GRBM_GUI_ACTIVE" in c and stats:
+        for r in csv.DictReader(open(stats[0])):
+            if "lockstep" in r["Name"]:
+                avg_ns = float(r["AverageNs"])
+                lines.append(f"- kernel-trace average duration (bench launches): {avg_ns / 1e6:.3f} ms")
+    hbm = None
+    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+        hbm = (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0
+        lines.append(f"- HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, KiB -> B): {hbm:.0f}")
+        json.dump({"N": N, "F": F, "trials": trials, "hbm_bytes_per_launch": hbm,
+                   "fetch_kib": c["FETCH_SIZE"], "write_kib": c["WRITE_SIZE"], "source": f"profiles/{tag}_summary.md"},
+                  open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
+    open(os.path.join(dst, f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 10_000_000)

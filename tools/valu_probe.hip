@@ -1,0 +1,80 @@
+// valu_probe.hip -- issue-rate microbenchmark for the VALU ops the round loop
+// uses (v_bcnt_u32_b32 popcount+accumulate, v_and_b32, v_add_u32), at full
+// occupancy with independent chains.  Prints lane-ops/s and cycles per
+// wave64 instruction per SIMD at the clock the part holds.
+// Build: hipcc --offload-arch=gfx950 -O3 tools/valu_probe.hip -o tools/valu_probe
+#include <hip/hip_runtime.h>
+#include <cstdio>
+
+template <int OP>
+__global__ void __launch_bounds__(256) probe(unsigned *sink, int iters, unsigned seed) {
+  unsigned a[8];
+  const unsigned x = threadIdx.x * 2654435761u + blockIdx.x + seed;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[i] = x + (unsigned)i;
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if (OP == 0) asm volatile("v_bcnt_u32_b32 %0, %1, %0" : "+v"(a[i]) : "v"(x));
+        if (OP == 1) asm volatile("v_add_u32 %0, %1, %0" : "+v"(a[i]) : "v"(x));
+        if (OP == 2) asm volatile("v_and_b32 %0, %1, %0" : "+v"(a[i]) : "v"(x));
+        if (OP == 3) asm volatile("v_fma_f32 %0, %1, %1, %0" : "+v"(a[i]) : "v"(x));
+        if (OP == 4) asm volatile("v_bcnt_u32_b32 %0, %1, %0" : "+v"(a[i]) : "s"(seed));
+        if (OP == 5) asm volatile("v_mov_b32 %0, %1" : "=v"(a[i]) : "s"(seed + i));
+        if (OP == 6) asm volatile("v_writelane_b32 %0, %1, 5" : "+v"(a[i]) : "s"(seed + i));
+        if (OP == 7) asm volatile("v_cmp_gt_u32 vcc, %0, %1" :: "v"(a[i]), "v"(x) : "vcc");
+        if (OP == 8) asm volatile("v_mul_hi_u32 %0, %1, %0" : "+v"(a[i]) : "v"(x));
+      }
+    }
+  }
+  unsigned s = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s ^= a[i];
+  if (s == 0x12345678u) sink[blockIdx.x] = s;
+}
+
+template <int OP>
+void run(const char *name, int cus, int blocks_per_cu) {
+  unsigned *sink;
+  (void)hipMalloc(&sink, sizeof(unsigned) * cus * 64);
+  const int grid = cus * blocks_per_cu, iters = 4096;
+  hipLaunchKernelGGL(probe<OP>, dim3(grid), dim3(256), 0, 0, sink, iters, 1u);
+  (void)hipDeviceSynchronize();
+  hipEvent_t a, b;
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  (void)hipEventRecord(a, 0);
+  const int reps = 10;
+  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(probe<OP>, dim3(grid), dim3(256), 0, 0, sink, iters, 1u);
+  (void)hipEventRecord(b, 0);
+  (void)hipEventSynchronize(b);
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, a, b);
+  const double ops = (double)grid * 256 * iters * 64 * reps;
+  const double rate = ops / (ms * 1e-3);
+  // cycles per wave64 instruction per SIMD at 2.4 GHz nominal
+  const double cyc = (double)cus * 4 * 64 * 2.4e9 / rate;
+  printf("%-24s blocks/CU=%2d  %.2f T lane-ops/s  (%.2f cyc/wave-instr/SIMD @2.4GHz)\n", name, blocks_per_cu,
+         rate / 1e12, cyc);
+  (void)hipFree(sink);
+}
+
+int main() {
+  int cus = 0;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+  printf("CUs: %d\n", cus);
+  for (int bpc : {8}) {
+    run<0>("v_bcnt_u32_b32 (v,v)", cus, bpc);
+    run<4>("v_bcnt_u32_b32 (s,v)", cus, bpc);
+    run<1>("v_add_u32", cus, bpc);
+    run<2>("v_and_b32", cus, bpc);
+    run<3>("v_fma_f32", cus, bpc);
+    run<5>("v_mov_b32 (s)", cus, bpc);
+    run<6>("v_writelane_b32", cus, bpc);
+    run<7>("v_cmp_gt_u32", cus, bpc);
+    run<8>("v_mul_hi_u32", cus, bpc);
+  }
+  return 0;
+}
