@@ -72,187 +72,30 @@ __device__ __forceinline__ uint4 rec(uint64_t is0, uint64_t is1) {
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 
-// Tally of one block of G receiver groups against a plane of W records.
-// a0[g] / a1[g] receive the counts of 0s / 1s (node.ts:56-62, :92-98).
-template <int G>
-__device__ __forceinline__ void tally_block(const uint4 *__restrict__ plane, uint32_t W,
-                                            uint32_t (&a0)[G], uint32_t (&a1)[G]) {
-#pragma unroll
-  for (int g = 0; g < G; ++g) { a0[g] = (uint32_t)g; a1[g] = (uint32_t)g; }
-  uint32_t w = 0;
-  for (; w + 1 < W; w += 2) {
-    const uint4 q = plane[w];
-    const uint4 s = plane[w + 1];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      a0[g] = tally(q.x, a0[g]);
-      a1[g] = tally(q.z, a1[g]);
-      a0[g] = tally(q.y, a0[g]);
-      a1[g] = tally(q.w, a1[g]);
-    }
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      a0[g] = tally(s.x, a0[g]);
-      a1[g] = tally(s.z, a1[g]);
-      a0[g] = tally(s.y, a0[g]);
-      a1[g] = tally(s.w, a1[g]);
-    }
+
+// Coins of the tied receivers of one group (node.ts:111).  The key words are
+// laundered through an empty asm so that Philox's ten round keys are not
+// hoisted out of the round loop into permanently live SGPRs.
+__device__ __forceinline__ uint64_t coin_ballot(uint32_t k0, uint32_t k1, uint32_t tlo, uint32_t thi,
+                                             const uint32_t *__restrict__ live_ids, uint32_t group,
+                                             uint32_t round, uint64_t tie) {
+  const uint32_t lane = threadIdx.x & 63u;
+  asm volatile("" : "+s"(k0), "+s"(k1));
+  bool c1 = false;
+  if ((tie >> lane) & 1ull) {
+    const uint32_t node = live_ids[group * 64u + lane];
+    const uint4 rr = philox4x32_10(k0, k1, make_uint4(tlo, thi, node, (round & 0x00FFFFFFu) | (kStreamCoin << 24)));
+    c1 = !(rr.x > 0x80000000u);                 // Math.random() > 0.5 ? 0 : 1
   }
-  if (w < W) {
-    const uint4 q = plane[w];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      a0[g] = tally(q.x, a0[g]);
-      a1[g] = tally(q.z, a1[g]);
-      a0[g] = tally(q.y, a0[g]);
-      a1[g] = tally(q.w, a1[g]);
-    }
-  }
-#pragma unroll
-  for (int g = 0; g < G; ++g) { a0[g] -= (uint32_t)g; a1[g] -= (uint32_t)g; }
+  return ballot(c1) & tie;
 }
 
-// ------------------------------------------------------------ the kernel
-template <int G>
-__global__ void __launch_bounds__(256) benor_lockstep_kernel(KParams p) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wv = threadIdx.x >> 6;
-  const uint32_t W = p.W, m = p.m, F = p.F;
-
-  uint32_t *lhist = reinterpret_cast<uint32_t *>(smem);
-  unsigned char *wbase = smem + p.hist_bytes + wv * p.wave_bytes;
-  uint4 *X = reinterpret_cast<uint4 *>(wbase);          // x planes      [W]
-  uint4 *P = X + W;                                      // proposal planes [W]
-  uint32_t *D = reinterpret_cast<uint32_t *>(P + W);    // decided bits  [nblocks][64]
-
-  for (uint32_t i = threadIdx.x; i < p.hist_len; i += blockDim.x) lhist[i] = 0u;
-  __syncthreads();
-
-  const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
-  const uint64_t waves_total = (uint64_t)gridDim.x * kWavesPerBlock;
-  const uint32_t nb = p.nblocks;
-
-  for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + wv; t < p.trial_count; t += waves_total) {
-    const uint64_t trial = p.trial_begin + t;
-    const uint32_t tlo = (uint32_t)trial, thi = (uint32_t)(trial >> 32);
-
-    // ---- /start (node.ts:167-188): round-1 x planes of the live nodes.
-    if (p.init_mode == BO_INIT_RANDOM) {
-      const uint32_t nphil = (W + 1u) >> 1;   // one Philox block = two u64 plane words
-      if (lane < nphil) {
-        const uint4 r = philox4x32_10(k0, k1, make_uint4(tlo, thi, lane, kStreamInit << 24));
-        const uint32_t w0 = 2u * lane, w1 = w0 + 1u;
-        const uint64_t v0 = group_mask(w0, m), v1 = group_mask(w1, m);
-        const uint64_t x1a = ((uint64_t)r.y << 32 | r.x) & v0;
-        X[w0] = rec(v0 & ~x1a, x1a);
-        if (w1 < W) {
-          const uint64_t x1b = ((uint64_t)r.w << 32 | r.z) & v1;
-          X[w1] = rec(v1 & ~x1b, x1b);
-        }
-      }
-    } else {
-      for (uint32_t w = lane; w < W; w += 64u) X[w] = p.init_plane[w];
-    }
-    for (uint32_t b = 0; b < nb; ++b) D[b * 64u + lane] = 0u;
-
-    uint32_t R = 0;
-    bool all_dec = false;
-    for (uint32_t r = 1; r <= p.k_max; ++r) {
-      // ---- R-phase ("proposal phase", node.ts:46-82): tally x, propose.
-      for (uint32_t b = 0; b < nb; ++b) {
-        uint32_t a0[G], a1[G];
-        tally_block<G>(X, W, a0, a1);
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-          const uint32_t j = b * G + g;
-          if (j < W) {
-            const uint64_t vm = group_mask(j, m);
-            const uint64_t p0 = ballot(a0[g] > a1[g]) & vm;   // node.ts:63-64
-            const uint64_t p1 = ballot(a1[g] > a0[g]) & vm;   // node.ts:65-66 (else "?")
-            if (lane == 0) P[j] = rec(p0, p1);
-          }
-        }
-      }
-      // ---- P-phase ("voting phase", node.ts:83-158): tally proposals,
-      //      decide on > F, adopt the strict majority, else flip a coin.
-      bool lane_done = true;
-      for (uint32_t b = 0; b < nb; ++b) {
-        uint32_t a0[G], a1[G];
-        tally_block<G>(P, W, a0, a1);
-        uint32_t db = D[b * 64u + lane];
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-          const uint32_t j = b * G + g;
-          if (j < W) {
-            const uint64_t vm = group_mask(j, m);
-            const bool d0l = a0[g] > F;                          // node.ts:99
-            const bool d1l = a1[g] > F;                          // node.ts:102
-            const uint64_t d0 = ballot(d0l) & vm;
-            const uint64_t d1 = ballot(d1l) & vm & ~d0;
-            const uint64_t rest = vm & ~(d0 | d1);
-            const uint64_t ad0 = ballot(a0[g] > a1[g]) & rest;   // node.ts:106-107
-            const uint64_t ad1 = ballot(a1[g] > a0[g]) & rest;   // node.ts:108-109
-            const uint64_t tie = rest & ~(ad0 | ad1);
-            uint64_t x1 = d1 | ad1;
-            if (tie) {                                           // node.ts:111
-              bool c1 = false;
-              if ((tie >> lane) & 1ull) {
-                const uint32_t node = p.live_ids[j * 64u + lane];
-                const uint4 rr = philox4x32_10(k0, k1, make_uint4(tlo, thi, node, (r & 0x00FFFFFFu) | (kStreamCoin << 24)));
-                c1 = !(rr.x > 0x80000000u);                      // Math.random() > 0.5 ? 0 : 1
-              }
-              x1 |= ballot(c1) & tie;
-            }
-            if (lane == 0) X[j] = rec(vm & ~x1, x1);
-            if (d0l || d1l) db |= (1u << g);
-            const bool valid = (j * 64u + lane) < m;
-            lane_done = lane_done && (!valid || ((db >> g) & 1u));
-          }
-        }
-        D[b * 64u + lane] = db;
-      }
-      R = r;                                                    // node.ts:147  k = r + 1
-      all_dec = __all(lane_done);                               // all-decided auto-stop (node.ts:116-145)
-      if (all_dec) break;
-    }
-
-    // ---- outcome: common final x (agreement check) and histogram bin.
-    bool any0 = false, any1 = false;
-    for (uint32_t w = lane; w < W; w += 64u) {
-      const uint4 q = X[w];
-      any0 = any0 || ((q.x | q.y) != 0u);
-      any1 = any1 || ((q.z | q.w) != 0u);
-    }
-    const bool g0 = __any(any0), g1 = __any(any1);
-    const uint32_t v = (g0 && g1) ? 2u : (g1 ? 1u : 0u);
-    if (lane == 0) {
-      const uint32_t bin = all_dec ? (R * 3u + v) : v;
-      atomicAdd(&lhist[bin], 1u);
-      if (all_dec && v == 2u) atomicAdd(&lhist[p.hist_len - 1u], 1u);
-      if (p.rounds_out) *p.rounds_out = all_dec ? R : 0u;
-    }
-    if (p.node_out) {                                           // GET /getState (node.ts:197-199)
-      for (uint32_t c = lane; c < m; c += 64u) {
-        const uint4 q = X[c >> 6];
-        const uint64_t x1 = (uint64_t)q.w << 32 | q.z;
-        const uint32_t db = D[((c >> 6) / G) * 64u + (c & 63u)];
-        bo_node_state s;
-        s.killed = 0;
-        s.x = (int8_t)((x1 >> (c & 63u)) & 1ull);
-        s.decided = (int8_t)((db >> ((c >> 6) % G)) & 1u);
-        s.pad = 0;
-        s.k = (int32_t)R + 1;
-        p.node_out[p.live_ids[c]] = s;
-      }
-    }
-  }
-
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < p.hist_len; i += blockDim.x) {
-    const uint32_t c = lhist[i];
-    if (c) atomicAdd(&p.hist[i], (unsigned long long)c);
-  }
+// A call's result comes back in VGPRs; the ballot is wave-uniform, so move it
+// to SGPRs for the mask arithmetic that follows.
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+  return (uint64_t)hi << 32 | lo;
 }
 
 // ------------------------------------------- W-specialised kernel (m <= 1024)
@@ -358,7 +201,9 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
       const uint64_t t = base + (uint64_t)s * waves_total;
       if (s < (uint32_t)TB && t < p.trial_count) {
         const uint64_t trial = p.trial_begin + t;
-        const uint4 r = philox4x32_10(k0, k1, make_uint4((uint32_t)trial, (uint32_t)(trial >> 32), b, kStreamInit << 24));
+        uint32_t kk0 = k0, kk1 = k1;
+        asm volatile("" : "+s"(kk0), "+s"(kk1));   // keep the round keys out of long-lived SGPRs
+        const uint4 r = philox4x32_10(kk0, kk1, make_uint4((uint32_t)trial, (uint32_t)(trial >> 32), b, kStreamInit << 24));
         const uint32_t w0 = 2u * b, w1 = w0 + 1u;
         const uint64_t v0 = group_mask(w0, m), v1 = group_mask(w1, m);
         const uint64_t x1a = ((uint64_t)r.y << 32 | r.x) & v0;
@@ -408,15 +253,7 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
             const uint64_t ad1 = ballot(a1[g] > a0[g]) & rest;         // node.ts:108-109
             const uint64_t tie = ballot(a1[g] == a0[g]) & rest;        // node.ts:110-111
             x1 |= ad1;
-            if (tie) {
-              bool c1 = false;
-              if ((tie >> lane) & 1ull) {
-                const uint32_t node = p.live_ids[g * 64 + lane];
-                const uint4 rr = philox4x32_10(k0, k1, make_uint4(tlo, thi, node, (r & 0x00FFFFFFu) | (kStreamCoin << 24)));
-                c1 = !(rr.x > 0x80000000u);                             // Math.random() > 0.5 ? 0 : 1
-              }
-              x1 |= ballot(c1) & tie;
-            }
+            if (tie) x1 |= (coin_ballot(k0, k1, tlo, thi, p.live_ids, g, r, tie));   // node.ts:111
           }
           st = stage4<g>(st, vm & ~x1, x1);
           dec[g] |= d0 | d1;
@@ -469,6 +306,206 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
   }
 }
 
+
+// --------------------------------------------- blocked kernel (1024 < m <= 4096)
+// Receiver groups are processed in NB blocks of G (NB = ceil(W/16), G =
+// ceil(W/NB), padding < NB groups); the record loop over the W plane words is
+// a runtime loop.  Per-lane `decided` bits live in registers (one word per
+// block).  Otherwise as the W-specialised kernel.
+template <int G>
+__device__ __forceinline__ void tally_groups(const uint4 *__restrict__ plane, uint32_t W, uint32_t (&a0)[G],
+                                             uint32_t (&a1)[G]) {
+  const uint4 q = plane[0];
+  Unroll<G>::run([&](auto gi) {
+    constexpr int g = decltype(gi)::value;
+    a0[g] = tally_first<g>(q.x);
+    a1[g] = tally_first<g>(q.z);
+  });
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    a0[g] = tally(q.y, a0[g]);
+    a1[g] = tally(q.w, a1[g]);
+  }
+  uint32_t w = 1;
+  for (; w + 1 < W; w += 2) {
+    const uint4 u = plane[w];
+    const uint4 v = plane[w + 1];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      a0[g] = tally(u.x, a0[g]);
+      a1[g] = tally(u.z, a1[g]);
+      a0[g] = tally(u.y, a0[g]);
+      a1[g] = tally(u.w, a1[g]);
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      a0[g] = tally(v.x, a0[g]);
+      a1[g] = tally(v.z, a1[g]);
+      a0[g] = tally(v.y, a0[g]);
+      a1[g] = tally(v.w, a1[g]);
+    }
+  }
+  if (w < W) {
+    const uint4 u = plane[w];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      a0[g] = tally(u.x, a0[g]);
+      a1[g] = tally(u.z, a1[g]);
+      a0[g] = tally(u.y, a0[g]);
+      a1[g] = tally(u.w, a1[g]);
+    }
+  }
+}
+
+template <int G>
+__global__ void __launch_bounds__(256) benor_lockstep_blocked_kernel(KParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = threadIdx.x >> 6;
+  const uint32_t m = p.m, F = p.F, W = p.W, NB = p.nblocks;
+  const uint32_t nph = (W + 1u) >> 1, tb = 64u / nph;
+  const uint32_t tail_n = m - (W - 1u) * 64u;          // live receivers in the last group
+
+  uint32_t *lhist = reinterpret_cast<uint32_t *>(smem);
+  uint4 *ring = reinterpret_cast<uint4 *>(smem + p.hist_bytes + wv * p.wave_bytes);   // [tb][W]
+  uint4 *X = ring + tb * W;                                                              // [NB*G]
+  uint4 *P = X + NB * G;                                                                 // [NB*G]
+  uint32_t *D = reinterpret_cast<uint32_t *>(P + NB * G);                               // [NB][64] decided bits
+
+  for (uint32_t i = threadIdx.x; i < p.hist_len; i += blockDim.x) lhist[i] = 0u;
+  if (p.init_mode != BO_INIT_RANDOM)
+    for (uint32_t w = lane; w < W; w += 64u) ring[w] = p.init_plane[w];
+  __syncthreads();
+
+  const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
+  const uint64_t waves_total = (uint64_t)gridDim.x * kWavesPerBlock;
+  const bool random_init = p.init_mode == BO_INIT_RANDOM;
+
+  for (uint64_t base = (uint64_t)blockIdx.x * kWavesPerBlock + wv; base < p.trial_count;
+       base += waves_total * tb) {
+    if (random_init) {                       // /start (node.ts:167-188), tb trials per Philox pass
+      const uint32_t s = lane / nph, bk = lane - s * nph;
+      const uint64_t t = base + (uint64_t)s * waves_total;
+      if (s < tb && t < p.trial_count) {
+        const uint64_t trial = p.trial_begin + t;
+        uint32_t kk0 = k0, kk1 = k1;
+        asm volatile("" : "+s"(kk0), "+s"(kk1));   // keep the round keys out of long-lived SGPRs
+        const uint4 r = philox4x32_10(kk0, kk1, make_uint4((uint32_t)trial, (uint32_t)(trial >> 32), bk, kStreamInit << 24));
+        const uint32_t w0 = 2u * bk, w1 = w0 + 1u;
+        const uint64_t v0 = group_mask(w0, m), v1 = group_mask(w1, m);
+        const uint64_t x1a = ((uint64_t)r.y << 32 | r.x) & v0;
+        ring[s * W + w0] = rec(v0 & ~x1a, x1a);
+        if (w1 < W) {
+          const uint64_t x1b = ((uint64_t)r.w << 32 | r.z) & v1;
+          ring[s * W + w1] = rec(v1 & ~x1b, x1b);
+        }
+      }
+    }
+    for (uint32_t s = 0; s < tb; ++s) {
+      const uint64_t t = base + (uint64_t)s * waves_total;
+      if (t >= p.trial_count) break;
+      const uint64_t trial = p.trial_begin + t;
+      const uint32_t tlo = (uint32_t)trial, thi = (uint32_t)(trial >> 32);
+      const uint4 *Xr = random_init ? ring + s * W : ring;
+      for (uint32_t b = 0; b < NB; ++b) D[b * 64u + lane] = 0u;
+      uint32_t R = 0;
+      bool all_dec = false;
+      for (uint32_t r = 1; r <= p.k_max; ++r) {
+        // ---- R-phase ("proposal phase", node.ts:46-82)
+#pragma nounroll
+        for (uint32_t b = 0; b < NB; ++b) {
+          uint32_t a0[G], a1[G];
+          tally_groups<G>(Xr, W, a0, a1);
+          uint32_t st = 0;
+          Unroll<G>::run([&](auto gi) {
+            constexpr int g = decltype(gi)::value;
+            const uint64_t vm = group_mask(b * G + g, m);
+            const uint64_t p0 = ballot(a0[g] > a1[g]) & vm;   // node.ts:63-64
+            const uint64_t p1 = ballot(a1[g] > a0[g]) & vm;   // node.ts:65-66 (else "?")
+            st = stage4<g>(st, p0, p1);
+          });
+          if (lane < 4u * G) reinterpret_cast<uint32_t *>(P + b * G)[lane] = st;
+        }
+        // ---- P-phase ("voting phase", node.ts:83-158)
+        bool done = true;
+#pragma nounroll
+        for (uint32_t b = 0; b < NB; ++b) {
+          uint32_t a0[G], a1[G];
+          tally_groups<G>(P, W, a0, a1);
+          uint32_t st = 0, dbb = D[b * 64u + lane];
+          Unroll<G>::run([&](auto gi) {
+            constexpr int g = decltype(gi)::value;
+            const uint64_t vm = group_mask(b * G + g, m);
+            const uint32_t Fg = F + (uint32_t)g;
+            const bool d0l = a0[g] > Fg, d1l = a1[g] > Fg;           // node.ts:99, :102
+            const uint64_t d0 = ballot(d0l) & vm;
+            const uint64_t d1 = ballot(d1l) & vm & ~d0;
+            const uint64_t rest = vm & ~(d0 | d1);
+            uint64_t x1 = d1;
+            if (rest) {
+              const uint64_t ad1 = ballot(a1[g] > a0[g]) & rest;     // node.ts:108-109
+              const uint64_t tie = ballot(a1[g] == a0[g]) & rest;    // node.ts:110-111
+              x1 |= ad1;
+              if (tie) x1 |= (coin_ballot(k0, k1, tlo, thi, p.live_ids, b * G + g, r, tie));   // node.ts:111
+            }
+            st = stage4<g>(st, vm & ~x1, x1);
+            dbb = (d0l || d1l) ? (dbb | (1u << g)) : dbb;
+          });
+          D[b * 64u + lane] = dbb;
+          if (lane < 4u * G) reinterpret_cast<uint32_t *>(X + b * G)[lane] = st;
+          // groups of this block that hold live receivers for this lane
+          const uint32_t j0 = b * G;
+          uint32_t expect = 0u;
+          if (j0 + 1u < W) {
+            const uint32_t nfull = (W - 1u - j0) < (uint32_t)G ? (W - 1u - j0) : (uint32_t)G;
+            expect = nfull >= 32u ? ~0u : ((1u << nfull) - 1u);
+          }
+          if (W - 1u >= j0 && W - 1u < j0 + G && lane < tail_n) expect |= 1u << (W - 1u - j0);
+          done = done && __all((dbb & expect) == expect);
+        }
+        Xr = X;
+        R = r;
+        all_dec = done;
+        if (all_dec) break;
+      }
+      // ---- outcome
+      bool any0 = false, any1 = false;
+      if (lane < W) {
+        const uint4 q = Xr[lane];
+        any0 = (q.x | q.y) != 0u;
+        any1 = (q.z | q.w) != 0u;
+      }
+      const bool g0 = __any(any0), g1 = __any(any1);
+      const uint32_t v = (g0 && g1) ? 2u : (g1 ? 1u : 0u);
+      if (lane == 0) {
+        atomicAdd(&lhist[all_dec ? (R * 3u + v) : v], 1u);
+        if (all_dec && v == 2u) atomicAdd(&lhist[p.hist_len - 1u], 1u);
+        if (p.rounds_out) *p.rounds_out = all_dec ? R : 0u;
+      }
+      if (p.node_out) {
+        for (uint32_t c = lane; c < m; c += 64u) {
+          const uint32_t j = c >> 6;
+          const uint4 q = Xr[j];
+          const uint64_t x1 = (uint64_t)q.w << 32 | q.z;
+          bo_node_state ns;
+          ns.killed = 0;
+          ns.x = (int8_t)((x1 >> lane) & 1ull);
+          ns.decided = (int8_t)((D[(j / G) * 64u + lane] >> (j % G)) & 1u);
+          ns.pad = 0;
+          ns.k = (int32_t)R + 1;
+          p.node_out[p.live_ids[c]] = ns;
+        }
+      }
+    }
+  }
+
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < p.hist_len; i += blockDim.x) {
+    const uint32_t c = lhist[i];
+    if (c) atomicAdd(&p.hist[i], (unsigned long long)c);
+  }
+}
+
 // --------------------------------------------------- popcount peak probe
 // Eight independent v_bcnt_u32_b32 chains per lane; the roofline's `peak`
 // is the spec VALU rate, this probe says what the part sustains.
@@ -495,9 +532,8 @@ void plan_geometry(KParams &p) {
   const uint32_t W = p.W;
   p.hist_len = (p.k_max + 1u) * 3u + 1u;
   p.hist_bytes = ((p.hist_len * 4u) + 15u) & ~15u;
-  if (W <= kMaxWSpecialised) {
-    // W-specialised kernel: init ring [TB][W] + X [W] + P [W] records per wave
-    const uint32_t nph = (W + 1u) / 2u, tb = 64u / nph;
+  const uint32_t nph = (W + 1u) / 2u, tb = 64u / nph;   // init ring: tb trials per Philox pass
+  if (W <= (uint32_t)kMaxWSpecialised) {
     p.G = W;
     p.nblocks = 1;
     p.variant = 1;
@@ -506,17 +542,11 @@ void plan_geometry(KParams &p) {
     const uint32_t nb = (W + 15u) / 16u;           // blocks of at most 16 groups
     const uint32_t G = (W + nb - 1u) / nb;         // balanced: padding < nb groups
     p.G = G;
-    p.nblocks = (W + G - 1u) / G;
+    p.nblocks = nb;
     p.variant = 0;
-    p.wave_bytes = W * 32u + p.nblocks * 256u;
+    p.wave_bytes = (tb * W + 2u * G * nb) * 16u + nb * 256u;
   }
   p.lds_bytes = p.hist_bytes + kWavesPerBlock * p.wave_bytes;
-}
-
-template <int G>
-static hipError_t launch_g(const KParams &p, int grid, hipStream_t s) {
-  hipLaunchKernelGGL(benor_lockstep_kernel<G>, dim3(grid), dim3(64 * kWavesPerBlock), p.lds_bytes, s, p);
-  return hipGetLastError();
 }
 
 template <int W>
@@ -525,23 +555,30 @@ static hipError_t launch_w(const KParams &p, int grid, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int... Is>
-static hipError_t dispatch_w(const KParams &p, int grid, hipStream_t s, std::integer_sequence<int, Is...>) {
-  hipError_t e = hipErrorInvalidValue;
-  ((p.W == (uint32_t)(Is + 1) ? (e = launch_w<Is + 1>(p, grid, s), true) : false) || ...);
-  return e;
+template <int G>
+static hipError_t launch_b(const KParams &p, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(benor_lockstep_blocked_kernel<G>, dim3(grid), dim3(64 * kWavesPerBlock), p.lds_bytes, s, p);
+  return hipGetLastError();
 }
 
 template <int... Is>
-static hipError_t dispatch_g(const KParams &p, int grid, hipStream_t s, std::integer_sequence<int, Is...>) {
+static hipError_t dispatch_w(const KParams &p, int grid, hipStream_t s, std::integer_sequence<int, Is...>) {
   hipError_t e = hipErrorInvalidValue;
-  ((p.G == (uint32_t)(Is + 1) ? (e = launch_g<Is + 1>(p, grid, s), true) : false) || ...);
+  (void)((p.W == (uint32_t)(Is + 1) ? (e = launch_w<Is + 1>(p, grid, s), true) : false) || ...);
+  return e;
+}
+
+// W in 17..64: G = ceil(W / ceil(W/16)) in 9..16
+template <int... Is>
+static hipError_t dispatch_b(const KParams &p, int grid, hipStream_t s, std::integer_sequence<int, Is...>) {
+  hipError_t e = hipErrorInvalidValue;
+  (void)((p.G == (uint32_t)(Is + 9) ? (e = launch_b<Is + 9>(p, grid, s), true) : false) || ...);
   return e;
 }
 
 hipError_t launch_lockstep(const KParams &p, int grid, hipStream_t s) {
   if (p.variant == 1) return dispatch_w(p, grid, s, std::make_integer_sequence<int, kMaxWSpecialised>{});
-  return dispatch_g(p, grid, s, std::make_integer_sequence<int, 16>{});
+  return dispatch_b(p, grid, s, std::make_integer_sequence<int, 8>{});
 }
 
 int lockstep_grid(const KParams &p, int device) {

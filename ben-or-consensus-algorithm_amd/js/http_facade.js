@@ -1,0 +1,107 @@
+'use strict';
+// HTTP facade: the reference's per-node routes, wire-compatible, served from
+// the simulated network state (SURVEY §8f #1).  With it, the reference's
+// src/nodes/consensus.ts (fetch GET /start, /stop on 3000 + i) and
+// __test__/tests/utils.ts (fetch GET /getState) work unchanged; only
+// src/index.ts's launchNetwork is swapped for the one below.
+//
+// Routes per node i on port basePort + i (node.ts:33-199):
+//   GET  /status    500 "faulty" | 200 "live"                    node.ts:33-39
+//   GET  /getState  200 NodeState JSON                           node.ts:197-199
+//   GET  /start     200 {"message":"Algorithm started"}          node.ts:167-188
+//   GET  /stop      200 "killed"                                 node.ts:191-194
+//   POST /message   200 {"message":"Message received"}           node.ts:43-163
+// The round loop itself runs on the GPU (one kernel launch) once every running
+// node has received /start -- the point at which, in the reference, all live
+// nodes have broadcast their round-1 proposals.  Until then a started node
+// reports k = 1 (node.ts:172).  Messages POSTed from outside are acknowledged
+// and not simulated.  Unlike the reference (node.ts:45,161), killed nodes
+// answer /message with 500 "faulty" instead of never answering.
+const http = require('http');
+const path = require('path');
+const addon = require(path.join(__dirname, 'benor.node'));
+
+const BASE_NODE_PORT = 3000;   // src/config.ts:1
+
+async function launchNetwork(N, F, initialValues, faultyList, options = {}) {
+  const basePort = options.basePort !== undefined ? options.basePort : BASE_NODE_PORT;
+  const kMax = options.kMax !== undefined ? options.kMax : 64;
+  const handle = addon.networkCreate(N, F, initialValues, faultyList);   // launchNodes.ts:10-13 errors
+  const net = {
+    handle, N, started: new Array(N).fill(false), running: null, ran: false, seed: options.seed,
+  };
+
+  const runningNodes = () => {
+    const r = [];
+    for (let i = 0; i < N; i++) if (!addon.getState(handle, i).killed) r.push(i);
+    return r;
+  };
+
+  function maybeRun() {
+    if (net.running || net.ran) return net.running;
+    const live = runningNodes();
+    if (live.length === 0 || !live.every((i) => net.started[i])) return null;
+    let seed = net.seed;
+    if (seed === undefined) {
+      seed = (BigInt(Math.floor(Math.random() * 2 ** 32)) << 32n) | BigInt(Math.floor(Math.random() * 2 ** 32));
+    }
+    net.running = addon.networkStart(handle, BigInt(seed), kMax).then(() => {
+      net.ran = true;
+      net.running = null;
+    });
+    return net.running;
+  }
+
+  function state(i) {
+    const s = addon.getState(handle, i);
+    if (!net.ran && net.started[i] && !s.killed) s.k = 1;   // node.ts:172, before the run lands
+    return s;
+  }
+
+  function send(res, code, body, json) {
+    const data = json ? JSON.stringify(body) : String(body);
+    res.writeHead(code, { 'Content-Type': json ? 'application/json; charset=utf-8' : 'text/html; charset=utf-8' });
+    res.end(data);
+  }
+
+  function handler(i) {
+    return (req, res) => {
+      const url = req.url.split('?')[0];
+      if (req.method === 'GET' && url === '/status') {
+        return addon.status(handle, i) === 500 ? send(res, 500, 'faulty') : send(res, 200, 'live');
+      }
+      if (req.method === 'GET' && url === '/getState') return send(res, 200, state(i), true);
+      if (req.method === 'GET' && url === '/stop') {
+        addon.nodeStop(handle, i);
+        return send(res, 200, 'killed');
+      }
+      if (req.method === 'GET' && url === '/start') {
+        if (!addon.getState(handle, i).killed) net.started[i] = true;
+        const p = maybeRun();
+        const reply = () => send(res, 200, { message: 'Algorithm started' }, true);
+        // respond once the round loop has landed, so a caller that polls
+        // /getState right after startConsensus sees final states
+        if (p) p.then(reply, (e) => send(res, 500, { message: String(e && e.message) }, true));
+        else reply();
+        return undefined;
+      }
+      if (req.method === 'POST' && url === '/message') {
+        req.resume();
+        return addon.getState(handle, i).killed ? send(res, 500, 'faulty')
+          : send(res, 200, { message: 'Message received' }, true);
+      }
+      return send(res, 404, 'not found');
+    };
+  }
+
+  const servers = [];
+  await Promise.all(Array.from({ length: N }, (_, i) => new Promise((resolve, reject) => {
+    const srv = http.createServer(handler(i));
+    srv.on('error', reject);
+    srv.listen(basePort + i, () => resolve());
+    servers[i] = srv;
+  })));
+  return servers;
+}
+
+module.exports = { BASE_NODE_PORT, launchNetwork };

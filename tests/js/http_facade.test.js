@@ -1,0 +1,101 @@
+'use strict';
+// The reference suite's HTTP-level interactions against the HTTP facade
+// (js/http_facade.js): the same routes, ports and JSON the reference's
+// consensus.ts and __test__/tests/utils.ts use, driven with Node's http
+// module (Node 12 has no global fetch).  Usage: node http_facade.test.js [setup|all]
+const path = require('path');
+const http = require('http');
+const assert = require('assert');
+const facade = require(path.join(__dirname, '..', '..', 'ben-or-consensus-algorithm_amd', 'js', 'http_facade.js'));
+
+const only = process.argv[2] || 'all';
+const BASE = Number(process.env.BENOR_TEST_PORT || 3100);
+const delay = (ms) => new Promise((r) => setTimeout(r, ms));
+
+function get(port, route) {
+  return new Promise((resolve, reject) => {
+    http.get({ host: '127.0.0.1', port, path: route }, (res) => {
+      let body = '';
+      res.on('data', (c) => { body += c; });
+      res.on('end', () => resolve({ status: res.statusCode, body }));
+    }).on('error', reject);
+  });
+}
+const startConsensus = async (N) => { for (let i = 0; i < N; i++) await get(BASE + i, '/start'); };   // consensus.ts:3-8
+const stopConsensus = async (N) => { for (let i = 0; i < N; i++) await get(BASE + i, '/stop'); };     // consensus.ts:10-15
+const getNodesState = (N) => Promise.all(Array.from({ length: N }, (_, i) =>
+  get(BASE + i, '/getState').then((r) => JSON.parse(r.body))));                                      // utils.ts:14-20
+const reachedFinality = (states) => states.find((el) => el.decided === false) === undefined;          // utils.ts:22-24
+const closeAll = (servers) => Promise.all(servers.map((s) => new Promise((r) => s.close(r))));
+
+const tests = [];
+const it = (name, group, fn) => tests.push({ name, group, fn });
+
+async function withNet(fa, init, fn) {
+  const servers = await facade.launchNetwork(fa.length, fa.filter((e) => e === true).length, init, fa,
+    { basePort: BASE, seed: 0x5EEDn });
+  try { await fn(servers); } finally { await stopConsensus(fa.length); await closeAll(servers); }
+}
+
+it('setup: status over HTTP (benorconsensus.test.ts:45-118)', 'setup', async () => {
+  for (const fa of [[true, false, false], [true, false, false, false, false, true, false, false, false, false]]) {
+    await withNet(fa, new Array(fa.length).fill(1), async () => {
+      await delay(20);
+      for (let i = 0; i < fa.length; i++) {
+        const r = await get(BASE + i, '/status');
+        if (fa[i]) { assert.strictEqual(r.status, 500); assert.strictEqual(r.body, 'faulty'); }
+        else assert.strictEqual(r.body, 'live');
+      }
+    });
+  }
+});
+
+it('setup: getState JSON and /stop', 'setup', async () => {
+  await withNet([true, false, false], [1, 0, '?'], async () => {
+    const st = await getNodesState(3);
+    assert.deepStrictEqual(st[0], { killed: true, x: null, decided: null, k: null });
+    assert.deepStrictEqual(st[2], { killed: false, x: '?', decided: false, k: 0 });
+    const r = await get(BASE + 1, '/stop');
+    assert.strictEqual(r.body, 'killed');
+    assert.strictEqual((await get(BASE + 1, '/status')).status, 500);
+  });
+});
+
+const finality = [
+  ['Unanimous Agreement', [false, false, false, false, false], [1, 1, 1, 1, 1], 'x1'],
+  ['Simple Majority', [false, false, false, false, true], [1, 1, 1, 0, 0], 'x1'],
+  ['Fault Tolerance Threshold', [true, true, true, true, false, false, false, false, false], [0, 0, 1, 1, 1, 0, 0, 1, 1], 'agree'],
+  ['Exceeding Fault Tolerance', [true, true, true, true, true, false, false, false, false, false], [0, 0, 1, 1, 1, 0, 0, 1, 1, 0], 'none'],
+  ['No Faulty Nodes', [false, false, false, false, false], [0, 1, 0, 1, 1], 'x1'],
+  ['One node', [false], [1], 'x1'],
+];
+for (const [name, fa, init, kind] of finality) {
+  it(`Finality over HTTP - ${name}`, 'gpu', async () => {
+    await withNet(fa, init, async () => {
+      await startConsensus(fa.length);
+      const t = Date.now();
+      let states = await getNodesState(fa.length);
+      while (Date.now() - t < 2000 && !reachedFinality(states)) { await delay(200); states = await getNodesState(fa.length); }
+      const vals = [];
+      states.forEach((s, i) => {
+        if (fa[i]) { assert.strictEqual(s.decided, null); assert.strictEqual(s.x, null); assert.strictEqual(s.k, null); return; }
+        if (kind === 'none') { assert.ok(!s.decided); assert.ok(s.k > 10); assert.notStrictEqual(s.x, null); return; }
+        assert.ok(s.decided);
+        if (kind === 'x1') { assert.strictEqual(s.x, 1); assert.ok(s.k <= 2); }
+        vals.push(s.x);
+      });
+      if (kind === 'agree') assert.ok(vals.every((v) => v === vals[0]));
+    });
+  });
+}
+
+(async () => {
+  let fail = 0, ran = 0;
+  for (const t of tests) {
+    if (only === 'setup' && t.group !== 'setup') continue;
+    ran++;
+    try { await t.fn(); console.log(`ok   ${t.name}`); } catch (e) { fail++; console.log(`FAIL ${t.name}: ${e && e.stack || e}`); }
+  }
+  console.log(`${ran - fail}/${ran} passed`);
+  process.exit(fail ? 1 : 0);
+})();

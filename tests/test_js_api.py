@@ -32,3 +32,24 @@ def test_js_setup_cases():
 @pytest.mark.gpu
 def test_js_reference_suite():
     _run("all")
+
+
+HTTP_SCRIPT = os.path.join(ROOT, "tests", "js", "http_facade.test.js")
+
+
+def _run_http(which):
+    p = subprocess.run(["node", HTTP_SCRIPT, which], capture_output=True, text=True, timeout=120)
+    print(p.stdout, p.stderr)
+    assert p.returncode == 0, p.stdout + p.stderr
+
+
+@needs_node
+def test_http_facade_setup_cases():
+    """/status, /getState, /stop served on 3100+i (SURVEY §8f #1)."""
+    _run_http("setup")
+
+
+@needs_node
+@pytest.mark.gpu
+def test_http_facade_reference_suite():
+    _run_http("all")
