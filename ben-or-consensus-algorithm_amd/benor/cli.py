@@ -1,0 +1,160 @@
+"""Command-line driver.
+
+    python -m benor.cli start [--N 10 --faulty 0,1,2,3 --init 1,1,...]   # src/start.ts
+    python -m benor.cli trials --N 1024 --F 341 --trials 1000000          # one batch, JSON summary
+    python -m benor.cli sweep --N 64,128,...,4096 --steps 32 --trials 2**30 --out sweep.csv
+                                                                          # C5 phase diagram
+
+`start` re-states src/start.ts:6-43: same default scenario (N = 10, nodes
+0-3 faulty, every initial value 1), same checks ("Lengths don't match",
+"Too many faulty nodes" when F > N/2), then launchNetwork + startConsensus,
+and prints every node's state.
+
+`sweep` runs the decision-round phase diagram: every N in the list crossed
+with F = floor(phi * N), phi on a `--steps` grid in [0, 0.5); the total trial
+budget is split evenly over cells, each cell's trials split across ranks
+(torch.distributed, one process per GPU) and merged with one all-reduce per
+cell.  Rows: N, F, m, trials, decided fraction, E[R], P(R = 1..4), P(v = 1),
+undecided, agreement violations.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+
+def _ints(s: str) -> list[int]:
+    out = []
+    for part in s.split(","):
+        part = part.strip()
+        if part:
+            out.append(int(eval(part, {"__builtins__": {}})))   # allows 2**30 style
+    return out
+
+
+def summarize(hist: np.ndarray, N: int, F: int, k_max: int) -> dict:
+    m = N - F
+    trials = int(hist[:-1].sum())
+    dec = np.array([int(hist[r * 3] + hist[r * 3 + 1] + hist[r * 3 + 2]) for r in range(1, k_max + 1)])
+    decided = int(dec.sum())
+    v1 = int(sum(hist[r * 3 + 1] for r in range(1, k_max + 1)))
+    er = float((dec * np.arange(1, k_max + 1)).sum() / decided) if decided else float("nan")
+    row = {"N": N, "F": F, "m": m, "trials": trials, "decided_frac": decided / trials if trials else 0.0,
+           "E_R": er, "P_v1_given_decided": v1 / decided if decided else float("nan"),
+           "undecided": int(hist[0] + hist[1] + hist[2]), "agreement_violations": int(hist[-1])}
+    for r in range(1, 5):
+        row[f"P_R{r}"] = (int(dec[r - 1]) / trials) if trials and r <= k_max else 0.0
+    return row
+
+
+def cmd_start(a) -> int:
+    import benor
+
+    N = a.N
+    faulty_idx = set(_ints(a.faulty)) if a.faulty is not None else {0, 1, 2, 3}
+    faulty = [i in faulty_idx for i in range(N)]
+    init = [("?" if v == "?" else int(v)) for v in a.init.split(",")] if a.init else [1] * N
+    if len(init) != len(faulty):                                   # start.ts:22-23
+        raise benor.Error("Lengths don't match")
+    if sum(faulty) > len(init) / 2:                                 # start.ts:25-29
+        raise benor.Error("Too many faulty nodes")
+    benor.launchNetwork(len(init), sum(faulty), init, faulty)       # start.ts:31-36
+    benor.startConsensus(len(init), seed=a.seed, k_max=a.k_max)     # start.ts:40
+    for i, s in enumerate(benor.getNodesState(len(init))):
+        print(f"Node {i}: {json.dumps(s)}")
+    return 0
+
+
+def cmd_trials(a) -> int:
+    import benor
+
+    plan = benor.TrialsPlan(a.N, a.F, seed=a.seed, k_max=a.k_max)
+    t0 = time.perf_counter()
+    h = plan.run(a.begin, a.trials)
+    dt = time.perf_counter() - t0
+    row = summarize(h, a.N, a.F, a.k_max)
+    row["seconds"] = dt
+    print(json.dumps(row))
+    return 0
+
+
+def cmd_sweep(a) -> int:
+    import torch
+
+    import benor
+    from benor.parallel import merge_histogram, strong_range
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    Ns = _ints(a.N)
+    phis = [i * 0.5 / a.steps for i in range(a.steps)]
+    cells = [(N, int(phi * N)) for N in Ns for phi in phis]
+    per_cell = max(1, int(eval(str(a.trials), {"__builtins__": {}})) // len(cells))
+    rows = []
+    t0 = time.perf_counter()
+    stream = torch.cuda.current_stream()
+    for ci, (N, F) in enumerate(cells):
+        plan = benor.TrialsPlan(N, F, seed=a.seed ^ (N << 20) ^ F, k_max=a.k_max)
+        h = torch.zeros(plan.hist_len, dtype=torch.int64, device="cuda")
+        b, n = strong_range(0, per_cell, rank, world)
+        plan.launch(b, n, h.data_ptr(), stream.cuda_stream)
+        merge_histogram(h)
+        hist = h.cpu().numpy().astype(np.uint64)
+        rows.append(summarize(hist, N, F, a.k_max))
+        if rank == 0 and a.progress:
+            print(f"[{ci + 1}/{len(cells)}] N={N} F={F} {time.perf_counter() - t0:.1f}s", file=sys.stderr, flush=True)
+    elapsed = time.perf_counter() - t0
+    if rank == 0:
+        keys = list(rows[0].keys())
+        out = open(a.out, "w") if a.out else sys.stdout
+        out.write(",".join(keys) + "\n")
+        for r in rows:
+            out.write(",".join(str(r[k]) for k in keys) + "\n")
+        if a.out:
+            out.close()
+        total = per_cell * len(cells)
+        print(json.dumps({"cells": len(cells), "trials": total, "seconds": elapsed, "gpus": world}), file=sys.stderr)
+    return 0
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(prog="benor")
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    s = sub.add_parser("start", help="src/start.ts scenario")
+    s.add_argument("--N", type=int, default=10)
+    s.add_argument("--faulty", default=None, help="comma-separated faulty node ids (default 0,1,2,3)")
+    s.add_argument("--init", default=None, help="comma-separated initial values 0/1/? (default all 1)")
+    s.add_argument("--seed", type=int, default=None)
+    s.add_argument("--k-max", type=int, default=64)
+    t = sub.add_parser("trials", help="one batch of independent trials")
+    t.add_argument("--N", type=int, default=1024)
+    t.add_argument("--F", type=int, default=341)
+    t.add_argument("--trials", type=int, default=1_000_000)
+    t.add_argument("--begin", type=int, default=0)
+    t.add_argument("--seed", type=int, default=0x243F6A8885A308D3)
+    t.add_argument("--k-max", type=int, default=16)
+    w = sub.add_parser("sweep", help="C5 decision-round phase diagram")
+    w.add_argument("--N", default="64,128,256,512,1024,2048,4096")
+    w.add_argument("--steps", type=int, default=32)
+    w.add_argument("--trials", default="2**30")
+    w.add_argument("--seed", type=int, default=0x243F6A8885A308D3)
+    w.add_argument("--k-max", type=int, default=32)
+    w.add_argument("--out", default=None)
+    w.add_argument("--progress", action="store_true")
+    a = ap.parse_args(argv)
+    return {"start": cmd_start, "trials": cmd_trials, "sweep": cmd_sweep}[a.cmd](a)
+
+
+if __name__ == "__main__":
+    sys.exit(main())
