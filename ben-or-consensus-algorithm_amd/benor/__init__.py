@@ -33,6 +33,7 @@ BO_ERR_HIP = 5
 BO_ERR_OUT_OF_RANGE = 6
 BO_ERR_UNSUPPORTED = 7
 BO_MODE_LOCKSTEP = 0
+BO_MODE_RANDOM_DELIVERY = 1
 BO_INIT_RANDOM = 0
 BO_INIT_FIXED = 1
 BO_MAX_N = 4096
@@ -268,18 +269,20 @@ class TrialsPlan:
     current device (bo_plan_*)."""
 
     def __init__(self, N: int, F: int, faulty: Sequence[bool] | None = None, *, seed: int = 0,
-                 k_max: int = DEFAULT_K_MAX, initial_values: Sequence | None = None):
+                 k_max: int = DEFAULT_K_MAX, initial_values: Sequence | None = None,
+                 mode: int = BO_MODE_LOCKSTEP):
         if faulty is None:                       # start.ts:7-18 placement: the first F nodes
             faulty = [i < F for i in range(N)]
         self.N, self.F, self.k_max, self.seed = N, F, k_max, seed
         self._fl = (ctypes.c_uint8 * max(1, N))(*[1 if v else 0 for v in faulty])
         if initial_values is None:
             self._init = (ctypes.c_int8 * max(1, N))()
-            mode = BO_INIT_RANDOM
+            init_mode = BO_INIT_RANDOM
         else:
             self._init = (ctypes.c_int8 * max(1, N))(*[_VAL[v] for v in initial_values])
-            mode = BO_INIT_FIXED
-        self._cfg = TrialsCfgC(N, F, k_max, mode, BO_MODE_LOCKSTEP, 0, seed,
+            init_mode = BO_INIT_FIXED
+        self.mode = mode
+        self._cfg = TrialsCfgC(N, F, k_max, init_mode, mode, 0, seed,
                                ctypes.cast(self._fl, ctypes.POINTER(ctypes.c_uint8)),
                                ctypes.cast(self._init, ctypes.POINTER(ctypes.c_int8)))
         h = ctypes.c_void_p()
@@ -319,16 +322,17 @@ class TrialsPlan:
 
 
 def run_trial_states(N: int, F: int, faulty: Sequence[bool], *, seed: int = 0, trial: int = 0,
-                     k_max: int = DEFAULT_K_MAX, initial_values: Sequence | None = None):
+                     k_max: int = DEFAULT_K_MAX, initial_values: Sequence | None = None,
+                     mode: int = BO_MODE_LOCKSTEP):
     """Per-node final states of one trial: (rounds, [NodeState dict] * N)."""
     fl = (ctypes.c_uint8 * max(1, N))(*[1 if v else 0 for v in faulty])
     if initial_values is None:
         init = (ctypes.c_int8 * max(1, N))()
-        mode = BO_INIT_RANDOM
+        init_mode = BO_INIT_RANDOM
     else:
         init = (ctypes.c_int8 * max(1, N))(*[_VAL[v] for v in initial_values])
-        mode = BO_INIT_FIXED
-    cfg = TrialsCfgC(N, F, k_max, mode, BO_MODE_LOCKSTEP, 0, seed,
+        init_mode = BO_INIT_FIXED
+    cfg = TrialsCfgC(N, F, k_max, init_mode, mode, 0, seed,
                      ctypes.cast(fl, ctypes.POINTER(ctypes.c_uint8)),
                      ctypes.cast(init, ctypes.POINTER(ctypes.c_int8)))
     st = (NodeStateC * max(1, N))()

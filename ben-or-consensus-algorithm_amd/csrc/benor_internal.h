@@ -13,6 +13,7 @@ namespace benor {
 // oracle/benor_oracle.c (the checker) -- DESIGN.md §3.
 constexpr uint32_t kStreamCoin = 0u;
 constexpr uint32_t kStreamInit = 1u;
+constexpr uint32_t kStreamDelivery = 2u;
 
 constexpr int kWavesPerBlock = 4;          // 256-thread workgroups, one trial per wave
 constexpr uint32_t kMaxW = BO_MAX_N / 64;  // u64 words per bit plane at N = 4096
@@ -24,7 +25,9 @@ struct KParams {
   uint32_t W;               // u64 words per plane = ceil(m / 64) = receiver groups
   uint32_t G;               // receiver groups per tally block (template parameter)
   uint32_t nblocks;         // ceil(W / G)
-  uint32_t variant;         // 1: W-specialised kernel (W <= 16), 0: blocked kernel
+  uint32_t variant;         // 1: W-specialised lockstep (W <= 16), 0: blocked lockstep, 2: random delivery
+  uint32_t mode;            // BO_MODE_LOCKSTEP / BO_MODE_RANDOM_DELIVERY
+  uint32_t q;               // quorum N - F (messages each receiver tallies per phase)
   uint32_t k_max;
   uint32_t init_mode;       // BO_INIT_RANDOM / BO_INIT_FIXED
   uint32_t hist_len;        // (k_max + 1) * 3 + 1

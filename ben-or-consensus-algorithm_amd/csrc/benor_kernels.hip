@@ -506,6 +506,195 @@ __global__ void __launch_bounds__(256) benor_lockstep_blocked_kernel(KParams p) 
   }
 }
 
+
+// ----------------------------------------- random-delivery kernel (f <= F)
+// Generalised delivery: with f <= F crashed nodes every live
+// receiver tallies, per phase, a uniformly random subset of exactly q = N-F of
+// the m = N-f live senders ("first N-F arrivals"), drawn by Floyd's algorithm
+// from Philox stream 2 (definition: oracle/benor_oracle.c
+// oracle_delivery_mask).  The subset is built per lane in an LDS bitset laid
+// out [word][lane] (any per-lane word index is bank-conflict free), then the
+// receiver's inbox is (sender plane AND delivery mask).  One receiver group
+// (64 receivers) at a time; this mode is bound by the subset's random draws.
+struct DStream {
+  uint32_t k0, k1, c0, c1, c2, c3;
+  uint4 buf;
+  uint32_t widx;
+  __device__ __forceinline__ uint32_t next() {
+    if ((widx & 3u) == 0u) buf = philox4x32_10(k0, k1, make_uint4(c0, c1, c2 | ((widx >> 2) << 12), c3));
+    const uint32_t j = widx & 3u;
+    ++widx;
+    return j == 0 ? buf.x : j == 1 ? buf.y : j == 2 ? buf.z : buf.w;
+  }
+  // uniform in [0, range): Lemire's multiply-shift with exact rejection
+  __device__ __forceinline__ uint32_t uniform(uint32_t range) {
+    uint64_t mm = (uint64_t)next() * range;
+    uint32_t l = (uint32_t)mm;
+    if (l < range) {
+      const uint32_t t = (0u - range) % range;
+      while (l < t) {
+        mm = (uint64_t)next() * range;
+        l = (uint32_t)mm;
+      }
+    }
+    return (uint32_t)(mm >> 32);
+  }
+};
+
+__device__ __forceinline__ void random_tally(const uint4 *__restrict__ plane, uint32_t *__restrict__ B,
+                                             uint32_t W, uint32_t m, uint32_t q, bool active, uint32_t k0,
+                                             uint32_t k1, uint32_t tlo, uint32_t thi, uint32_t node, uint32_t r,
+                                             uint32_t phase, uint32_t &c0, uint32_t &c1) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t e = m - q;
+  const bool deliver_T = q <= e;
+  const uint32_t k = deliver_T ? q : e;
+  if (active && k) {
+    DStream ds;
+    ds.k0 = k0; ds.k1 = k1; ds.c0 = tlo; ds.c1 = thi; ds.c2 = node & 0xFFFu;
+    ds.c3 = (r & 0xFFFFFu) | ((phase & 1u) << 20) | (kStreamDelivery << 24);
+    ds.widx = 0;
+    for (uint32_t jj = m - k; jj < m; ++jj) {                    // Floyd: uniform k-subset of [0, m)
+      const uint32_t t = ds.uniform(jj + 1u);
+      const uint32_t cur = B[(t >> 5) * 64u + lane];
+      const uint32_t idx = ((cur >> (t & 31u)) & 1u) ? jj : t;
+      B[(idx >> 5) * 64u + lane] |= 1u << (idx & 31u);
+    }
+  }
+  uint32_t a0 = 0, a1 = 0;
+  for (uint32_t w = 0; w < W; ++w) {
+    const uint4 rc = plane[w];
+    const uint32_t tlo_w = B[(2u * w) * 64u + lane], thi_w = B[(2u * w + 1u) * 64u + lane];
+    B[(2u * w) * 64u + lane] = 0u;
+    B[(2u * w + 1u) * 64u + lane] = 0u;
+    const uint64_t vm = group_mask(w, m);
+    const uint32_t dlo = deliver_T ? tlo_w : ((uint32_t)vm & ~tlo_w);
+    const uint32_t dhi = deliver_T ? thi_w : ((uint32_t)(vm >> 32) & ~thi_w);
+    a0 += __builtin_popcount(rc.x & dlo) + __builtin_popcount(rc.y & dhi);
+    a1 += __builtin_popcount(rc.z & dlo) + __builtin_popcount(rc.w & dhi);
+  }
+  c0 = a0;
+  c1 = a1;
+}
+
+__global__ void __launch_bounds__(256) benor_random_kernel(KParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = threadIdx.x >> 6;
+  const uint32_t m = p.m, F = p.F, W = p.W, q = p.q;
+
+  uint32_t *lhist = reinterpret_cast<uint32_t *>(smem);
+  uint4 *X = reinterpret_cast<uint4 *>(smem + p.hist_bytes + wv * p.wave_bytes);   // [W]
+  uint4 *P = X + W;                                                                 // [W]
+  uint32_t *B = reinterpret_cast<uint32_t *>(P + W);                                // [2W][64] bitset
+
+  for (uint32_t i = threadIdx.x; i < p.hist_len; i += blockDim.x) lhist[i] = 0u;
+  for (uint32_t w = 0; w < 2u * W; ++w) B[w * 64u + lane] = 0u;
+  __syncthreads();
+
+  uint64_t expect = 0ull;                          // groups holding a live receiver for this lane
+  for (uint32_t j = 0; j < W; ++j)
+    if (j * 64u + lane < m) expect |= 1ull << j;
+
+  const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
+  const uint64_t waves_total = (uint64_t)gridDim.x * kWavesPerBlock;
+
+  for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + wv; t < p.trial_count; t += waves_total) {
+    const uint64_t trial = p.trial_begin + t;
+    const uint32_t tlo = (uint32_t)trial, thi = (uint32_t)(trial >> 32);
+    if (p.init_mode == BO_INIT_RANDOM) {           // /start (node.ts:167-188)
+      const uint32_t nph = (W + 1u) >> 1;
+      if (lane < nph) {
+        const uint4 r = philox4x32_10(k0, k1, make_uint4(tlo, thi, lane, kStreamInit << 24));
+        const uint32_t w0 = 2u * lane, w1 = w0 + 1u;
+        const uint64_t v0 = group_mask(w0, m), v1 = group_mask(w1, m);
+        const uint64_t x1a = ((uint64_t)r.y << 32 | r.x) & v0;
+        X[w0] = rec(v0 & ~x1a, x1a);
+        if (w1 < W) {
+          const uint64_t x1b = ((uint64_t)r.w << 32 | r.z) & v1;
+          X[w1] = rec(v1 & ~x1b, x1b);
+        }
+      }
+    } else {
+      for (uint32_t w = lane; w < W; w += 64u) X[w] = p.init_plane[w];
+    }
+    uint64_t dec = 0ull;
+    uint32_t R = 0;
+    bool all_dec = false;
+    for (uint32_t r = 1; r <= p.k_max; ++r) {
+      // ---- R-phase ("proposal phase", node.ts:46-82) over each receiver's first N-F arrivals
+      for (uint32_t j = 0; j < W; ++j) {
+        const uint32_t c = j * 64u + lane;
+        const bool active = c < m;
+        const uint32_t node = active ? p.live_ids[c] : 0u;
+        uint32_t a0, a1;
+        random_tally(X, B, W, m, q, active, k0, k1, tlo, thi, node, r, 0u, a0, a1);
+        const uint64_t vm = group_mask(j, m);
+        const uint64_t p0 = ballot(a0 > a1) & vm;
+        const uint64_t p1 = ballot(a1 > a0) & vm;
+        if (lane == 0) P[j] = rec(p0, p1);
+      }
+      // ---- P-phase ("voting phase", node.ts:83-158)
+      for (uint32_t j = 0; j < W; ++j) {
+        const uint32_t c = j * 64u + lane;
+        const bool active = c < m;
+        const uint32_t node = active ? p.live_ids[c] : 0u;
+        uint32_t a0, a1;
+        random_tally(P, B, W, m, q, active, k0, k1, tlo, thi, node, r, 1u, a0, a1);
+        const uint64_t vm = group_mask(j, m);
+        const bool d0l = a0 > F, d1l = a1 > F;
+        const uint64_t d0 = ballot(d0l) & vm;
+        const uint64_t d1 = ballot(d1l) & vm & ~d0;
+        const uint64_t rest = vm & ~(d0 | d1);
+        uint64_t x1 = d1;
+        if (rest) {
+          x1 |= ballot(a1 > a0) & rest;
+          const uint64_t tie = ballot(a1 == a0) & rest;
+          if (tie) x1 |= coin_ballot(k0, k1, tlo, thi, p.live_ids, j, r, tie);
+        }
+        if (lane == 0) X[j] = rec(vm & ~x1, x1);
+        if (d0l || d1l) dec |= 1ull << j;
+      }
+      R = r;
+      all_dec = __all((dec & expect) == expect);
+      if (all_dec) break;
+    }
+    bool any0 = false, any1 = false;
+    if (lane < W) {
+      const uint4 qq = X[lane];
+      any0 = (qq.x | qq.y) != 0u;
+      any1 = (qq.z | qq.w) != 0u;
+    }
+    const bool g0 = __any(any0), g1 = __any(any1);
+    const uint32_t v = (g0 && g1) ? 2u : (g1 ? 1u : 0u);
+    if (lane == 0) {
+      atomicAdd(&lhist[all_dec ? (R * 3u + v) : v], 1u);
+      if (all_dec && v == 2u) atomicAdd(&lhist[p.hist_len - 1u], 1u);
+      if (p.rounds_out) *p.rounds_out = all_dec ? R : 0u;
+    }
+    if (p.node_out) {
+      for (uint32_t c = lane; c < m; c += 64u) {
+        const uint32_t j = c >> 6;
+        const uint4 qq = X[j];
+        const uint64_t x1 = (uint64_t)qq.w << 32 | qq.z;
+        bo_node_state ns;
+        ns.killed = 0;
+        ns.x = (int8_t)((x1 >> lane) & 1ull);
+        ns.decided = (int8_t)((dec >> j) & 1ull);
+        ns.pad = 0;
+        ns.k = (int32_t)R + 1;
+        p.node_out[p.live_ids[c]] = ns;
+      }
+    }
+  }
+
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < p.hist_len; i += blockDim.x) {
+    const uint32_t c = lhist[i];
+    if (c) atomicAdd(&p.hist[i], (unsigned long long)c);
+  }
+}
+
 // --------------------------------------------------- popcount peak probe
 // Eight independent v_bcnt_u32_b32 chains per lane; the roofline's `peak`
 // is the spec VALU rate, this probe says what the part sustains.
@@ -532,6 +721,14 @@ void plan_geometry(KParams &p) {
   const uint32_t W = p.W;
   p.hist_len = (p.k_max + 1u) * 3u + 1u;
   p.hist_bytes = ((p.hist_len * 4u) + 15u) & ~15u;
+  if (p.mode == BO_MODE_RANDOM_DELIVERY) {
+    p.G = 1;
+    p.nblocks = W;
+    p.variant = 2;
+    p.wave_bytes = 2u * W * 16u + 2u * W * 64u * 4u;   // X, P records + per-lane bitset
+    p.lds_bytes = p.hist_bytes + kWavesPerBlock * p.wave_bytes;
+    return;
+  }
   const uint32_t nph = (W + 1u) / 2u, tb = 64u / nph;   // init ring: tb trials per Philox pass
   if (W <= (uint32_t)kMaxWSpecialised) {
     p.G = W;
@@ -577,6 +774,15 @@ static hipError_t dispatch_b(const KParams &p, int grid, hipStream_t s, std::int
 }
 
 hipError_t launch_lockstep(const KParams &p, int grid, hipStream_t s) {
+  if (p.variant == 2) {
+    if (p.lds_bytes > 64u * 1024u) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&benor_random_kernel),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds_bytes);
+      if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(benor_random_kernel, dim3(grid), dim3(64 * kWavesPerBlock), p.lds_bytes, s, p);
+    return hipGetLastError();
+  }
   if (p.variant == 1) return dispatch_w(p, grid, s, std::make_integer_sequence<int, kMaxWSpecialised>{});
   return dispatch_b(p, grid, s, std::make_integer_sequence<int, 8>{});
 }

@@ -195,7 +195,8 @@ int bo_plan_create(const bo_trials_cfg *cfg, bo_plan **out) {
   *out = nullptr;
   if (cfg->N < 1 || cfg->N > BO_MAX_N) return fail(BO_ERR_UNSUPPORTED, "N must be in [1, 4096]");
   if (cfg->k_max < 1 || cfg->k_max > BO_MAX_K) return fail(BO_ERR_INVALID_ARGUMENT, "k_max must be in [1, 1024]");
-  if (cfg->mode != BO_MODE_LOCKSTEP) return fail(BO_ERR_UNSUPPORTED, "unknown delivery mode");
+  if (cfg->mode != BO_MODE_LOCKSTEP && cfg->mode != BO_MODE_RANDOM_DELIVERY)
+    return fail(BO_ERR_UNSUPPORTED, "unknown delivery mode");
   if (cfg->init_mode != BO_INIT_RANDOM && cfg->init_mode != BO_INIT_FIXED)
     return fail(BO_ERR_INVALID_ARGUMENT, "unknown init_mode");
   if (!cfg->faulty) return fail(BO_ERR_INVALID_ARGUMENT, "faulty is NULL");
@@ -203,8 +204,10 @@ int bo_plan_create(const bo_trials_cfg *cfg, bo_plan **out) {
   uint32_t f = 0;
   for (uint32_t i = 0; i < cfg->N; ++i) f += cfg->faulty[i] ? 1u : 0u;
   // Lockstep = the reference's admissible inputs: exactly F crash faults
-  // (launchNodes.ts:12-13).
-  if (f != cfg->F) return fail(BO_ERR_FAULTY_COUNT, "faultyList doesnt have F faulties");
+  // (launchNodes.ts:12-13).  Random delivery admits f <= F.
+  if (cfg->mode == BO_MODE_LOCKSTEP && f != cfg->F) return fail(BO_ERR_FAULTY_COUNT, "faultyList doesnt have F faulties");
+  if (cfg->mode == BO_MODE_RANDOM_DELIVERY && f > cfg->F)
+    return fail(BO_ERR_FAULTY_COUNT, "random delivery needs at most F crash-faulty nodes");
   int dev = 0;
   int rc = check_device(&dev);
   if (rc) return rc;
@@ -225,6 +228,8 @@ int bo_plan_create(const bo_trials_cfg *cfg, bo_plan **out) {
   kp.k_max = cfg->k_max;
   kp.init_mode = cfg->init_mode;
   kp.seed = cfg->seed;
+  kp.mode = cfg->mode;
+  kp.q = cfg->N - cfg->F;
   if (m > 0) {
     benor::plan_geometry(kp);
     std::vector<uint4> plane(kp.W, make_uint4(0, 0, 0, 0));

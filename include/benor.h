@@ -42,8 +42,13 @@ enum {
 
 /* Delivery model.  LOCKSTEP is the reference's semantics for its admissible
  * inputs (exactly F crash faults, launchNodes.ts:12-13): every live node
- * receives every live node's message in every phase. */
-enum { BO_MODE_LOCKSTEP = 0 };
+ * receives every live node's message in every phase.
+ * RANDOM_DELIVERY generalises to f <= F crashed nodes: in every phase each
+ * live receiver tallies the first N-F arrivals, a uniformly random subset of
+ * exactly N-F of the N-f live senders drawn from Philox (no
+ * reference counterpart -- the reference rejects f != F).  At f == F the two
+ * modes give identical results. */
+enum { BO_MODE_LOCKSTEP = 0, BO_MODE_RANDOM_DELIVERY = 1 };
 
 enum { BO_INIT_RANDOM = 0, BO_INIT_FIXED = 1 };
 
@@ -107,10 +112,10 @@ typedef struct bo_trials_cfg {
     uint32_t N, F;            /* network size; fault parameter (quorum N-F, decide on > F) */
     uint32_t k_max;           /* round cap, 1..BO_MAX_K */
     uint32_t init_mode;       /* BO_INIT_RANDOM: iid Bernoulli(1/2) per live node; BO_INIT_FIXED */
-    uint32_t mode;            /* BO_MODE_LOCKSTEP */
+    uint32_t mode;            /* BO_MODE_LOCKSTEP or BO_MODE_RANDOM_DELIVERY */
     uint32_t reserved;
     uint64_t seed;            /* Philox4x32-10 key */
-    const uint8_t *faulty;    /* host [N]; exactly F set in LOCKSTEP mode */
+    const uint8_t *faulty;    /* host [N]; exactly F set (LOCKSTEP), at most F (RANDOM_DELIVERY) */
     const int8_t *init;       /* host [N]; used when init_mode == BO_INIT_FIXED */
 } bo_trials_cfg;
 

@@ -44,6 +44,7 @@
 
 #define ORC_STREAM_COIN 0u
 #define ORC_STREAM_INIT 1u
+#define ORC_STREAM_DELIVERY 2u
 #define ORC_STREAM_ORDER 3u
 
 /* ---------------------------------------------------------------- Philox */
@@ -274,7 +275,78 @@ typedef struct {
     const uint8_t *faulty;    /* [N] crash-faulty (never send, never receive) */
     const int8_t *init;       /* [N] 0/1/2('?'), used when init_mode == 1 */
     int32_t threads;          /* <=0: all available */
+    uint32_t mode;            /* 0 = lockstep (exactly F crashed), 1 = random delivery (f <= F) */
 } orc_trials_cfg;
+
+/* ------------------------------------------------ random delivery model */
+/* Generalised delivery (no reference counterpart: the
+ * reference admits only f == F, launchNodes.ts:12-13).  With f <= F crashed,
+ * each live receiver tallies, in each phase, the first N-F arrivals: a
+ * uniformly random subset of exactly q = N-F of the m = N-f live senders,
+ * independent per (receiver, round, phase).  At f == F it is every live
+ * sender, i.e. lockstep.
+ *
+ * Subset: k = min(e, q) with e = m - q; Floyd's algorithm draws a uniform
+ * k-subset T of [0, m): for j = m-k .. m-1, t = uniform[0, j] (Lemire's
+ * multiply-shift with exact rejection), T += (t in T) ? j : t.  Delivered set
+ * = T if q <= e, else the live senders minus T.  Random words: Philox stream 2,
+ * ctr {trial_lo, trial_hi, (node & 0xFFF) | (block << 12),
+ * (round & 0xFFFFF) | (phase << 20) | (2 << 24)}, consumed in order
+ * (word i = block i>>2, lane i&3).  `node` is the receiver's node id. */
+typedef struct {
+    uint32_t key[2], ctr[4];
+    uint32_t buf[4];
+    uint32_t widx;
+} orc_dstream;
+
+static inline uint32_t dstream_next(orc_dstream *s) {
+    if ((s->widx & 3u) == 0) {
+        uint32_t c[4] = {s->ctr[0], s->ctr[1], s->ctr[2] | ((s->widx >> 2) << 12), s->ctr[3]};
+        oracle_philox4x32_10(s->key, c, s->buf);
+    }
+    return s->buf[s->widx++ & 3u];
+}
+
+/* uniform integer in [0, range) (Lemire 2019, exact) */
+static inline uint32_t dstream_uniform(orc_dstream *s, uint32_t range) {
+    uint64_t m = (uint64_t)dstream_next(s) * range;
+    uint32_t l = (uint32_t)m;
+    if (l < range) {
+        uint32_t t = (uint32_t)(-range) % range;
+        while (l < t) {
+            m = (uint64_t)dstream_next(s) * range;
+            l = (uint32_t)m;
+        }
+    }
+    return (uint32_t)(m >> 32);
+}
+
+/* D[W]: delivered-sender mask (compact sender indices) of receiver `node`. */
+void oracle_delivery_mask(uint64_t seed, uint64_t trial, uint32_t node, uint32_t round, uint32_t phase,
+                          uint32_t m, uint32_t q, uint64_t *D) {
+    const uint32_t W = (m + 63) / 64;
+    orc_dstream s;
+    s.key[0] = (uint32_t)seed; s.key[1] = (uint32_t)(seed >> 32);
+    s.ctr[0] = (uint32_t)trial; s.ctr[1] = (uint32_t)(trial >> 32);
+    s.ctr[2] = node & 0xFFFu;
+    s.ctr[3] = (round & 0xFFFFFu) | ((phase & 1u) << 20) | (ORC_STREAM_DELIVERY << 24);
+    s.widx = 0;
+    const uint32_t e = m - q;
+    const int deliver_T = q <= e;
+    const uint32_t k = deliver_T ? q : e;
+    uint64_t T[64];
+    for (uint32_t w = 0; w < W; ++w) T[w] = 0;
+    for (uint32_t j = m - k; j < m; ++j) {
+        const uint32_t t = dstream_uniform(&s, j + 1u);
+        const uint32_t idx = ((T[t >> 6] >> (t & 63)) & 1ull) ? j : t;
+        T[idx >> 6] |= 1ull << (idx & 63);
+    }
+    for (uint32_t w = 0; w < W; ++w) {
+        const uint32_t lo = w * 64, n = (m - lo) < 64 ? (m - lo) : 64;
+        const uint64_t vm = n == 64 ? ~0ull : ((1ull << n) - 1);
+        D[w] = deliver_T ? T[w] : (vm & ~T[w]);
+    }
+}
 
 static inline int popc64(uint64_t v) { return __builtin_popcountll(v); }
 
@@ -314,6 +386,11 @@ static void run_one(const orc_trials_cfg *cfg, const uint32_t *live_ids, uint32_
             const uint64_t *a0 = x0, *a1 = x1;
             __asm__ volatile("" : "+r"(a0), "+r"(a1));   /* per-receiver tally: no hoisting */
             int c0 = 0, c1 = 0;
+            if (cfg->mode == 1) {
+                uint64_t D[64];
+                oracle_delivery_mask(cfg->seed, trial, live_ids[c], r, 0, m, (uint32_t)quorum, D);
+                for (uint32_t w = 0; w < W; ++w) { c0 += popc64(a0[w] & D[w]); c1 += popc64(a1[w] & D[w]); }
+            } else
             for (uint32_t w = 0; w < W; ++w) { c0 += popc64(a0[w]); c1 += popc64(a1[w]); }
             if (c0 > c1) p0[c >> 6] |= 1ull << (c & 63);
             else if (c1 > c0) p1[c >> 6] |= 1ull << (c & 63);
@@ -325,6 +402,11 @@ static void run_one(const orc_trials_cfg *cfg, const uint32_t *live_ids, uint32_
             const uint64_t *a0 = p0, *a1 = p1;
             __asm__ volatile("" : "+r"(a0), "+r"(a1));
             int c0 = 0, c1 = 0;
+            if (cfg->mode == 1) {
+                uint64_t D[64];
+                oracle_delivery_mask(cfg->seed, trial, live_ids[c], r, 1, m, (uint32_t)quorum, D);
+                for (uint32_t w = 0; w < W; ++w) { c0 += popc64(a0[w] & D[w]); c1 += popc64(a1[w] & D[w]); }
+            } else
             for (uint32_t w = 0; w < W; ++w) { c0 += popc64(a0[w]); c1 += popc64(a1[w]); }
             int x;
             uint64_t bit = 1ull << (c & 63);
@@ -374,10 +456,11 @@ int oracle_run_trials(const orc_trials_cfg *cfg, uint64_t *hist, orc_node_state 
     uint32_t *live_ids = (uint32_t *)malloc(sizeof(uint32_t) * (cfg->N + 1));
     uint32_t m = 0;
     for (uint32_t i = 0; i < cfg->N; ++i) if (!cfg->faulty[i]) live_ids[m++] = i;
-    /* this restatement covers the reference's admissible inputs: the number of
-     * crash-faulty nodes is exactly F (launchNodes.ts:12-13), or fewer live
-     * nodes than the quorum (stall).  f < F needs the random-delivery model. */
-    if ((int64_t)m > (int64_t)cfg->N - (int64_t)cfg->F) { free(live_ids); return -2; }
+    /* lockstep covers the reference's admissible inputs: exactly F crash faults
+     * (launchNodes.ts:12-13), or fewer live nodes than the quorum (stall).
+     * f < F needs the random-delivery model (mode 1). */
+    if (cfg->mode == 0 && (int64_t)m > (int64_t)cfg->N - (int64_t)cfg->F) { free(live_ids); return -2; }
+    if (cfg->mode > 1) { free(live_ids); return -1; }
     if (node_out) {
         for (uint32_t i = 0; i < cfg->N; ++i) {
             int f = cfg->faulty[i] != 0;

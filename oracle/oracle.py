@@ -29,7 +29,7 @@ class TrialsCfg(ctypes.Structure):
                 ("init_mode", ctypes.c_uint32), ("seed", ctypes.c_uint64),
                 ("trial_begin", ctypes.c_uint64), ("trial_count", ctypes.c_uint64),
                 ("faulty", ctypes.POINTER(ctypes.c_uint8)), ("init", ctypes.POINTER(ctypes.c_int8)),
-                ("threads", ctypes.c_int32)]
+                ("threads", ctypes.c_int32), ("mode", ctypes.c_uint32)]
 
 
 def build() -> str:
@@ -60,6 +60,10 @@ def lib():
         L.oracle_run_trials.argtypes = [ctypes.POINTER(TrialsCfg), ctypes.POINTER(ctypes.c_uint64),
                                         ctypes.POINTER(NodeState)]
         L.oracle_run_trials.restype = ctypes.c_int
+        L.oracle_delivery_mask.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                           ctypes.POINTER(ctypes.c_uint64)]
+        L.oracle_delivery_mask.restype = None
         _lib = L
     return _lib
 
@@ -119,19 +123,31 @@ class TrialsResult:
     states: list | None
 
 
+def delivery_mask(seed, trial, node, rnd, phase, m, q) -> list[int]:
+    """Delivered-sender mask (list of W uint64 words) of one receiver-phase
+    in the random-delivery model."""
+    W = (m + 63) // 64
+    D = (ctypes.c_uint64 * max(1, W))()
+    lib().oracle_delivery_mask(seed, trial, node, rnd, phase, m, q, D)
+    return [int(D[i]) for i in range(W)]
+
+
+MODE_LOCKSTEP, MODE_RANDOM_DELIVERY = 0, 1
+
+
 def run_trials(N, F, faulty_list, *, seed=0, trial_begin=0, trial_count=1, k_max=64,
-               initial_values=None, threads=0, want_states=False) -> TrialsResult:
+               initial_values=None, threads=0, want_states=False, mode=MODE_LOCKSTEP) -> TrialsResult:
     """(ii) round-level bit-plane restatement over a batch of trials."""
     f = (ctypes.c_uint8 * max(1, N))(*[1 if v else 0 for v in faulty_list])
     if initial_values is None:
         init = (ctypes.c_int8 * max(1, N))()
-        mode = 0
+        init_mode = 0
     else:
         init = (ctypes.c_int8 * max(1, N))(*[VAL_CODE[v] for v in initial_values])
-        mode = 1
-    cfg = TrialsCfg(N, F, k_max, mode, seed, trial_begin, trial_count,
+        init_mode = 1
+    cfg = TrialsCfg(N, F, k_max, init_mode, seed, trial_begin, trial_count,
                     ctypes.cast(f, ctypes.POINTER(ctypes.c_uint8)),
-                    ctypes.cast(init, ctypes.POINTER(ctypes.c_int8)), threads)
+                    ctypes.cast(init, ctypes.POINTER(ctypes.c_int8)), threads, mode)
     hist = np.zeros(hist_len(k_max), dtype=np.uint64)
     st = (NodeState * max(1, N))() if want_states else None
     rc = lib().oracle_run_trials(ctypes.byref(cfg), hist.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),

@@ -123,6 +123,16 @@ HIST_CASES = [
 ]
 
 
+RANDOM_HIST_CASES = [
+    # (N, F, f, trials, k_max): random-delivery model, the first f nodes crashed
+    (10, 4, 2, 20000, 16), (10, 4, 0, 20000, 16), (7, 3, 1, 20000, 16), (100, 30, 10, 2000, 16),
+    (200, 90, 0, 500, 16), (70, 40, 0, 2000, 16), (130, 20, 5, 500, 16), (1100, 40, 20, 20, 16),
+    (1024, 341, 0, 40, 16), (64, 10, 3, 1000, 16),
+]
+
+RANDOM_STATE_CASES = [(12, 4, 1), (10, 4, 2), (100, 30, 5), (70, 40, 0), (130, 40, 10)]
+
+
 def encode_state(s):
     """NodeState -> [killed, x, decided, k] with null = -1 and '?' = 2."""
     x = {None: -1, 0: 0, 1: 1, "?": 2}[s["x"]]
@@ -161,10 +171,29 @@ def main():
         nz = {str(i): int(v) for i, v in enumerate(res.hist) if v}
         hists.append({"N": N, "F": F, "seed": SEED ^ N, "trial_begin": 12345, "trial_count": ntr, "k_max": k_max,
                       "hist_nonzero": nz})
+    rhists = []
+    for (N, F, f, ntr, k_max) in RANDOM_HIST_CASES:
+        fl = first_f(N, f)
+        res = oracle.run_trials(N, F, fl, seed=SEED ^ (N * 31 + f), trial_begin=777, trial_count=ntr, k_max=k_max,
+                                mode=oracle.MODE_RANDOM_DELIVERY)
+        rhists.append({"N": N, "F": F, "faulty": fl, "seed": SEED ^ (N * 31 + f), "trial_begin": 777,
+                       "trial_count": ntr, "k_max": k_max,
+                       "hist_nonzero": {str(i): int(v) for i, v in enumerate(res.hist) if v}})
+    rstates = []
+    for (N, F, f) in RANDOM_STATE_CASES:
+        for t in range(4):
+            fl = first_f(N, f)
+            init = None if t % 2 else [int(b) for b in format((t * 2654435761) % (1 << N), f"0{N}b")[:N]]
+            res = oracle.run_trials(N, F, fl, seed=SEED + t, trial_begin=50 + t, trial_count=1, k_max=24,
+                                    initial_values=init, want_states=True, mode=oracle.MODE_RANDOM_DELIVERY)
+            rstates.append({"N": N, "F": F, "faulty": fl, "init": init, "seed": SEED + t, "trial": 50 + t,
+                            "k_max": 24, "states": [encode_state(x) for x in res.states]})
     with open(os.path.join(HERE, "oracle_vectors.json"), "w") as f:
         json.dump({"generator": "tests/golden/make_golden.py (oracle/benor_oracle.c restatements (i)+(ii))",
-                   "states": states, "hists": hists}, f, separators=(",", ":"))
-    print(f"{len(states)} state cases, {len(hists)} histograms")
+                   "states": states, "hists": hists, "random_hists": rhists, "random_states": rstates}, f,
+                  separators=(",", ":"))
+    print(f"{len(states)} state cases, {len(hists)} histograms, {len(rhists)} random-delivery histograms, "
+          f"{len(rstates)} random-delivery state cases")
 
 
 if __name__ == "__main__":

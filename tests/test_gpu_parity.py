@@ -163,3 +163,42 @@ def test_no_decision_case_f_gt_half():
 def test_popc_peak_probe_runs():
     peak = benor.popc_peak(5)
     assert peak > 1e12
+
+
+# ------------------------------------------------- random delivery (f <= F)
+RD = benor.BO_MODE_RANDOM_DELIVERY
+
+
+def test_random_delivery_golden(oracle_vectors):
+    for h in oracle_vectors["random_hists"]:
+        plan = benor.TrialsPlan(h["N"], h["F"], h["faulty"], seed=h["seed"], k_max=h["k_max"], mode=RD)
+        got = plan.run(h["trial_begin"], h["trial_count"])
+        assert {str(i): int(v) for i, v in enumerate(got) if v} == h["hist_nonzero"], (h["N"], h["F"])
+    for c in oracle_vectors["random_states"]:
+        _, st = benor.run_trial_states(c["N"], c["F"], c["faulty"], seed=c["seed"], trial=c["trial"],
+                                       k_max=c["k_max"], initial_values=c["init"], mode=RD)
+        assert st == [decode_state(e) for e in c["states"]], c
+
+
+@pytest.mark.parametrize("N,F,f,trials", [(10, 4, 1, 100_000), (9, 4, 0, 100_000), (66, 20, 3, 3000),
+                                          (300, 120, 40, 200), (2100, 700, 0, 3), (4096, 1365, 1000, 2)])
+def test_random_delivery_matches_oracle(N, F, f, trials):
+    fl = first_f(N, f)
+    seed = 0x51ED ^ N ^ (f << 16)
+    got = benor.TrialsPlan(N, F, fl, seed=seed, k_max=16, mode=RD).run(5, trials)
+    ref = oracle.run_trials(N, F, fl, seed=seed, trial_begin=5, trial_count=trials, k_max=16,
+                            mode=oracle.MODE_RANDOM_DELIVERY)
+    np.testing.assert_array_equal(got, ref.hist)
+
+
+def test_random_delivery_equals_lockstep_at_f_equals_F():
+    for N, F in [(10, 4), (100, 33), (1024, 341)]:
+        fl = first_f(N, F)
+        a = benor.TrialsPlan(N, F, fl, seed=3, k_max=16, mode=RD).run(0, 20_000)
+        b = benor.TrialsPlan(N, F, fl, seed=3, k_max=16).run(0, 20_000)
+        np.testing.assert_array_equal(a, b)
+
+
+def test_random_delivery_rejects_too_many_faults():
+    with pytest.raises(benor.Error):
+        benor.TrialsPlan(10, 2, first_f(10, 3), mode=RD)

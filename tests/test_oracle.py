@@ -146,3 +146,47 @@ def test_golden_vectors_reproduce(oracle_vectors):
         res = oracle.run_trials(h["N"], h["F"], [i < h["F"] for i in range(h["N"])], seed=h["seed"],
                                 trial_begin=h["trial_begin"], trial_count=h["trial_count"], k_max=h["k_max"])
         assert {str(i): int(v) for i, v in enumerate(res.hist) if v} == h["hist_nonzero"]
+
+
+# ------------------------------------------------- random delivery model
+@pytest.mark.parametrize("m,q", [(10, 6), (100, 60), (100, 30), (1024, 683), (64, 64), (200, 1), (37, 0)])
+def test_delivery_mask_exact_size_and_uniform(m, q):
+    """Each receiver-phase tallies exactly q = N-F distinct live senders, and
+    every sender is included with probability q/m (chi-square)."""
+    from scipy import stats
+
+    reps = 400 if m > 500 else 2000
+    cnt = np.zeros(m)
+    for node in range(reps):
+        D = oracle.delivery_mask(0xABCDEF, 7, node, 3, node & 1, m, q)
+        bits = np.array([(D[i >> 6] >> (i & 63)) & 1 for i in range(m)])
+        assert bits.sum() == q
+        if m % 64:
+            assert D[-1] >> (m % 64) == 0
+        cnt += bits
+    if 0 < q < m:
+        exp = np.full(m, reps * q / m)
+        p = stats.chisquare(cnt, exp).pvalue
+        assert p > 1e-4, p
+
+
+def test_random_delivery_reduces_to_lockstep_at_f_equals_F():
+    for N, F in [(10, 4), (64, 21), (130, 2), (5, 1)]:
+        fl = [i < F for i in range(N)]
+        a = oracle.run_trials(N, F, fl, seed=9, trial_count=3000, k_max=16, mode=oracle.MODE_RANDOM_DELIVERY)
+        b = oracle.run_trials(N, F, fl, seed=9, trial_count=3000, k_max=16, mode=oracle.MODE_LOCKSTEP)
+        np.testing.assert_array_equal(a.hist, b.hist)
+
+
+def test_random_delivery_relative_majority_can_split():
+    """With f < F the reference's relative-majority proposal (node.ts:63-69)
+    lets different receivers propose different values, so split decisions
+    appear: the agreement-violation counter is the model's report of it."""
+    N, F = 1024, 341
+    r = oracle.run_trials(N, F, [False] * N, seed=1, trial_count=60, k_max=16, mode=oracle.MODE_RANDOM_DELIVERY)
+    assert r.hist.sum() - r.hist[-1] == 60
+    assert r.hist[-1] > 0
+    # with a strict-majority-sized fault bound the law is benign: f = F - 1 at N = 10, F = 2
+    r = oracle.run_trials(10, 2, [True] + [False] * 9, seed=2, trial_count=20000, k_max=16,
+                          mode=oracle.MODE_RANDOM_DELIVERY)
+    assert r.hist[-1] == 0
