@@ -22,7 +22,7 @@ import secrets
 from typing import Sequence
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libbenor.so")
+LIB_PATH = os.environ.get("BENOR_LIB_PATH") or os.path.join(os.path.dirname(_HERE), "lib", "libbenor.so")
 
 BO_OK = 0
 BO_ERR_ARRAYS_DONT_MATCH = 1

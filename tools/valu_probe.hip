@@ -26,6 +26,13 @@ __global__ void __launch_bounds__(256) probe(unsigned *sink, int iters, unsigned
         if (OP == 6) asm volatile("v_writelane_b32 %0, %1, 5" : "+v"(a[i]) : "s"(seed + i));
         if (OP == 7) asm volatile("v_cmp_gt_u32 vcc, %0, %1" :: "v"(a[i]), "v"(x) : "vcc");
         if (OP == 8) asm volatile("v_mul_hi_u32 %0, %1, %0" : "+v"(a[i]) : "v"(x));
+        if (OP == 9) {
+          unsigned long long t;
+          asm volatile("v_mov_b64 %0, %1" : "=v"(t) : "s"((unsigned long long)seed << 32 | (unsigned)i));
+          a[i] ^= (unsigned)t;
+        }
+        if (OP == 10) asm volatile("v_not_b32 %0, %0" : "+v"(a[i]));
+        if (OP == 11) asm volatile("v_xor_b32 %0, %1, %0" : "+v"(a[i]) : "s"(seed));
       }
     }
   }
@@ -75,6 +82,9 @@ int main() {
     run<6>("v_writelane_b32", cus, bpc);
     run<7>("v_cmp_gt_u32", cus, bpc);
     run<8>("v_mul_hi_u32", cus, bpc);
+    run<9>("v_mov_b64 (s) + v_xor", cus, bpc);
+    run<10>("v_not_b32", cus, bpc);
+    run<11>("v_xor_b32 (s,v)", cus, bpc);
   }
   return 0;
 }
