@@ -1,0 +1,69 @@
+"""Throughput of the round-loop kernels across network shapes (GPU).
+
+For each (N, F, f, mode) runs `trials` trials once for warm-up and once timed
+with HIP events on the launch stream, and prints live node-rounds/s and the
+popcount-roofline fraction (4*ceil(m/32) words per live node-round vs the
+v_bcnt issue peak, 39.3 T/s).  One JSON line per shape.
+
+    python tools/perf_matrix.py [--quick]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ben-or-consensus-algorithm_amd"))
+PEAK = 256 * 4 * 16 * 2.4e9
+
+SHAPES = [
+    # N, F, f (crashed), mode, trials
+    (5, 1, 1, 0, 20_000_000), (10, 4, 4, 0, 20_000_000), (10, 5, 5, 0, 2_000_000), (64, 21, 21, 0, 10_000_000),
+    (256, 85, 85, 0, 10_000_000), (512, 170, 170, 0, 10_000_000), (1024, 341, 341, 0, 20_000_000),
+    (1024, 0, 0, 0, 4_000_000), (1536, 512, 512, 0, 2_000_000), (2048, 682, 682, 0, 1_000_000),
+    (4096, 1365, 1365, 0, 400_000), (4096, 0, 0, 0, 100_000),
+    (10, 4, 2, 1, 2_000_000), (100, 30, 10, 1, 200_000), (1024, 341, 300, 1, 20_000), (1024, 341, 0, 1, 2_000),
+]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--quick", action="store_true")
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+
+    import benor
+
+    torch.cuda.set_device(0)
+    stream = torch.cuda.current_stream()
+    for (N, F, f, mode, trials) in SHAPES:
+        if a.quick:
+            trials = max(1, trials // 10)
+        plan = benor.TrialsPlan(N, F, [i < f for i in range(N)], seed=0x1234 + N, k_max=32, mode=mode)
+        m = N - f
+        h = torch.zeros(plan.hist_len, dtype=torch.int64, device="cuda")
+        plan.launch(0, max(1, trials // 10), h.data_ptr(), stream.cuda_stream)
+        torch.cuda.synchronize()
+        h.zero_()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        plan.launch(10**9, trials, h.data_ptr(), stream.cuda_stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1)
+        hist = h.cpu().numpy().astype(np.uint64)
+        k = 32
+        rounds = sum(r * int(hist[r * 3] + hist[r * 3 + 1] + hist[r * 3 + 2]) for r in range(1, k + 1))
+        rounds += k * int(hist[0] + hist[1] + hist[2])
+        nr = rounds * m
+        words = 4 * ((m + 31) // 32)
+        rate = nr / (ms * 1e-3)
+        print(json.dumps({"N": N, "F": F, "f": f, "mode": ["lockstep", "random"][mode], "trials": trials,
+                          "mean_rounds": rounds / trials, "ms": round(ms, 3), "node_rounds_per_s": rate,
+                          "popc_frac": rate * words / PEAK,
+                          "agreement_violations": int(hist[-1])}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
