@@ -34,6 +34,10 @@
 
 #include "benor_internal.h"
 
+#ifndef BENOR_P_SGPR
+#define BENOR_P_SGPR 1
+#endif
+
 namespace benor {
 
 // ------------------------------------------------------------------ Philox
@@ -154,6 +158,59 @@ __device__ __forceinline__ void tally_plane(const uint4 *__restrict__ plane, uin
   }
 }
 
+
+// Proposal planes can stay in SGPRs for the few hundred cycles between the
+// R-phase ballots that produce them and the P-phase tallies that read them:
+// v_bcnt_u32_b32 takes its word from an SGPR at the same issue rate, so this
+// saves the four staging moves per receiver group of the R-phase.
+template <int C>
+__device__ __forceinline__ uint32_t tally_first_s(uint32_t word) {
+  uint32_t r;
+  asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "s"(word), "i"(C));
+  return r;
+}
+
+__device__ __forceinline__ uint32_t tally_s(uint32_t word, uint32_t acc) {
+  uint32_t r;
+  asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "s"(word), "v"(acc));
+  return r;
+}
+
+__device__ __forceinline__ uint32_t sgpr32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+
+template <int W>
+__device__ __forceinline__ void tally_sgpr(const uint64_t (&is0)[W], const uint64_t (&is1)[W], uint32_t (&a0)[W],
+                                           uint32_t (&a1)[W]) {
+  {
+    const uint32_t w0 = sgpr32((uint32_t)is0[0]), w1 = sgpr32((uint32_t)is1[0]);
+    Unroll<W>::run([&](auto gi) {
+      constexpr int g = decltype(gi)::value;
+      a0[g] = tally_first_s<g>(w0);
+      a1[g] = tally_first_s<g>(w1);
+    });
+    const uint32_t h0 = sgpr32((uint32_t)(is0[0] >> 32)), h1 = sgpr32((uint32_t)(is1[0] >> 32));
+#pragma unroll
+    for (int g = 0; g < W; ++g) {
+      a0[g] = tally_s(h0, a0[g]);
+      a1[g] = tally_s(h1, a1[g]);
+    }
+  }
+#pragma unroll
+  for (int w = 1; w < W; ++w) {
+    const uint32_t l0 = sgpr32((uint32_t)is0[w]), l1 = sgpr32((uint32_t)is1[w]);
+    const uint32_t h0 = sgpr32((uint32_t)(is0[w] >> 32)), h1 = sgpr32((uint32_t)(is1[w] >> 32));
+#pragma unroll
+    for (int g = 0; g < W; ++g) {
+      a0[g] = tally_s(l0, a0[g]);
+      a1[g] = tally_s(l1, a1[g]);
+      a0[g] = tally_s(h0, a0[g]);
+      a1[g] = tally_s(h1, a1[g]);
+    }
+  }
+}
+
 template <int L>
 __device__ __forceinline__ uint32_t writelane(uint32_t v, uint32_t val) {
   asm("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(val), "i"(L));
@@ -229,6 +286,18 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
         uint32_t a0[W], a1[W];
         // ---- R-phase ("proposal phase", node.ts:46-82)
         tally_plane<W>(Xr, a0, a1);
+#if BENOR_P_SGPR
+        uint64_t p0s[W], p1s[W];
+#pragma unroll
+        for (int g = 0; g < W; ++g) {
+          const uint64_t vm = (g == W - 1) ? tailm : ~0ull;
+          p0s[g] = ballot(a0[g] > a1[g]) & vm;   // node.ts:63-64
+          p1s[g] = ballot(a1[g] > a0[g]) & vm;   // node.ts:65-66 (else "?")
+        }
+        uint32_t st = 0;
+        // ---- P-phase ("voting phase", node.ts:83-158)
+        tally_sgpr<W>(p0s, p1s, a0, a1);
+#else
         uint32_t st = 0;
         Unroll<W>::run([&](auto gi) {
           constexpr int g = decltype(gi)::value;
@@ -240,6 +309,7 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
         if (lane < 4u * W) reinterpret_cast<uint32_t *>(P)[lane] = st;
         // ---- P-phase ("voting phase", node.ts:83-158)
         tally_plane<W>(P, a0, a1);
+#endif
         bool done = true;
         Unroll<W>::run([&](auto gi) {
           constexpr int g = decltype(gi)::value;
