@@ -34,6 +34,8 @@ BO_ERR_OUT_OF_RANGE = 6
 BO_ERR_UNSUPPORTED = 7
 BO_MODE_LOCKSTEP = 0
 BO_MODE_RANDOM_DELIVERY = 1
+BO_MODE_EVENT = 2
+NEVER = 0xFFFFFFFF             # crash_at entry: never stopped
 BO_INIT_RANDOM = 0
 BO_INIT_FIXED = 1
 BO_MAX_N = 4096
@@ -65,7 +67,14 @@ class TrialsCfgC(ctypes.Structure):
     _fields_ = [("N", ctypes.c_uint32), ("F", ctypes.c_uint32), ("k_max", ctypes.c_uint32),
                 ("init_mode", ctypes.c_uint32), ("mode", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
                 ("seed", ctypes.c_uint64), ("faulty", ctypes.POINTER(ctypes.c_uint8)),
-                ("init", ctypes.POINTER(ctypes.c_int8))]
+                ("init", ctypes.POINTER(ctypes.c_int8)), ("crash_at", ctypes.POINTER(ctypes.c_uint32)),
+                ("crash_count", ctypes.c_uint32), ("crash_window", ctypes.c_uint32)]
+
+
+def _crash_array(N, crash_at):
+    if crash_at is None:
+        return None
+    return (ctypes.c_uint32 * max(1, N))(*[NEVER if v is None else int(v) for v in crash_at])
 
 
 _lib = None
@@ -270,7 +279,8 @@ class TrialsPlan:
 
     def __init__(self, N: int, F: int, faulty: Sequence[bool] | None = None, *, seed: int = 0,
                  k_max: int = DEFAULT_K_MAX, initial_values: Sequence | None = None,
-                 mode: int = BO_MODE_LOCKSTEP):
+                 mode: int = BO_MODE_LOCKSTEP, crash_at: Sequence | None = None, crash_count: int = 0,
+                 crash_window: int = 0):
         if faulty is None:                       # start.ts:7-18 placement: the first F nodes
             faulty = [i < F for i in range(N)]
         self.N, self.F, self.k_max, self.seed = N, F, k_max, seed
@@ -282,9 +292,12 @@ class TrialsPlan:
             self._init = (ctypes.c_int8 * max(1, N))(*[_VAL[v] for v in initial_values])
             init_mode = BO_INIT_FIXED
         self.mode = mode
+        self._crash = _crash_array(N, crash_at)
         self._cfg = TrialsCfgC(N, F, k_max, init_mode, mode, 0, seed,
                                ctypes.cast(self._fl, ctypes.POINTER(ctypes.c_uint8)),
-                               ctypes.cast(self._init, ctypes.POINTER(ctypes.c_int8)))
+                               ctypes.cast(self._init, ctypes.POINTER(ctypes.c_int8)),
+                               ctypes.cast(self._crash, ctypes.POINTER(ctypes.c_uint32)) if self._crash else None,
+                               crash_count, crash_window)
         h = ctypes.c_void_p()
         _check(lib().bo_plan_create(ctypes.byref(self._cfg), ctypes.byref(h)))
         self._h = h
@@ -323,7 +336,8 @@ class TrialsPlan:
 
 def run_trial_states(N: int, F: int, faulty: Sequence[bool], *, seed: int = 0, trial: int = 0,
                      k_max: int = DEFAULT_K_MAX, initial_values: Sequence | None = None,
-                     mode: int = BO_MODE_LOCKSTEP):
+                     mode: int = BO_MODE_LOCKSTEP, crash_at: Sequence | None = None, crash_count: int = 0,
+                     crash_window: int = 0):
     """Per-node final states of one trial: (rounds, [NodeState dict] * N)."""
     fl = (ctypes.c_uint8 * max(1, N))(*[1 if v else 0 for v in faulty])
     if initial_values is None:
@@ -332,9 +346,11 @@ def run_trial_states(N: int, F: int, faulty: Sequence[bool], *, seed: int = 0, t
     else:
         init = (ctypes.c_int8 * max(1, N))(*[_VAL[v] for v in initial_values])
         init_mode = BO_INIT_FIXED
+    ca = _crash_array(N, crash_at)
     cfg = TrialsCfgC(N, F, k_max, init_mode, mode, 0, seed,
                      ctypes.cast(fl, ctypes.POINTER(ctypes.c_uint8)),
-                     ctypes.cast(init, ctypes.POINTER(ctypes.c_int8)))
+                     ctypes.cast(init, ctypes.POINTER(ctypes.c_int8)),
+                     ctypes.cast(ca, ctypes.POINTER(ctypes.c_uint32)) if ca else None, crash_count, crash_window)
     st = (NodeStateC * max(1, N))()
     rounds = ctypes.c_uint32(0)
     _check(lib().bo_run_trial_states(ctypes.byref(cfg), trial, st, ctypes.byref(rounds)))

@@ -14,6 +14,8 @@ namespace benor {
 constexpr uint32_t kStreamCoin = 0u;
 constexpr uint32_t kStreamInit = 1u;
 constexpr uint32_t kStreamDelivery = 2u;
+constexpr uint32_t kStreamOrder = 3u;
+constexpr uint32_t kStreamCrash = 4u;
 
 constexpr int kWavesPerBlock = 4;          // 256-thread workgroups, one trial per wave
 constexpr uint32_t kMaxW = BO_MAX_N / 64;  // u64 words per bit plane at N = 4096
@@ -42,6 +44,14 @@ struct KParams {
   unsigned long long *hist;        // [hist_len] (device, accumulated)
   bo_node_state *node_out;         // [N] (device) or nullptr; only with trial_count == 1
   uint32_t *rounds_out;            // (device) or nullptr
+  // event-level mode (variant 4)
+  uint64_t faulty_mask;            // N <= 64
+  const int8_t *init_x;            // [N] (device; fixed init)
+  const uint32_t *crash_at;        // [N] (device) or nullptr
+  uint32_t crash_count, crash_window;
+  uint32_t ev_cap, ev_stride;      // per-lane pool capacity and scratch stride (u32 words)
+  uint64_t ev_lanes;               // lanes the scratch buffer holds
+  uint32_t *scratch;               // [ev_lanes][ev_stride]
 };
 
 // Pick the tally block size G and fill nblocks / LDS sizes.

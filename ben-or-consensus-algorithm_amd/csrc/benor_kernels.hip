@@ -239,7 +239,6 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
   uint32_t *lhist = reinterpret_cast<uint32_t *>(smem);
   uint4 *ring = reinterpret_cast<uint4 *>(smem + p.hist_bytes + wv * p.wave_bytes);   // [TB][W]
   uint4 *X = ring + TB * W;                                                              // [W]
-  uint4 *P = X + W;                                                                      // [W]
 
   for (uint32_t i = threadIdx.x; i < p.hist_len; i += blockDim.x) lhist[i] = 0u;
   if (p.init_mode != BO_INIT_RANDOM && lane < (uint32_t)W) ring[lane] = p.init_plane[lane];
@@ -765,6 +764,220 @@ __global__ void __launch_bounds__(256) benor_random_kernel(KParams p) {
   }
 }
 
+
+// ------------------------------------------------ event-level kernel (N <= 64)
+// message-granular simulation with the reference's literal
+// handler (node.ts:45-158), a seeded delivery order and mid-run GET /stop
+// (node.ts:191-194).  Definition: oracle/benor_oracle.c event_trial().  One
+// lane = one trial; each lane runs its own event loop over a message pool in
+// its slice of an HBM scratch buffer (pool of 4N^2+64 messages, per-node
+// inbox counters for a 4-round window, x / k per node, completion masks,
+// sorted crash list).  Exactly F nodes are crash-faulty from the start
+// (launchNodes.ts:12-13), so every trigger fires once: the window of rounds a
+// node can receive for is {k, k+1}, and round k's slots are recycled for
+// round k+4.
+__device__ __forceinline__ uint64_t splitmix64(uint64_t &s) {
+  uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+struct EvLane {
+  uint32_t *pool;      // [cap]
+  uint32_t *ibox;      // [N][4][2] packed {c0, c1, len} bytes
+  int8_t *xs;          // [N]
+  int16_t *ks;         // [N]
+  uint64_t *comp;      // [4] completion masks, round k at k & 3
+  uint32_t *crash;     // [64] sorted (event << 6 | node)
+};
+
+__global__ void __launch_bounds__(256) benor_event_kernel(KParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint32_t *lhist = reinterpret_cast<uint32_t *>(smem);
+  for (uint32_t i = threadIdx.x; i < p.hist_len; i += blockDim.x) lhist[i] = 0u;
+  __syncthreads();
+
+  const uint32_t N = p.N, F = p.F, quorum = p.N - p.F, m = p.m;
+  const uint64_t all = N == 64 ? ~0ull : ((1ull << N) - 1ull);
+  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t lanes = (uint64_t)gridDim.x * blockDim.x;
+  const uint32_t cap = p.ev_cap;
+  uint32_t *base = p.scratch + gid * p.ev_stride;
+  EvLane L;
+  L.pool = base;
+  L.ibox = L.pool + cap;
+  L.comp = reinterpret_cast<uint64_t *>(L.ibox + N * 8u);
+  L.crash = reinterpret_cast<uint32_t *>(L.comp + 4);
+  L.xs = reinterpret_cast<int8_t *>(L.crash + 64);
+  L.ks = reinterpret_cast<int16_t *>(L.xs + 64);
+  const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
+
+  for (uint64_t t = gid; t < p.trial_count; t += lanes) {
+    const uint64_t trial = p.trial_begin + t;
+    const uint32_t tlo = (uint32_t)trial, thi = (uint32_t)(trial >> 32);
+    uint64_t killed = p.faulty_mask, decided = 0;
+    // ---- node.ts:21-26 and initial values (compact live order)
+    uint4 ir = make_uint4(0, 0, 0, 0);
+    if (p.init_mode == BO_INIT_RANDOM) ir = philox4x32_10(k0, k1, make_uint4(tlo, thi, 0u, kStreamInit << 24));
+    for (uint32_t c = 0; c < m; ++c) {
+      const uint32_t i = p.live_ids[c];
+      int8_t v;
+      if (p.init_mode == BO_INIT_RANDOM) v = (int8_t)((((c >> 5) ? ir.y : ir.x) >> (c & 31u)) & 1u);
+      else v = p.init_x[i];
+      L.xs[i] = v;
+      L.ks[i] = 0;
+    }
+    for (uint32_t i = 0; i < N; ++i)
+      if ((killed >> i) & 1ull) { L.xs[i] = -1; L.ks[i] = -1; }
+    for (uint32_t j = 0; j < N * 8u; ++j) L.ibox[j] = 0u;
+    for (int j = 0; j < 4; ++j) L.comp[j] = 0ull;
+    // ---- mid-run /stop schedule, sorted by event index
+    uint32_t ncrash = 0;
+    if (p.crash_at) {
+      for (uint32_t i = 0; i < N; ++i)
+        if (p.crash_at[i] != 0xFFFFFFFFu && p.crash_at[i] < (1u << 26)) L.crash[ncrash++] = (p.crash_at[i] << 6) | i;
+    } else if (p.crash_count > 0 && m > 0 && p.crash_window > 0) {
+      DStream ds;
+      ds.k0 = k0; ds.k1 = k1; ds.c0 = tlo; ds.c1 = thi; ds.c2 = 0u; ds.c3 = kStreamCrash << 24; ds.widx = 0;
+      const uint32_t kk = p.crash_count < m ? p.crash_count : m;
+      uint64_t T = 0;
+      uint32_t picks[64];
+      uint32_t n = 0;
+      for (uint32_t j = m - kk; j < m; ++j, ++n) {
+        const uint32_t tt = ds.uniform(j + 1u);
+        const uint32_t idx = ((T >> tt) & 1ull) ? j : tt;
+        T |= 1ull << idx;
+        picks[n] = idx;
+      }
+      for (uint32_t q2 = 0; q2 < kk; ++q2) {
+        const uint32_t when = ds.uniform(p.crash_window);
+        if (when < (1u << 26)) L.crash[ncrash++] = (when << 6) | p.live_ids[picks[q2]];
+      }
+    }
+    for (uint32_t a = 1; a < ncrash; ++a) {            // insertion sort (<= 64 entries)
+      const uint32_t v = L.crash[a];
+      uint32_t b = a;
+      while (b > 0 && L.crash[b - 1] > v) { L.crash[b] = L.crash[b - 1]; --b; }
+      L.crash[b] = v;
+    }
+    uint32_t next = 0;
+    // ---- delivery order
+    uint64_t rng;
+    {
+      const uint4 o = philox4x32_10(k0, k1, make_uint4(tlo, thi, 0u, kStreamOrder << 24));
+      rng = (((uint64_t)o.x << 32) | o.y) ^ 0xD1B54A32D192ED03ull;
+    }
+    // ---- /start (node.ts:167-188)
+    uint32_t len = 0;
+    for (uint32_t i = 0; i < N; ++i) {
+      if ((killed >> i) & 1ull) continue;
+      L.ks[i] = 1;
+      const uint32_t body = ((uint32_t)(L.xs[i] & 3) << 7) | (1u << 9);
+      for (uint32_t to = 0; to < N; ++to) L.pool[len++] = to | body;
+    }
+    uint32_t cur = 1, R = 0, halted = 0;
+    bool overflow = false;
+    for (uint32_t e = 0;; ++e) {
+      // scheduled GET /stop (node.ts:191-194)
+      bool crashed = false;
+      while (next < ncrash && (L.crash[next] >> 6) == e) {
+        const uint32_t i = L.crash[next] & 63u;
+        killed |= 1ull << i;
+        crashed = true;
+        ++next;
+      }
+      if (crashed) {
+        if (killed == all) { halted = 3; break; }
+        while ((L.comp[cur & 3u] | killed) == all) {
+          if ((decided | killed) == all) { halted = 1; R = cur; break; }
+          if (cur >= p.k_max) { halted = 2; R = cur; break; }
+          L.comp[cur & 3u] = 0ull;
+          ++cur;
+        }
+        if (halted) break;
+      }
+      if (len == 0) { halted = 3; break; }
+      const uint32_t pick = (uint32_t)(((uint64_t)(uint32_t)(splitmix64(rng) >> 32) * (uint64_t)len) >> 32);
+      const uint32_t msg = L.pool[pick];
+      L.pool[pick] = L.pool[--len];
+      const uint32_t to = msg & 63u, ph = (msg >> 6) & 1u, k = msg >> 9;
+      const uint32_t x = (msg >> 7) & 3u;
+      if ((killed >> to) & 1ull) continue;             // node.ts:45
+      uint32_t *bx = &L.ibox[(to * 4u + (k & 3u)) * 2u + ph];
+      uint32_t b = *bx;
+      b += 1u << 16;                                   // len
+      if (x == 0u) b += 1u;                            // c0
+      else if (x == 1u) b += 1u << 8;                  // c1
+      *bx = b;
+      if ((b >> 16) != quorum) continue;               // node.ts:52, :88 (fires once: exactly F faulty)
+      const uint32_t c0 = b & 0xFFu, c1 = (b >> 8) & 0xFFu;
+      uint32_t body;
+      if (ph == 0u) {                                  // node.ts:53-80
+        const uint32_t v = c0 > c1 ? 0u : (c1 > c0 ? 1u : 2u);
+        body = (1u << 6) | (v << 7) | (k << 9);
+      } else {                                         // node.ts:89-157
+        int8_t nx;
+        if (c0 > F) { nx = 0; decided |= 1ull << to; }
+        else if (c1 > F) { nx = 1; decided |= 1ull << to; }
+        else if (c0 + c1 > 0 && c0 > c1) nx = 0;
+        else if (c0 + c1 > 0 && c0 < c1) nx = 1;
+        else {
+          const uint4 rr = philox4x32_10(k0, k1, make_uint4(tlo, thi, to, (k & 0x00FFFFFFu) | (kStreamCoin << 24)));
+          nx = (rr.x > 0x80000000u) ? 0 : 1;           // node.ts:111
+        }
+        L.xs[to] = nx;
+        L.ks[to] = (int16_t)(k + 1u);
+        L.ibox[(to * 4u + ((k + 2u) & 3u)) * 2u + 0u] = 0u;   // recycle round k-2's slots for k+2
+        L.ibox[(to * 4u + ((k + 2u) & 3u)) * 2u + 1u] = 0u;
+        L.comp[k & 3u] |= 1ull << to;
+        while ((L.comp[cur & 3u] | killed) == all) {
+          if ((decided | killed) == all) { halted = 1; R = cur; break; }
+          if (cur >= p.k_max) { halted = 2; R = cur; break; }
+          L.comp[cur & 3u] = 0ull;
+          ++cur;
+        }
+        if (halted) break;
+        body = ((uint32_t)(nx & 3) << 7) | ((k + 1u) << 9);
+      }
+      if (len + N > cap) { overflow = true; halted = 3; break; }
+      for (uint32_t dst = 0; dst < N; ++dst) L.pool[len++] = dst | body;
+    }
+    // ---- outcome over the nodes still running
+    bool any0 = false, any1 = false, anyq = false;
+    uint32_t nlive = 0;
+    for (uint32_t i = 0; i < N; ++i) {
+      if ((killed >> i) & 1ull) continue;
+      ++nlive;
+      const int8_t v = L.xs[i];
+      if (v == 0) any0 = true; else if (v == 1) any1 = true; else anyq = true;
+    }
+    const uint32_t v = (nlive == 0 || anyq || (any0 && any1)) ? 2u : (any1 ? 1u : 0u);
+    atomicAdd(&lhist[halted == 1 ? (R * 3u + v) : v], 1u);
+    if (halted == 1 && v == 2u) atomicAdd(&lhist[p.hist_len - 1u], 1u);
+    if (overflow && p.rounds_out) atomicOr(p.rounds_out, 0x80000000u);
+    if (p.node_out) {
+      for (uint32_t i = 0; i < N; ++i) {
+        const bool f = (p.faulty_mask >> i) & 1ull;
+        bo_node_state ns;
+        ns.killed = (int8_t)((killed >> i) & 1ull);
+        ns.x = L.xs[i];
+        ns.decided = f ? (int8_t)-1 : (int8_t)((decided >> i) & 1ull);
+        ns.pad = 0;
+        ns.k = L.ks[i];
+        p.node_out[i] = ns;
+      }
+      if (p.rounds_out) atomicOr(p.rounds_out, halted == 1 ? R : 0u);
+    }
+  }
+
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < p.hist_len; i += blockDim.x) {
+    const uint32_t c = lhist[i];
+    if (c) atomicAdd(&p.hist[i], (unsigned long long)c);
+  }
+}
+
 // --------------------------------------------------- popcount peak probe
 // Eight independent v_bcnt_u32_b32 chains per lane; the roofline's `peak`
 // is the spec VALU rate, this probe says what the part sustains.
@@ -791,6 +1004,18 @@ void plan_geometry(KParams &p) {
   const uint32_t W = p.W;
   p.hist_len = (p.k_max + 1u) * 3u + 1u;
   p.hist_bytes = ((p.hist_len * 4u) + 15u) & ~15u;
+  if (p.mode == BO_MODE_EVENT) {
+    p.G = 1;
+    p.nblocks = 1;
+    p.variant = 4;
+    p.wave_bytes = 0;
+    p.lds_bytes = p.hist_bytes;
+    // per-lane scratch (u32 words): pool, inbox window, comp[4] (u64), crash[64], xs[64] (i8), ks[64] (i16)
+    p.ev_cap = 4u * p.N * p.N + 64u;
+    p.ev_stride = p.ev_cap + p.N * 8u + 8u + 64u + 16u + 32u;
+    p.ev_stride = (p.ev_stride + 31u) & ~31u;
+    return;
+  }
   if (p.mode == BO_MODE_RANDOM_DELIVERY) {
     p.G = 1;
     p.nblocks = W;
@@ -804,7 +1029,7 @@ void plan_geometry(KParams &p) {
     p.G = W;
     p.nblocks = 1;
     p.variant = 1;
-    p.wave_bytes = (tb * W + 2u * W) * 16u;
+    p.wave_bytes = (tb * W + W) * 16u;
   } else {
     const uint32_t nb = (W + 15u) / 16u;           // blocks of at most 16 groups
     const uint32_t G = (W + nb - 1u) / nb;         // balanced: padding < nb groups
@@ -844,6 +1069,10 @@ static hipError_t dispatch_b(const KParams &p, int grid, hipStream_t s, std::int
 }
 
 hipError_t launch_lockstep(const KParams &p, int grid, hipStream_t s) {
+  if (p.variant == 4) {
+    hipLaunchKernelGGL(benor_event_kernel, dim3(grid), dim3(256), p.lds_bytes, s, p);
+    return hipGetLastError();
+  }
   if (p.variant == 2) {
     if (p.lds_bytes > 64u * 1024u) {
       hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&benor_random_kernel),
@@ -860,6 +1089,12 @@ hipError_t launch_lockstep(const KParams &p, int grid, hipStream_t s) {
 int lockstep_grid(const KParams &p, int device) {
   int cus = 256;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+  if (p.variant == 4) {   // event mode: one lane per trial, grid = the scratch's lane count
+    const uint64_t blocks_needed = (p.trial_count + 255u) / 256u;
+    uint64_t grid = p.ev_lanes / 256u;
+    if (blocks_needed < grid) grid = blocks_needed;
+    return (int)(grid < 1 ? 1 : grid);
+  }
   // 8 workgroups (32 waves) per CU when registers and LDS allow it.
   const uint64_t waves_needed = p.trial_count;
   const uint64_t blocks_needed = (waves_needed + kWavesPerBlock - 1) / kWavesPerBlock;

@@ -270,6 +270,7 @@ typedef struct {
     int8_t *init;
     uint64_t trial_begin, trial_count;
     uint64_t *hist;
+    uint32_t *crash;
     uint32_t hlen;
     int rc;
     char err[512];
@@ -301,6 +302,7 @@ static void trials_complete(napi_env env, napi_status status, void *data) {
     free(j->faulty);
     free(j->init);
     free(j->hist);
+    free(j->crash);
     free(j);
 }
 
@@ -344,7 +346,11 @@ static napi_value run_trials(napi_env env, napi_callback_info info) {
     j->cfg.seed = prop_u64(env, o, "seed", 0);
     j->trial_begin = prop_u64(env, o, "trialBegin", 0);
     j->trial_count = prop_u64(env, o, "trialCount", 1);
-    j->cfg.mode = BO_MODE_LOCKSTEP;
+    uint32_t mode = BO_MODE_LOCKSTEP;
+    prop_u32(env, o, "mode", BO_MODE_LOCKSTEP, &mode);          /* 0 lockstep, 1 random delivery, 2 event */
+    j->cfg.mode = mode;
+    prop_u32(env, o, "crashCount", 0, &j->cfg.crash_count);
+    prop_u32(env, o, "crashWindow", 0, &j->cfg.crash_window);
     const uint32_t N = j->cfg.N;
     j->faulty = (uint8_t *)calloc(N + 1, 1);
     j->init = (int8_t *)calloc(N + 1, 1);
@@ -376,6 +382,27 @@ static napi_value run_trials(napi_env env, napi_callback_info info) {
                 napi_get_element(env, arr, i, &e);
                 j->init[i] = encode_value(env, e);
             }
+    }
+    napi_has_named_property(env, o, "crashAt", &has);
+    if (has) {                                                   /* EVENT mode /stop schedule */
+        napi_get_named_property(env, o, "crashAt", &arr);
+        uint32_t n = 0;
+        if (read_array(env, arr, &n)) {
+            j->crash = (uint32_t *)malloc(sizeof(uint32_t) * (N + 1));
+            for (uint32_t i = 0; i < N; ++i) j->crash[i] = 0xFFFFFFFFu;
+            for (uint32_t i = 0; i < n && i < N; ++i) {
+                napi_value e;
+                napi_valuetype t;
+                napi_get_element(env, arr, i, &e);
+                napi_typeof(env, e, &t);
+                if (t == napi_number) {
+                    double d = 0;
+                    napi_get_value_double(env, e, &d);
+                    if (d >= 0 && d < 4294967295.0) j->crash[i] = (uint32_t)d;
+                }
+            }
+            j->cfg.crash_at = j->crash;
+        }
     }
     j->cfg.faulty = j->faulty;
     j->cfg.init = j->init;

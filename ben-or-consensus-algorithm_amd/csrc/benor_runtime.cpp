@@ -71,6 +71,9 @@ struct bo_plan {
   std::vector<uint32_t> live_ids;
   uint32_t *d_live = nullptr;
   uint4 *d_init = nullptr;
+  int8_t *d_init_x = nullptr;      // event mode
+  uint32_t *d_crash = nullptr;     // event mode
+  uint32_t *d_scratch = nullptr;   // event mode
   int device = 0;
 };
 
@@ -195,8 +198,9 @@ int bo_plan_create(const bo_trials_cfg *cfg, bo_plan **out) {
   *out = nullptr;
   if (cfg->N < 1 || cfg->N > BO_MAX_N) return fail(BO_ERR_UNSUPPORTED, "N must be in [1, 4096]");
   if (cfg->k_max < 1 || cfg->k_max > BO_MAX_K) return fail(BO_ERR_INVALID_ARGUMENT, "k_max must be in [1, 1024]");
-  if (cfg->mode != BO_MODE_LOCKSTEP && cfg->mode != BO_MODE_RANDOM_DELIVERY)
+  if (cfg->mode != BO_MODE_LOCKSTEP && cfg->mode != BO_MODE_RANDOM_DELIVERY && cfg->mode != BO_MODE_EVENT)
     return fail(BO_ERR_UNSUPPORTED, "unknown delivery mode");
+  if (cfg->mode == BO_MODE_EVENT && cfg->N > 64) return fail(BO_ERR_UNSUPPORTED, "event mode simulates N <= 64");
   if (cfg->init_mode != BO_INIT_RANDOM && cfg->init_mode != BO_INIT_FIXED)
     return fail(BO_ERR_INVALID_ARGUMENT, "unknown init_mode");
   if (!cfg->faulty) return fail(BO_ERR_INVALID_ARGUMENT, "faulty is NULL");
@@ -205,7 +209,8 @@ int bo_plan_create(const bo_trials_cfg *cfg, bo_plan **out) {
   for (uint32_t i = 0; i < cfg->N; ++i) f += cfg->faulty[i] ? 1u : 0u;
   // Lockstep = the reference's admissible inputs: exactly F crash faults
   // (launchNodes.ts:12-13).  Random delivery admits f <= F.
-  if (cfg->mode == BO_MODE_LOCKSTEP && f != cfg->F) return fail(BO_ERR_FAULTY_COUNT, "faultyList doesnt have F faulties");
+  if (cfg->mode != BO_MODE_RANDOM_DELIVERY && f != cfg->F)
+    return fail(BO_ERR_FAULTY_COUNT, "faultyList doesnt have F faulties");
   if (cfg->mode == BO_MODE_RANDOM_DELIVERY && f > cfg->F)
     return fail(BO_ERR_FAULTY_COUNT, "random delivery needs at most F crash-faulty nodes");
   int dev = 0;
@@ -216,6 +221,7 @@ int bo_plan_create(const bo_trials_cfg *cfg, bo_plan **out) {
   pl->cfg = *cfg;
   pl->cfg.faulty = nullptr;
   pl->cfg.init = nullptr;
+  pl->cfg.crash_at = nullptr;
   pl->device = dev;
   for (uint32_t i = 0; i < cfg->N; ++i)
     if (!cfg->faulty[i]) pl->live_ids.push_back(i);
@@ -230,6 +236,10 @@ int bo_plan_create(const bo_trials_cfg *cfg, bo_plan **out) {
   kp.seed = cfg->seed;
   kp.mode = cfg->mode;
   kp.q = cfg->N - cfg->F;
+  kp.crash_count = cfg->crash_count;
+  kp.crash_window = cfg->crash_window;
+  for (uint32_t i = 0; i < cfg->N && i < 64; ++i)
+    if (cfg->faulty[i]) kp.faulty_mask |= 1ull << i;
   if (m > 0) {
     benor::plan_geometry(kp);
     std::vector<uint4> plane(kp.W, make_uint4(0, 0, 0, 0));
@@ -250,6 +260,32 @@ int bo_plan_create(const bo_trials_cfg *cfg, bo_plan **out) {
     if (e != hipSuccess) { bo_plan_destroy(pl); return hip_fail(e, "plan upload"); }
     kp.live_ids = pl->d_live;
     kp.init_plane = pl->d_init;
+    if (cfg->mode == BO_MODE_EVENT) {
+      std::vector<int8_t> ix(cfg->N, 0);
+      if (cfg->init_mode == BO_INIT_FIXED)
+        for (uint32_t i = 0; i < cfg->N; ++i) ix[i] = cfg->init[i];
+      // scratch: one slice per lane, at most ~4 GiB
+      const uint64_t stride_bytes = (uint64_t)kp.ev_stride * 4u;
+      int cus = 256;
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      uint64_t lanes = (uint64_t)cus * 8u * 256u;
+      const uint64_t fit = (4ull << 30) / stride_bytes;
+      if (fit < lanes) lanes = fit;
+      lanes = lanes / 256u * 256u;
+      if (lanes < 256u) lanes = 256u;
+      kp.ev_lanes = lanes;
+      e = hipMalloc(&pl->d_init_x, cfg->N);
+      if (e == hipSuccess) e = hipMemcpy(pl->d_init_x, ix.data(), cfg->N, hipMemcpyHostToDevice);
+      if (e == hipSuccess && cfg->crash_at) {
+        e = hipMalloc(&pl->d_crash, sizeof(uint32_t) * cfg->N);
+        if (e == hipSuccess) e = hipMemcpy(pl->d_crash, cfg->crash_at, sizeof(uint32_t) * cfg->N, hipMemcpyHostToDevice);
+      }
+      if (e == hipSuccess) e = hipMalloc(&pl->d_scratch, lanes * stride_bytes);
+      if (e != hipSuccess) { bo_plan_destroy(pl); return hip_fail(e, "event-mode scratch"); }
+      kp.init_x = pl->d_init_x;
+      kp.crash_at = pl->d_crash;
+      kp.scratch = pl->d_scratch;
+    }
   } else {
     kp.hist_len = bo_hist_len(cfg->k_max);
   }
@@ -261,6 +297,9 @@ void bo_plan_destroy(bo_plan *pl) {
   if (!pl) return;
   if (pl->d_live) (void)hipFree(pl->d_live);
   if (pl->d_init) (void)hipFree(pl->d_init);
+  if (pl->d_init_x) (void)hipFree(pl->d_init_x);
+  if (pl->d_crash) (void)hipFree(pl->d_crash);
+  if (pl->d_scratch) (void)hipFree(pl->d_scratch);
   delete pl;
 }
 

@@ -57,6 +57,13 @@ export interface TrialsConfig {
   kMax?: number;
   trialBegin?: bigint | number;
   trialCount?: bigint | number;
+  /** 0 lockstep (default), 1 random delivery (f <= F), 2 event level (N <= 64) */
+  mode?: 0 | 1 | 2;
+  /** event mode: deliveries after which node i is stopped (null = never) */
+  crashAt?: (number | null)[];
+  /** event mode, random schedule: stop crashCount live nodes at uniform delivery counts in [0, crashWindow) */
+  crashCount?: number;
+  crashWindow?: number;
 }
 
 /** Outcome histogram, (kMax + 1) * 3 + 1 bins (include/benor.h). */

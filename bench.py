@@ -97,9 +97,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    # one process per GPU; BENOR_DIST_BACKEND=gloo rehearses several ranks on one GPU
+    backend = os.environ.get("BENOR_DIST_BACKEND", "nccl")
+    dev = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
     N, F, k_max, T = args.N, args.F, args.k_max, args.trials
     faulty = [i < F for i in range(N)]
     plan = benor.TrialsPlan(N, F, faulty, seed=args.seed, k_max=k_max)

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define BENOR_ABI_VERSION 1
+#define BENOR_ABI_VERSION 2
 
 /* Return codes.  The first two are the reference's two launch errors. */
 enum {
@@ -48,7 +48,11 @@ enum {
  * exactly N-F of the N-f live senders drawn from Philox (no
  * reference counterpart -- the reference rejects f != F).  At f == F the two
  * modes give identical results. */
-enum { BO_MODE_LOCKSTEP = 0, BO_MODE_RANDOM_DELIVERY = 1 };
+/* EVENT is message-granular: the reference's handler
+ * (node.ts:45-158) delivery by delivery, in a seeded random order, with the
+ * reference's mid-run GET /stop (node.ts:191-194) applied at scheduled
+ * delivery counts.  Exactly F crash-faulty nodes; N <= 64. */
+enum { BO_MODE_LOCKSTEP = 0, BO_MODE_RANDOM_DELIVERY = 1, BO_MODE_EVENT = 2 };
 
 enum { BO_INIT_RANDOM = 0, BO_INIT_FIXED = 1 };
 
@@ -115,8 +119,15 @@ typedef struct bo_trials_cfg {
     uint32_t mode;            /* BO_MODE_LOCKSTEP or BO_MODE_RANDOM_DELIVERY */
     uint32_t reserved;
     uint64_t seed;            /* Philox4x32-10 key */
-    const uint8_t *faulty;    /* host [N]; exactly F set (LOCKSTEP), at most F (RANDOM_DELIVERY) */
+    const uint8_t *faulty;    /* host [N]; exactly F set (LOCKSTEP, EVENT), at most F (RANDOM_DELIVERY) */
     const int8_t *init;       /* host [N]; used when init_mode == BO_INIT_FIXED */
+    /* EVENT mode only: GET /stop schedule.  crash_at[i] = number of deliveries
+     * after which node i is stopped (UINT32_MAX = never), or, when crash_at is
+     * NULL, crash_count distinct live nodes stopped at uniform delivery counts
+     * in [0, crash_window), drawn per trial from Philox. */
+    const uint32_t *crash_at; /* host [N] or NULL */
+    uint32_t crash_count;
+    uint32_t crash_window;
 } bo_trials_cfg;
 
 /* Histogram length for a round cap: (k_max + 1) * 3 + 1 uint64 bins.

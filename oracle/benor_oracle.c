@@ -501,3 +501,208 @@ int oracle_run_trials(const orc_trials_cfg *cfg, uint64_t *hist, orc_node_state 
     free(live_ids);
     return 0;
 }
+
+/* ===================================================================== */
+/* (iii) event-level asynchronous mode                    */
+/* ===================================================================== */
+/* Message-granular restatement of node.ts:43-199 with the reference's own
+ * mid-run crash: GET /stop (node.ts:191-194) may hit a live node at any
+ * moment.  Per trial:
+ *   - /start (node.ts:167-188): every running node sets k = 1 and broadcasts
+ *     its x to all N nodes, in node order;
+ *   - events e = 0, 1, ...: first every scheduled /stop with crash_at[i] == e
+ *     is applied (node i killed, its x/decided/k kept), then one pending
+ *     message is delivered: index = (hi32(splitmix64) * len) >> 32 over the
+ *     pool, removed by swap-with-last; splitmix64 state =
+ *     (philox(ctr {trial, 0, 3<<24})[0] << 32 | [1]) ^ 0xD1B54A32D192ED03;
+ *   - delivery follows node.ts:45-158 literally (killed receivers drop,
+ *     `>= N-F` triggers, broadcasts to all N nodes);
+ *   - halting: round K is complete when every non-killed node has finished
+ *     its round-K P-phase; the network stops at the first complete round in
+ *     which every non-killed node has decided, or at round k_max, or when no
+ *     message is left (a stall: fewer than N-F senders remain).
+ * Random crash schedule (crash_at == NULL, crash_count > 0): Philox stream 4
+ * (ctr {trial, block << 12, 4 << 24}, words in order) picks crash_count
+ * distinct live nodes by Floyd's algorithm over compact live indices, then
+ * one uniform event index in [0, crash_window) per pick, in pick order. */
+typedef struct {
+    uint32_t N, F, k_max, init_mode;
+    uint64_t seed, trial_begin, trial_count;
+    const uint8_t *faulty;
+    const int8_t *init;
+    const uint32_t *crash_at;       /* [N] or NULL; UINT32_MAX = never */
+    uint32_t crash_count, crash_window;
+    int32_t threads;
+} orc_event_cfg;
+
+#define ORC_STREAM_CRASH 4u
+
+typedef struct { int8_t c0, c1, len, pad; } orc_ibox;
+
+/* One trial.  Returns the outcome bin (index into the histogram) and fills
+ * state_out[N] when given; *events_out = messages delivered. */
+static uint32_t event_trial(const orc_event_cfg *cfg, uint64_t trial, orc_node_state *st_out,
+                            uint64_t *events_out) {
+    const uint32_t N = cfg->N, F = cfg->F, KR = cfg->k_max + 3;
+    const int64_t quorum = (int64_t)N - (int64_t)F;
+    const size_t H = (size_t)(cfg->k_max + 1) * 3;
+    orc_node_state st[64];
+    uint32_t live_ids[64], m = 0;
+    uint64_t killed = 0, decided = 0, all = (N == 64) ? ~0ull : ((1ull << N) - 1);
+    for (uint32_t i = 0; i < N; ++i) {
+        const int f = cfg->faulty[i] != 0;
+        st[i].killed = (int8_t)f; st[i].decided = f ? -1 : 0; st[i].k = f ? -1 : 0; st[i].pad = 0;
+        st[i].x = -1;
+        if (f) killed |= 1ull << i; else live_ids[m++] = i;
+    }
+    for (uint32_t c = 0; c < m; ++c) {
+        const uint32_t i = live_ids[c];
+        st[i].x = (int8_t)(cfg->init_mode == 1 ? cfg->init[i] : oracle_random_init(cfg->seed, trial, c));
+    }
+    /* crash schedule */
+    uint32_t crash_at[64];
+    for (uint32_t i = 0; i < N; ++i) crash_at[i] = cfg->crash_at ? cfg->crash_at[i] : 0xFFFFFFFFu;
+    if (!cfg->crash_at && cfg->crash_count > 0 && m > 0 && cfg->crash_window > 0) {
+        orc_dstream s;
+        s.key[0] = (uint32_t)cfg->seed; s.key[1] = (uint32_t)(cfg->seed >> 32);
+        s.ctr[0] = (uint32_t)trial; s.ctr[1] = (uint32_t)(trial >> 32);
+        s.ctr[2] = 0; s.ctr[3] = ORC_STREAM_CRASH << 24; s.widx = 0;
+        const uint32_t k = cfg->crash_count < m ? cfg->crash_count : m;
+        uint64_t T = 0;
+        uint32_t picks[64];
+        for (uint32_t j = m - k, n = 0; j < m; ++j, ++n) {
+            const uint32_t t = dstream_uniform(&s, j + 1u);
+            const uint32_t idx = ((T >> t) & 1ull) ? j : t;
+            T |= 1ull << idx;
+            picks[n] = idx;
+        }
+        for (uint32_t n = 0; n < k; ++n) crash_at[live_ids[picks[n]]] = dstream_uniform(&s, cfg->crash_window);
+    }
+    /* inboxes[node][k][phase] */
+    orc_ibox *ib = (orc_ibox *)calloc((size_t)N * KR * 2, sizeof(orc_ibox));
+    uint64_t *comp = (uint64_t *)calloc(KR, sizeof(uint64_t));
+    uint8_t *pdone = (uint8_t *)calloc((size_t)N * KR, 1);
+    size_t cap = (size_t)4 * N * N + 64, len = 0;
+    uint32_t *pool = (uint32_t *)malloc(cap * sizeof(uint32_t));
+    /* message: to (6) | phase << 6 | (x & 3) << 7 | k << 9 */
+#define EV_SEND(K, X, PH)                                                               \
+    do {                                                                                \
+        for (uint32_t to_ = 0; to_ < N; ++to_) {                                        \
+            if (len == cap) { cap *= 2; pool = (uint32_t *)realloc(pool, cap * 4); }   \
+            pool[len++] = to_ | ((uint32_t)(PH) << 6) | ((uint32_t)((X) & 3) << 7) | ((uint32_t)(K) << 9); \
+        }                                                                               \
+    } while (0)
+    orc_rng rng;
+    rng.s = (((uint64_t)orc_philox_word(cfg->seed, trial, 0, ORC_STREAM_ORDER << 24, 0) << 32) |
+             orc_philox_word(cfg->seed, trial, 0, ORC_STREAM_ORDER << 24, 1)) ^ 0xD1B54A32D192ED03ull;
+    for (uint32_t i = 0; i < N; ++i)                    /* /start, node.ts:171-185 */
+        if (!((killed >> i) & 1ull)) { st[i].k = 1; EV_SEND(1u, st[i].x, 0u); }
+    uint32_t cur = 1, R = 0;
+    int halted = 0;                                      /* 1 decided, 2 k_max, 3 stall */
+    uint64_t e = 0;
+    for (;;) {
+        /* scheduled /stop (node.ts:191-194) */
+        int crashed = 0;
+        for (uint32_t i = 0; i < N; ++i)
+            if (crash_at[i] == e && !((killed >> i) & 1ull)) { killed |= 1ull << i; st[i].killed = 1; crashed = 1; }
+        if (crashed && killed == all) { halted = 3; break; }
+        if (crashed) {
+            while (cur < KR && (comp[cur] | killed) == all) {
+                if ((decided | killed) == all) { halted = 1; R = cur; break; }
+                if (cur >= cfg->k_max) { halted = 2; R = cur; break; }
+                ++cur;
+            }
+            if (halted) break;
+        }
+        if (len == 0) { halted = 3; break; }
+        const uint32_t pick = (uint32_t)(((uint64_t)(uint32_t)(orc_splitmix(&rng) >> 32) * (uint64_t)len) >> 32);
+        const uint32_t msg = pool[pick];
+        pool[pick] = pool[--len];
+        ++e;
+        const uint32_t to = msg & 63u, ph = (msg >> 6) & 1u, k = msg >> 9;
+        const int8_t x = (int8_t)((msg >> 7) & 3u);
+        if ((killed >> to) & 1ull) continue;             /* node.ts:45 */
+        if (k >= KR) continue;
+        orc_ibox *b = &ib[((size_t)to * KR + k) * 2 + ph];
+        b->len++;
+        if (x == 0) b->c0++; else if (x == 1) b->c1++;
+        if ((int64_t)b->len < quorum) continue;          /* node.ts:52, :88 */
+        const int c0 = b->c0, c1 = b->c1;
+        if (ph == 0) {                                   /* node.ts:53-80 */
+            const int8_t v = (c0 > c1) ? 0 : (c1 > c0) ? 1 : 2;
+            EV_SEND(k, v, 1u);
+        } else {                                         /* node.ts:89-157 */
+            if (c0 > (int)F) { st[to].x = 0; st[to].decided = 1; decided |= 1ull << to; }
+            else if (c1 > (int)F) { st[to].x = 1; st[to].decided = 1; decided |= 1ull << to; }
+            else if (c0 + c1 > 0 && c0 > c1) st[to].x = 0;
+            else if (c0 + c1 > 0 && c0 < c1) st[to].x = 1;
+            else st[to].x = (int8_t)oracle_coin(cfg->seed, trial, to, k);
+            st[to].k = (int32_t)k + 1;
+            uint8_t *pd = &pdone[(size_t)to * KR + k];
+            if (!*pd) {
+                *pd = 1;
+                comp[k] |= 1ull << to;
+                while (cur < KR && (comp[cur] | killed) == all) {
+                    if ((decided | killed) == all) { halted = 1; R = cur; break; }
+                    if (cur >= cfg->k_max) { halted = 2; R = cur; break; }
+                    ++cur;
+                }
+                if (halted) break;
+            }
+            EV_SEND(k + 1, st[to].x, 0u);
+        }
+    }
+#undef EV_SEND
+    free(ib); free(comp); free(pdone); free(pool);
+    if (events_out) *events_out = e;
+    /* outcome over the nodes still running */
+    int any0 = 0, any1 = 0, anyq = 0, nlive = 0;
+    for (uint32_t i = 0; i < N; ++i) {
+        if ((killed >> i) & 1ull) continue;
+        ++nlive;
+        if (st[i].x == 0) any0 = 1; else if (st[i].x == 1) any1 = 1; else anyq = 1;
+    }
+    const uint32_t v = (nlive == 0 || anyq || (any0 && any1)) ? 2u : (any1 ? 1u : 0u);
+    if (st_out) for (uint32_t i = 0; i < N; ++i) st_out[i] = st[i];
+    if (halted == 1) return (uint32_t)((size_t)R * 3 + v) | (v == 2 ? 0x80000000u : 0u);
+    (void)H;
+    return v;
+}
+
+/* Batch: hist as oracle_run_trials; events_out (optional) = total messages delivered. */
+int oracle_event_trials(const orc_event_cfg *cfg, uint64_t *hist, orc_node_state *node_out, uint64_t *events_out) {
+    if (cfg->k_max < 1 || cfg->N < 1 || cfg->N > 64) return -1;
+    uint32_t f = 0;
+    for (uint32_t i = 0; i < cfg->N; ++i) f += cfg->faulty[i] ? 1 : 0;
+    if (f != cfg->F) return -2;                          /* launchNodes.ts:12-13 */
+    const size_t HS = (size_t)(cfg->k_max + 1) * 3 + 1;
+    uint64_t ev = 0;
+    int nthreads = 1;
+#ifdef _OPENMP
+    nthreads = cfg->threads > 0 ? cfg->threads : omp_get_max_threads();
+#endif
+    if (node_out) nthreads = 1;
+    uint64_t *hl = (uint64_t *)calloc((size_t)nthreads * HS, sizeof(uint64_t));
+    uint64_t *el = (uint64_t *)calloc((size_t)nthreads, sizeof(uint64_t));
+#ifdef _OPENMP
+#pragma omp parallel for num_threads(nthreads) schedule(static)
+#endif
+    for (int64_t t = 0; t < (int64_t)cfg->trial_count; ++t) {
+        int tid = 0;
+#ifdef _OPENMP
+        tid = omp_get_thread_num();
+#endif
+        uint64_t e = 0;
+        const uint32_t bin = event_trial(cfg, cfg->trial_begin + (uint64_t)t, node_out, &e);
+        hl[(size_t)tid * HS + (bin & 0x7FFFFFFFu)]++;
+        if (bin & 0x80000000u) hl[(size_t)tid * HS + HS - 1]++;
+        el[tid] += e;
+    }
+    for (int t = 0; t < nthreads; ++t) {
+        for (size_t j = 0; j < HS; ++j) hist[j] += hl[(size_t)t * HS + j];
+        ev += el[t];
+    }
+    free(hl); free(el);
+    if (events_out) *events_out = ev;
+    return 0;
+}

@@ -64,6 +64,9 @@ def lib():
                                            ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                            ctypes.POINTER(ctypes.c_uint64)]
         L.oracle_delivery_mask.restype = None
+        L.oracle_event_trials.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
+                                          ctypes.POINTER(NodeState), ctypes.POINTER(ctypes.c_uint64)]
+        L.oracle_event_trials.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -132,7 +135,45 @@ def delivery_mask(seed, trial, node, rnd, phase, m, q) -> list[int]:
     return [int(D[i]) for i in range(W)]
 
 
-MODE_LOCKSTEP, MODE_RANDOM_DELIVERY = 0, 1
+MODE_LOCKSTEP, MODE_RANDOM_DELIVERY, MODE_EVENT = 0, 1, 2
+
+
+class EventCfg(ctypes.Structure):
+    _fields_ = [("N", ctypes.c_uint32), ("F", ctypes.c_uint32), ("k_max", ctypes.c_uint32),
+                ("init_mode", ctypes.c_uint32), ("seed", ctypes.c_uint64), ("trial_begin", ctypes.c_uint64),
+                ("trial_count", ctypes.c_uint64), ("faulty", ctypes.POINTER(ctypes.c_uint8)),
+                ("init", ctypes.POINTER(ctypes.c_int8)), ("crash_at", ctypes.POINTER(ctypes.c_uint32)),
+                ("crash_count", ctypes.c_uint32), ("crash_window", ctypes.c_uint32), ("threads", ctypes.c_int32)]
+
+
+NEVER = 0xFFFFFFFF
+
+
+def event_trials(N, F, faulty_list, *, seed=0, trial_begin=0, trial_count=1, k_max=64, initial_values=None,
+                 crash_at=None, crash_count=0, crash_window=0, threads=0, want_states=False):
+    """(iii) event-level mode: message-granular run with seeded delivery order
+    and scheduled (crash_at[i] = event index) or random mid-run /stop.
+    Returns (TrialsResult, events delivered)."""
+    f = (ctypes.c_uint8 * max(1, N))(*[1 if v else 0 for v in faulty_list])
+    if initial_values is None:
+        init, init_mode = (ctypes.c_int8 * max(1, N))(), 0
+    else:
+        init, init_mode = (ctypes.c_int8 * max(1, N))(*[VAL_CODE[v] for v in initial_values]), 1
+    ca = None
+    if crash_at is not None:
+        ca = (ctypes.c_uint32 * max(1, N))(*[NEVER if v is None else int(v) for v in crash_at])
+    cfg = EventCfg(N, F, k_max, init_mode, seed, trial_begin, trial_count,
+                   ctypes.cast(f, ctypes.POINTER(ctypes.c_uint8)), ctypes.cast(init, ctypes.POINTER(ctypes.c_int8)),
+                   ctypes.cast(ca, ctypes.POINTER(ctypes.c_uint32)) if ca is not None else None,
+                   crash_count, crash_window, threads)
+    hist = np.zeros(hist_len(k_max), dtype=np.uint64)
+    st = (NodeState * max(1, N))() if want_states else None
+    ev = ctypes.c_uint64(0)
+    rc = lib().oracle_event_trials(ctypes.byref(cfg), hist.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), st,
+                                   ctypes.byref(ev))
+    if rc != 0:
+        raise ValueError(f"oracle_event_trials rc={rc}")
+    return TrialsResult(hist, _states(st, N) if want_states else None), int(ev.value)
 
 
 def run_trials(N, F, faulty_list, *, seed=0, trial_begin=0, trial_count=1, k_max=64,

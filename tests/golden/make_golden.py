@@ -133,6 +133,20 @@ RANDOM_HIST_CASES = [
 RANDOM_STATE_CASES = [(12, 4, 1), (10, 4, 2), (100, 30, 5), (70, 40, 0), (130, 40, 10)]
 
 
+EVENT_HIST_CASES = [
+    # (N, F, trials, k_max, crash_count, crash_window): event-level mode, first F nodes faulty
+    (10, 4, 3000, 16, 0, 0), (10, 4, 3000, 16, 1, 150), (5, 1, 3000, 16, 1, 40), (16, 5, 1000, 16, 2, 400),
+    (33, 10, 300, 16, 1, 2000), (64, 21, 100, 16, 3, 8000), (12, 4, 2000, 16, 0, 0), (7, 3, 2000, 12, 1, 60),
+]
+
+EVENT_STATE_CASES = [
+    # (N, F, init, crash_at (None = never), trial)
+    (10, 4, [1] * 10, {7: 0}, 1), (10, 4, [1] * 10, {7: 60}, 7), (10, 4, [1] * 10, {7: 70}, 7),
+    (5, 1, [1, 1, 1, 0, 0], {0: 5}, 2), (6, 2, [0, 1, 0, 1, 1, 0], {2: 12, 3: 30}, 3),
+    (9, 4, [0, 0, 1, 1, 1, 0, 0, 1, 1], None, 4), (12, 4, [0, 1] * 6, {5: 100}, 5),
+]
+
+
 def encode_state(s):
     """NodeState -> [killed, x, decided, k] with null = -1 and '?' = 2."""
     x = {None: -1, 0: 0, 1: 1, "?": 2}[s["x"]]
@@ -188,10 +202,27 @@ def main():
                                     initial_values=init, want_states=True, mode=oracle.MODE_RANDOM_DELIVERY)
             rstates.append({"N": N, "F": F, "faulty": fl, "init": init, "seed": SEED + t, "trial": 50 + t,
                             "k_max": 24, "states": [encode_state(x) for x in res.states]})
+    ehists = []
+    for (N, F, ntr, k_max, cc, cw) in EVENT_HIST_CASES:
+        fl = first_f(N, F)
+        res, ev = oracle.event_trials(N, F, fl, seed=SEED ^ (N * 131 + cc), trial_begin=99, trial_count=ntr,
+                                      k_max=k_max, crash_count=cc, crash_window=cw)
+        ehists.append({"N": N, "F": F, "faulty": fl, "seed": SEED ^ (N * 131 + cc), "trial_begin": 99,
+                       "trial_count": ntr, "k_max": k_max, "crash_count": cc, "crash_window": cw, "events": ev,
+                       "hist_nonzero": {str(i): int(v) for i, v in enumerate(res.hist) if v}})
+    estates = []
+    for (N, F, init, crashes, trial) in EVENT_STATE_CASES:
+        fl = first_f(N, F)
+        ca = None if crashes is None else [crashes.get(i) for i in range(N)]
+        res, ev = oracle.event_trials(N, F, fl, seed=SEED, trial_begin=trial, trial_count=1, k_max=24,
+                                      initial_values=init, crash_at=ca, want_states=True)
+        estates.append({"N": N, "F": F, "faulty": fl, "init": init, "crash_at": ca, "seed": SEED, "trial": trial,
+                        "k_max": 24, "events": ev, "states": [encode_state(x) for x in res.states],
+                        "hist_nonzero": {str(i): int(v) for i, v in enumerate(res.hist) if v}})
     with open(os.path.join(HERE, "oracle_vectors.json"), "w") as f:
-        json.dump({"generator": "tests/golden/make_golden.py (oracle/benor_oracle.c restatements (i)+(ii))",
-                   "states": states, "hists": hists, "random_hists": rhists, "random_states": rstates}, f,
-                  separators=(",", ":"))
+        json.dump({"generator": "tests/golden/make_golden.py (oracle/benor_oracle.c restatements (i)+(ii)+(iii))",
+                   "states": states, "hists": hists, "random_hists": rhists, "random_states": rstates,
+                   "event_hists": ehists, "event_states": estates}, f, separators=(",", ":"))
     print(f"{len(states)} state cases, {len(hists)} histograms, {len(rhists)} random-delivery histograms, "
           f"{len(rstates)} random-delivery state cases")
 

@@ -202,3 +202,39 @@ def test_random_delivery_equals_lockstep_at_f_equals_F():
 def test_random_delivery_rejects_too_many_faults():
     with pytest.raises(benor.Error):
         benor.TrialsPlan(10, 2, first_f(10, 3), mode=RD)
+
+
+# ------------------------------------------------- event-level mode (N <= 64)
+EV = benor.BO_MODE_EVENT
+
+
+def test_event_mode_golden(oracle_vectors):
+    for h in oracle_vectors["event_hists"]:
+        plan = benor.TrialsPlan(h["N"], h["F"], h["faulty"], seed=h["seed"], k_max=h["k_max"], mode=EV,
+                                crash_count=h["crash_count"], crash_window=h["crash_window"])
+        got = plan.run(h["trial_begin"], h["trial_count"])
+        assert {str(i): int(v) for i, v in enumerate(got) if v} == h["hist_nonzero"], (h["N"], h["crash_count"])
+    for c in oracle_vectors["event_states"]:
+        _, st = benor.run_trial_states(c["N"], c["F"], c["faulty"], seed=c["seed"], trial=c["trial"],
+                                       k_max=c["k_max"], initial_values=c["init"], mode=EV, crash_at=c["crash_at"])
+        assert st == [decode_state(e) for e in c["states"]], c
+
+
+@pytest.mark.parametrize("N,F,cc,cw,trials", [(10, 4, 0, 0, 200_000), (10, 4, 1, 150, 200_000),
+                                              (20, 6, 2, 600, 20_000), (64, 21, 4, 10_000, 500),
+                                              (3, 1, 1, 6, 50_000), (1, 0, 0, 0, 1000)])
+def test_event_mode_matches_oracle(N, F, cc, cw, trials):
+    fl = first_f(N, F)
+    seed = 0xE7E7 ^ N
+    got = benor.TrialsPlan(N, F, fl, seed=seed, k_max=16, mode=EV, crash_count=cc, crash_window=cw).run(3, trials)
+    ref, _ = oracle.event_trials(N, F, fl, seed=seed, trial_begin=3, trial_count=trials, k_max=16,
+                                 crash_count=cc, crash_window=cw)
+    np.testing.assert_array_equal(got, ref.hist)
+
+
+def test_event_mode_without_stop_equals_lockstep_kernel():
+    for N, F in [(10, 4), (64, 21), (33, 0)]:
+        fl = first_f(N, F)
+        a = benor.TrialsPlan(N, F, fl, seed=8, k_max=16, mode=EV).run(0, 50_000)
+        b = benor.TrialsPlan(N, F, fl, seed=8, k_max=16).run(0, 50_000)
+        np.testing.assert_array_equal(a, b)

@@ -190,3 +190,47 @@ def test_random_delivery_relative_majority_can_split():
     r = oracle.run_trials(10, 2, [True] + [False] * 9, seed=2, trial_count=20000, k_max=16,
                           mode=oracle.MODE_RANDOM_DELIVERY)
     assert r.hist[-1] == 0
+
+
+# ------------------------------------------------- event-level mode
+@pytest.mark.parametrize("N,F", [(5, 1), (10, 4), (12, 4), (9, 4), (10, 5), (16, 5)])
+def test_event_mode_without_stop_equals_lockstep(N, F):
+    """Exactly F faults and no mid-run /stop: every delivery order gives the
+    lockstep outcome, per node and per histogram."""
+    fl = [i < F for i in range(N)]
+    a, ev = oracle.event_trials(N, F, fl, seed=21, trial_count=4000, k_max=16)
+    b = oracle.run_trials(N, F, fl, seed=21, trial_count=4000, k_max=16)
+    np.testing.assert_array_equal(a.hist, b.hist)
+    assert ev > 0
+    rng = np.random.default_rng(N)
+    for t in range(20):
+        init = [int(v) for v in rng.integers(0, 2, N)]
+        sa, _ = oracle.event_trials(N, F, fl, seed=5, trial_begin=t, trial_count=1, k_max=16, initial_values=init,
+                                    want_states=True)
+        sb = oracle.run_trials(N, F, fl, seed=5, trial_begin=t, trial_count=1, k_max=16, initial_values=init,
+                               want_states=True)
+        assert sa.states == sb.states
+
+
+def test_event_mode_stop_before_first_delivery_stalls():
+    """A live node stopped before the first delivery: its round-1 proposals
+    (already sent at /start) still arrive, so every running node completes the
+    R-phase, but only N-F-1 nodes send votes -- no P-phase trigger can fire
+    (node.ts:88); everyone sits at k = 1 (node.ts:172), undecided."""
+    N, F = 10, 4
+    ca = [None] * N
+    ca[6] = 0
+    r, ev = oracle.event_trials(N, F, [i < F for i in range(N)], seed=1, trial_count=1, k_max=16,
+                                initial_values=[1] * N, crash_at=ca, want_states=True)
+    live = r.states[F:]
+    assert live[2]["killed"] and all(s["k"] == 1 and s["decided"] is False for s in live)
+    assert r.hist[1] == 1 and ev == (N - F) * N + (N - F - 1) * N   # all round-1 messages, then nothing
+
+
+def test_event_mode_stop_after_decision_is_harmless():
+    N, F = 10, 4
+    ca = [None] * N
+    ca[7] = 10_000
+    r, _ = oracle.event_trials(N, F, [i < F for i in range(N)], seed=1, trial_begin=7, trial_count=1, k_max=16,
+                               initial_values=[1] * N, crash_at=ca, want_states=True)
+    assert all(s["decided"] and s["x"] == 1 and s["k"] == 2 for s in r.states[F:])
