@@ -1,6 +1,6 @@
 """Throughput of the round-loop kernels across network shapes (GPU).
 
-For each (N, F, f, mode) runs `trials` trials once for warm-up and once timed
+For each (N, F, f, mode) -- mode 0 lockstep, 1 random delivery, 2 event level -- runs `trials` trials once for warm-up and once timed
 with HIP events on the launch stream, and prints live node-rounds/s and the
 popcount-roofline fraction (4*ceil(m/32) words per live node-round vs the
 v_bcnt issue peak, 39.3 T/s).  One JSON line per shape.
@@ -23,6 +23,7 @@ SHAPES = [
     (1024, 0, 0, 0, 4_000_000), (1536, 512, 512, 0, 2_000_000), (2048, 682, 682, 0, 1_000_000),
     (4096, 1365, 1365, 0, 400_000), (4096, 0, 0, 0, 100_000),
     (10, 4, 2, 1, 2_000_000), (100, 30, 10, 1, 200_000), (1024, 341, 300, 1, 20_000), (1024, 341, 0, 1, 2_000),
+    (10, 4, 4, 2, 2_000_000), (32, 10, 10, 2, 200_000), (64, 21, 21, 2, 100_000),
 ]
 
 
@@ -59,10 +60,12 @@ def main():
         nr = rounds * m
         words = 4 * ((m + 31) // 32)
         rate = nr / (ms * 1e-3)
-        print(json.dumps({"N": N, "F": F, "f": f, "mode": ["lockstep", "random"][mode], "trials": trials,
+        print(json.dumps({"N": N, "F": F, "f": f, "mode": ["lockstep", "random", "event"][mode], "trials": trials,
                           "mean_rounds": rounds / trials, "ms": round(ms, 3), "node_rounds_per_s": rate,
                           "popc_frac": rate * words / PEAK,
-                          "agreement_violations": int(hist[-1])}), flush=True)
+                          "agreement_violations": int(hist[-1]),
+                          # event level: each live node-round is 2 broadcasts of N messages
+                          "messages_per_s": rate * 2 * N if mode == 2 else None}), flush=True)
 
 
 if __name__ == "__main__":
