@@ -20,6 +20,7 @@ constexpr uint32_t kStreamCrash = 4u;
 constexpr int kWavesPerBlock = 4;          // 256-thread workgroups, one trial per wave
 constexpr uint32_t kMaxW = BO_MAX_N / 64;  // u64 words per bit plane at N = 4096
 constexpr int kMaxWSpecialised = 16;       // m <= 1024: fully unrolled W-specialised kernel
+constexpr uint32_t kMaxPackedM = 32;       // m <= 32: packed kernel, floor(32/m) trials per half-wave
 
 struct KParams {
   uint32_t N, F;            // network size, fault parameter
@@ -27,7 +28,8 @@ struct KParams {
   uint32_t W;               // u64 words per plane = ceil(m / 64) = receiver groups
   uint32_t G;               // receiver groups per tally block (template parameter)
   uint32_t nblocks;         // ceil(W / G)
-  uint32_t variant;         // 1: W-specialised lockstep (W <= 16), 0: blocked lockstep, 2: random delivery
+  uint32_t variant;         // 5: packed lockstep (m <= 32), 1: W-specialised lockstep (W <= 16),
+                            // 0: blocked lockstep, 2: random delivery, 4: event level
   uint32_t mode;            // BO_MODE_LOCKSTEP / BO_MODE_RANDOM_DELIVERY
   uint32_t q;               // quorum N - F (messages each receiver tallies per phase)
   uint32_t k_max;

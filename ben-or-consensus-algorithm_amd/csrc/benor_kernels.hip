@@ -576,6 +576,156 @@ __global__ void __launch_bounds__(256) benor_lockstep_blocked_kernel(KParams p) 
 }
 
 
+// ------------------------------------------------ packed kernel (m <= 32)
+// Small networks (BASELINE configs C1 N=5, C2 N=10, and the C5 sweep's small
+// cells) would leave most of a wave idle with one trial per wave.  Here every
+// 32-lane half of a wave holds P = floor(32/m) independent trials
+// ("segments") of m lanes each, so one wave runs 2P trials concurrently:
+//
+//   * lane (h*32 + i*m + c) is live node c (compact order) of segment h*P + i;
+//   * a phase's messages for all segments are ONE pair of wave ballots
+//     {is0, is1}; each receiver tallies its own segment's bits:
+//     popcount((ballot >> 32h) & segment_mask) per count;
+//   * segments advance independently: when a segment's trial halts (every
+//     live node decided, or k_max rounds), its leader lane records the
+//     outcome and the segment pulls the wave's next trial from a per-wave
+//     queue.  Random initial values for the queue come from an LDS ring of
+//     128 words filled 64 trials per Philox pass (one trial per lane);
+//   * coins (node.ts:111) are per lane, only on rounds where some receiver ties.
+// Same outcome definition as the other lockstep kernels: the histogram is
+// bit-identical to theirs (the trial -> wave assignment only changes order).
+__device__ __forceinline__ uint32_t seg_tally(uint64_t plane, uint32_t half_shift, uint32_t segmask) {
+  // one receiver's count over its segment's senders (node.ts:56-62, :92-98)
+  return (uint32_t)__builtin_popcount((uint32_t)(plane >> half_shift) & segmask);
+}
+
+__global__ void __launch_bounds__(256) benor_packed_kernel(KParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = threadIdx.x >> 6;
+  const uint32_t m = p.m, F = p.F;
+  const uint32_t P = 32u / m;                       // segments per half
+  uint32_t *lhist = reinterpret_cast<uint32_t *>(smem);
+  uint32_t *ring = reinterpret_cast<uint32_t *>(smem + p.hist_bytes + wv * p.wave_bytes);   // [128]
+
+  for (uint32_t i = threadIdx.x; i < p.hist_len; i += blockDim.x) lhist[i] = 0u;
+  __syncthreads();
+
+  const uint32_t hl = lane & 31u;
+  const uint32_t si = hl / m;                       // segment index within the half
+  const uint32_t c = hl - si * m;                   // compact live index of this lane's node
+  const bool valid = si < P;
+  const uint32_t half_shift = lane & 32u;
+  const uint32_t mbits = m == 32u ? ~0u : ((1u << m) - 1u);
+  const uint32_t segmask = valid ? (mbits << (si * m)) : 0u;
+  const uint32_t node = valid ? p.live_ids[c] : 0u;
+  const bool random_init = p.init_mode == BO_INIT_RANDOM;
+  // fixed init (BO_INIT_FIXED): word 0 of the plane holds every live node (m <= 32)
+  const uint4 fixed = random_init ? make_uint4(0, 0, 0, 0) : p.init_plane[0];
+  const uint32_t fixed_x = ((fixed.z >> c) & 1u) ? 1u : (((fixed.x >> c) & 1u) ? 0u : 2u);
+
+  const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
+  const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
+  const uint64_t waves_total = (uint64_t)gridDim.x * kWavesPerBlock;
+
+  uint64_t next_j = 0, filled = 0;                  // wave queue: j-th trial of the wave = gw + j * waves_total
+  bool need = valid, act = false, dec = false;
+  uint32_t x = 2u, r = 0u;
+  uint64_t trial = 0;
+
+  for (;;) {
+    // ---- pull: segments that need a trial take the next queue entries (node.ts:167-188 /start)
+    const uint64_t Lb = ballot(need && c == 0u);
+    if (Lb) {
+      const uint32_t nf = (uint32_t)__builtin_popcountll(Lb);
+      if (random_init && next_j + nf > filled) {   // refill 64 ring slots, one trial per lane
+        const uint64_t j = filled + lane;
+        const uint64_t t = gw + j * waves_total;
+        if (t < p.trial_count) {
+          const uint64_t tr = p.trial_begin + t;
+          uint32_t kk0 = k0, kk1 = k1;
+          asm volatile("" : "+s"(kk0), "+s"(kk1));
+          ring[j & 127u] = philox4x32_10(kk0, kk1, make_uint4((uint32_t)tr, (uint32_t)(tr >> 32), 0u, kStreamInit << 24)).x;
+        }
+        filled += 64u;
+      }
+      if (need) {
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(Lb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)Lb, 0u));
+        const uint64_t j = next_j + below - (c ? 1u : 0u);
+        const uint64_t t = gw + j * waves_total;
+        need = false;
+        act = t < p.trial_count;
+        if (act) {
+          trial = p.trial_begin + t;
+          x = random_init ? ((ring[j & 127u] >> c) & 1u) : fixed_x;
+          dec = false;
+          r = 0u;
+        }
+      }
+      next_j += nf;
+    }
+    if (!__any(act)) break;
+
+    // ---- R-phase ("proposal phase", node.ts:46-82)
+    const uint64_t is0 = ballot(act && x == 0u), is1 = ballot(act && x == 1u);
+    const uint32_t c0 = seg_tally(is0, half_shift, segmask), c1 = seg_tally(is1, half_shift, segmask);
+    // ---- P-phase ("voting phase", node.ts:83-158)
+    const uint64_t p0 = ballot(act && c0 > c1), p1 = ballot(act && c1 > c0);   // node.ts:63-69 (else "?")
+    const uint32_t v0 = seg_tally(p0, half_shift, segmask), v1 = seg_tally(p1, half_shift, segmask);
+    ++r;
+    const bool d0 = v0 > F, d1 = !d0 && v1 > F;                                    // node.ts:99, :102
+    const bool tie = act && !d0 && !d1 && v0 == v1;                                // node.ts:110-111
+    uint32_t nx = d0 ? 0u : (d1 ? 1u : (v1 > v0 ? 1u : 0u));                        // node.ts:106-109
+    if (__any(tie)) {
+      uint32_t kk0 = k0, kk1 = k1;
+      asm volatile("" : "+s"(kk0), "+s"(kk1));
+      if (tie) {
+        const uint4 rr = philox4x32_10(kk0, kk1, make_uint4((uint32_t)trial, (uint32_t)(trial >> 32), node,
+                                                            (r & 0x00FFFFFFu) | (kStreamCoin << 24)));
+        nx = (rr.x > 0x80000000u) ? 0u : 1u;                                       // Math.random() > 0.5 ? 0 : 1
+      }
+    }
+    if (act) {
+      x = nx;
+      dec = dec || d0 || d1;                                                        // sticky (node.ts:100-105)
+    }
+    // ---- halt: every live node of the segment decided (auto-stop, node.ts:116-145) or k_max
+    const uint64_t db = ballot(act && dec);
+    const bool seg_done = seg_tally(db, half_shift, segmask) == m;
+    const bool fin = act && (seg_done || r >= p.k_max);
+    if (__any(fin)) {
+      const uint64_t n0 = ballot(act && x == 0u), n1 = ballot(act && x == 1u);
+      if (fin) {
+        const bool any0 = seg_tally(n0, half_shift, segmask) != 0u, any1 = seg_tally(n1, half_shift, segmask) != 0u;
+        const uint32_t v = (any0 && any1) ? 2u : (any1 ? 1u : 0u);
+        if (c == 0u) {
+          atomicAdd(&lhist[seg_done ? (r * 3u + v) : v], 1u);
+          if (seg_done && v == 2u) atomicAdd(&lhist[p.hist_len - 1u], 1u);
+          if (p.rounds_out) *p.rounds_out = seg_done ? r : 0u;
+        }
+        if (p.node_out) {                                                           // GET /getState (node.ts:197-199)
+          bo_node_state ns;
+          ns.killed = 0;
+          ns.x = (int8_t)x;
+          ns.decided = (int8_t)(dec ? 1 : 0);
+          ns.pad = 0;
+          ns.k = (int32_t)r + 1;                                                    // node.ts:147
+          p.node_out[node] = ns;
+        }
+        act = false;
+        need = true;
+      }
+    }
+  }
+
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < p.hist_len; i += blockDim.x) {
+    const uint32_t cnt = lhist[i];
+    if (cnt) atomicAdd(&p.hist[i], (unsigned long long)cnt);
+  }
+}
+
+
 // ----------------------------------------- random-delivery kernel (f <= F)
 // Generalised delivery: with f <= F crashed nodes every live
 // receiver tallies, per phase, a uniformly random subset of exactly q = N-F of
@@ -1024,6 +1174,14 @@ void plan_geometry(KParams &p) {
     p.lds_bytes = p.hist_bytes + kWavesPerBlock * p.wave_bytes;
     return;
   }
+  if (p.m <= kMaxPackedM) {                         // packed: floor(32/m) trials per half-wave
+    p.G = 1;
+    p.nblocks = 1;
+    p.variant = 5;
+    p.wave_bytes = 128u * 4u;                       // init-word ring
+    p.lds_bytes = p.hist_bytes + kWavesPerBlock * p.wave_bytes;
+    return;
+  }
   const uint32_t nph = (W + 1u) / 2u, tb = 64u / nph;   // init ring: tb trials per Philox pass
   if (W <= (uint32_t)kMaxWSpecialised) {
     p.G = W;
@@ -1073,6 +1231,10 @@ hipError_t launch_lockstep(const KParams &p, int grid, hipStream_t s) {
     hipLaunchKernelGGL(benor_event_kernel, dim3(grid), dim3(256), p.lds_bytes, s, p);
     return hipGetLastError();
   }
+  if (p.variant == 5) {
+    hipLaunchKernelGGL(benor_packed_kernel, dim3(grid), dim3(64 * kWavesPerBlock), p.lds_bytes, s, p);
+    return hipGetLastError();
+  }
   if (p.variant == 2) {
     if (p.lds_bytes > 64u * 1024u) {
       hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&benor_random_kernel),
@@ -1096,7 +1258,8 @@ int lockstep_grid(const KParams &p, int device) {
     return (int)(grid < 1 ? 1 : grid);
   }
   // 8 workgroups (32 waves) per CU when registers and LDS allow it.
-  const uint64_t waves_needed = p.trial_count;
+  const uint64_t per_wave = p.variant == 5 ? 2u * (32u / p.m) : 1u;   // trials a wave runs at once
+  const uint64_t waves_needed = (p.trial_count + per_wave - 1u) / per_wave;
   const uint64_t blocks_needed = (waves_needed + kWavesPerBlock - 1) / kWavesPerBlock;
   uint64_t per_cu = 8;
   if (p.lds_bytes > 0) {

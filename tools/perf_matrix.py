@@ -18,7 +18,8 @@ PEAK = 256 * 4 * 16 * 2.4e9
 
 SHAPES = [
     # N, F, f (crashed), mode, trials
-    (5, 1, 1, 0, 20_000_000), (10, 4, 4, 0, 20_000_000), (10, 5, 5, 0, 2_000_000), (64, 21, 21, 0, 10_000_000),
+    (5, 1, 1, 0, 20_000_000), (10, 4, 4, 0, 20_000_000), (10, 5, 5, 0, 2_000_000), (3, 1, 1, 0, 20_000_000),
+    (20, 6, 6, 0, 20_000_000), (40, 8, 8, 0, 10_000_000), (48, 20, 20, 0, 10_000_000), (64, 21, 21, 0, 10_000_000),
     (256, 85, 85, 0, 10_000_000), (512, 170, 170, 0, 10_000_000), (1024, 341, 341, 0, 20_000_000),
     (1024, 0, 0, 0, 4_000_000), (1536, 512, 512, 0, 2_000_000), (2048, 682, 682, 0, 1_000_000),
     (4096, 1365, 1365, 0, 400_000), (4096, 0, 0, 0, 100_000),
