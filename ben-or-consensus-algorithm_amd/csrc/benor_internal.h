@@ -34,6 +34,7 @@ struct KParams {
   uint32_t q;               // quorum N - F (messages each receiver tallies per phase)
   uint32_t k_max;
   uint32_t init_mode;       // BO_INIT_RANDOM / BO_INIT_FIXED
+  uint32_t init_q;          // live nodes whose fixed initial value is "?" (0 for random init)
   uint32_t hist_len;        // (k_max + 1) * 3 + 1
   uint32_t lds_bytes;       // dynamic LDS per workgroup
   uint32_t wave_bytes;      // per-wave LDS region

@@ -34,8 +34,8 @@
 
 #include "benor_internal.h"
 
-#ifndef BENOR_P_SGPR
-#define BENOR_P_SGPR 1
+#ifndef BENOR_FUSED
+#define BENOR_FUSED 1
 #endif
 
 namespace benor {
@@ -75,6 +75,18 @@ __device__ __forceinline__ uint4 rec(uint64_t is0, uint64_t is1) {
 }
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+
+// Ballot whose SGPR result may feed an inline-asm VALU (v_bcnt / v_writelane
+// with an SGPR operand).  gfx950 needs 2 wait states between a VALU write of
+// an SGPR/VCC and a VALU read of it; the compiler inserts them for its own
+// instructions (s_nop 1 after v_cmp) but cannot see the read inside an asm
+// statement.  The dependent s_nop below supplies them: every consumer of the
+// returned mask is ordered after it.
+__device__ __forceinline__ uint64_t ballot_s(bool p) {
+  uint64_t b = __ballot(p);
+  asm volatile("s_nop 1" : "+s"(b));
+  return b;
+}
 
 
 // Coins of the tied receivers of one group (node.ts:111).  The key words are
@@ -131,33 +143,54 @@ __device__ __forceinline__ uint32_t tally_first(uint32_t word) {
   return r;
 }
 
+
+
+// R-phase tally of one receiver group set: c1 only.  A receiver's R-phase
+// trigger fires with exactly m messages in its inbox (node.ts:52, len >= N-F,
+// m = N-F live senders in lockstep); each is 0, 1 or "?", so
+// c0 = m - c1 - c? (node.ts:56-62) and c? is 0 in every round but the first
+// of a fixed-init run with "?" initial values (a plan constant there).  The x
+// planes therefore carry only the is1 word: 2 dwords per group, read as
+// 16-byte pairs of groups.
 template <int W>
-__device__ __forceinline__ void tally_plane(const uint4 *__restrict__ plane, uint32_t (&a0)[W],
-                                            uint32_t (&a1)[W]) {
-  const uint4 q = plane[0];
-  Unroll<W>::run([&](auto gi) {
-    constexpr int g = decltype(gi)::value;
-    a0[g] = tally_first<g>(q.x);
-    a1[g] = tally_first<g>(q.z);
-  });
+__device__ __forceinline__ void tally_x1(const uint2 *__restrict__ plane, uint32_t (&a1)[W]) {
+  const uint4 *q4 = reinterpret_cast<const uint4 *>(plane);
+  {
+    const uint4 q = q4[0];
+    Unroll<W>::run([&](auto gi) {
+      constexpr int g = decltype(gi)::value;
+      a1[g] = tally_first<g>(q.x);
+    });
 #pragma unroll
-  for (int g = 0; g < W; ++g) {
-    a0[g] = tally(q.y, a0[g]);
-    a1[g] = tally(q.w, a1[g]);
+    for (int g = 0; g < W; ++g) a1[g] = tally(q.y, a1[g]);
+    if constexpr (W > 1) {
+#pragma unroll
+      for (int g = 0; g < W; ++g) {
+        a1[g] = tally(q.z, a1[g]);
+        a1[g] = tally(q.w, a1[g]);
+      }
+    }
   }
 #pragma unroll
-  for (int w = 1; w < W; ++w) {
-    const uint4 s = plane[w];
+  for (int w = 1; w < W / 2; ++w) {
+    const uint4 s = q4[w];
 #pragma unroll
     for (int g = 0; g < W; ++g) {
-      a0[g] = tally(s.x, a0[g]);
+      a1[g] = tally(s.x, a1[g]);
+      a1[g] = tally(s.y, a1[g]);
       a1[g] = tally(s.z, a1[g]);
-      a0[g] = tally(s.y, a0[g]);
       a1[g] = tally(s.w, a1[g]);
     }
   }
+  if constexpr (W > 1 && (W & 1)) {
+    const uint2 s = plane[W - 1];
+#pragma unroll
+    for (int g = 0; g < W; ++g) {
+      a1[g] = tally(s.x, a1[g]);
+      a1[g] = tally(s.y, a1[g]);
+    }
+  }
 }
-
 
 // Proposal planes can stay in SGPRs for the few hundred cycles between the
 // R-phase ballots that produce them and the P-phase tallies that read them:
@@ -180,36 +213,6 @@ __device__ __forceinline__ uint32_t sgpr32(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
 }
 
-template <int W>
-__device__ __forceinline__ void tally_sgpr(const uint64_t (&is0)[W], const uint64_t (&is1)[W], uint32_t (&a0)[W],
-                                           uint32_t (&a1)[W]) {
-  {
-    const uint32_t w0 = sgpr32((uint32_t)is0[0]), w1 = sgpr32((uint32_t)is1[0]);
-    Unroll<W>::run([&](auto gi) {
-      constexpr int g = decltype(gi)::value;
-      a0[g] = tally_first_s<g>(w0);
-      a1[g] = tally_first_s<g>(w1);
-    });
-    const uint32_t h0 = sgpr32((uint32_t)(is0[0] >> 32)), h1 = sgpr32((uint32_t)(is1[0] >> 32));
-#pragma unroll
-    for (int g = 0; g < W; ++g) {
-      a0[g] = tally_s(h0, a0[g]);
-      a1[g] = tally_s(h1, a1[g]);
-    }
-  }
-#pragma unroll
-  for (int w = 1; w < W; ++w) {
-    const uint32_t l0 = sgpr32((uint32_t)is0[w]), l1 = sgpr32((uint32_t)is1[w]);
-    const uint32_t h0 = sgpr32((uint32_t)(is0[w] >> 32)), h1 = sgpr32((uint32_t)(is1[w] >> 32));
-#pragma unroll
-    for (int g = 0; g < W; ++g) {
-      a0[g] = tally_s(l0, a0[g]);
-      a1[g] = tally_s(l1, a1[g]);
-      a0[g] = tally_s(h0, a0[g]);
-      a1[g] = tally_s(h1, a1[g]);
-    }
-  }
-}
 
 template <int L>
 __device__ __forceinline__ uint32_t writelane(uint32_t v, uint32_t val) {
@@ -231,137 +234,186 @@ template <int W>
 __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
   constexpr int NPH = (W + 1) / 2;          // Philox blocks per trial (2 plane words each)
   constexpr int TB = 64 / NPH;              // trials per init batch
+  constexpr int WP = 2 * NPH;               // x1 words per plane row, padded to 16 bytes
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wv = threadIdx.x >> 6;
-  const uint32_t m = p.m, F = p.F;
+  // Kernel arguments are copied to locals once: nothing below (lambdas
+  // included) refers to `p`, so the struct is never materialised in SGPRs.
+  const uint32_t m = p.m, F = p.F, k_max = p.k_max, hist_len = p.hist_len;
+  const uint64_t trial_begin = p.trial_begin, trial_count = p.trial_count;
+  const uint32_t *__restrict__ live_ids = p.live_ids;
+  bo_node_state *node_out = p.node_out;
+  uint32_t *rounds_out = p.rounds_out;
 
   uint32_t *lhist = reinterpret_cast<uint32_t *>(smem);
-  uint4 *ring = reinterpret_cast<uint4 *>(smem + p.hist_bytes + wv * p.wave_bytes);   // [TB][W]
-  uint4 *X = ring + TB * W;                                                              // [W]
+  uint2 *ring = reinterpret_cast<uint2 *>(smem + p.hist_bytes + wv * p.wave_bytes);   // [TB][WP] x1 words
+  uint2 *X = ring + TB * WP;                                                            // [WP]
 
-  for (uint32_t i = threadIdx.x; i < p.hist_len; i += blockDim.x) lhist[i] = 0u;
-  if (p.init_mode != BO_INIT_RANDOM && lane < (uint32_t)W) ring[lane] = p.init_plane[lane];
+  for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) lhist[i] = 0u;
+  if (p.init_mode != BO_INIT_RANDOM && lane < (uint32_t)W) {
+    const uint4 q = p.init_plane[lane];
+    ring[lane] = make_uint2(q.z, q.w);
+  }
   __syncthreads();
 
   const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
   const uint64_t waves_total = (uint64_t)gridDim.x * kWavesPerBlock;
   const uint64_t tailm = group_mask(W - 1, m);
   const bool random_init = p.init_mode == BO_INIT_RANDOM;
+  const uint32_t m_first = m - p.init_q;      // binary-valued senders in round 1 ("?" excluded)
 
-  for (uint64_t base = (uint64_t)blockIdx.x * kWavesPerBlock + wv; base < p.trial_count;
+  for (uint64_t base = (uint64_t)blockIdx.x * kWavesPerBlock + wv; base < trial_count;
        base += waves_total * TB) {
     // ---- /start (node.ts:167-188): round-1 x planes of TB trials at once.
     if (random_init) {
       const uint32_t s = lane / NPH, b = lane - s * NPH;
       const uint64_t t = base + (uint64_t)s * waves_total;
-      if (s < (uint32_t)TB && t < p.trial_count) {
-        const uint64_t trial = p.trial_begin + t;
+      if (s < (uint32_t)TB && t < trial_count) {
+        const uint64_t trial = trial_begin + t;
         uint32_t kk0 = k0, kk1 = k1;
         asm volatile("" : "+s"(kk0), "+s"(kk1));   // keep the round keys out of long-lived SGPRs
         const uint4 r = philox4x32_10(kk0, kk1, make_uint4((uint32_t)trial, (uint32_t)(trial >> 32), b, kStreamInit << 24));
-        const uint32_t w0 = 2u * b, w1 = w0 + 1u;
-        const uint64_t v0 = group_mask(w0, m), v1 = group_mask(w1, m);
-        const uint64_t x1a = ((uint64_t)r.y << 32 | r.x) & v0;
-        ring[s * W + w0] = rec(v0 & ~x1a, x1a);
-        if (w1 < (uint32_t)W) {
-          const uint64_t x1b = ((uint64_t)r.w << 32 | r.z) & v1;
-          ring[s * W + w1] = rec(v1 & ~x1b, x1b);
-        }
+        const uint64_t v0 = group_mask(2u * b, m), v1 = group_mask(2u * b + 1u, m);
+        const uint64_t x1a = ((uint64_t)r.y << 32 | r.x) & v0, x1b = ((uint64_t)r.w << 32 | r.z) & v1;
+        reinterpret_cast<uint4 *>(ring + s * WP)[b] =
+            make_uint4((uint32_t)x1a, (uint32_t)(x1a >> 32), (uint32_t)x1b, (uint32_t)(x1b >> 32));
       }
     }
     for (int s = 0; s < TB; ++s) {
       const uint64_t t = base + (uint64_t)s * waves_total;
-      if (t >= p.trial_count) break;
-      const uint64_t trial = p.trial_begin + t;
+      if (t >= trial_count) break;
+      const uint64_t trial = trial_begin + t;
       const uint32_t tlo = (uint32_t)trial, thi = (uint32_t)(trial >> 32);
-      const uint4 *Xr = random_init ? ring + s * W : ring;
+      const uint2 *Xr = random_init ? ring + s * WP : ring;
       uint64_t dec[W];
+      uint64_t any0 = 0, any1 = 0;            // final round's x: some live node 0 / some 1
 #pragma unroll
       for (int g = 0; g < W; ++g) dec[g] = 0ull;
-      uint32_t R = 0;
+      uint32_t R = 0, M = m_first;
       bool all_dec = false;
-      for (uint32_t r = 1; r <= p.k_max; ++r) {
+      for (uint32_t r = 1;; ++r) {
+        // ---- R-phase ("proposal phase", node.ts:46-82): c1 per receiver, c0 = M - c1
+        uint32_t c1r[W];
+        tally_x1<W>(Xr, c1r);
+        const uint32_t hi_t = M >> 1, lo_t = (M + 1u) >> 1;
+        // ---- P-phase ("voting phase", node.ts:83-158) tallies, fused with the R-phase
+        // ballots: sender group w's proposals (two SGPR pairs) are added to every
+        // receiver group's P-phase counts as soon as they exist, so only one
+        // group's proposal planes is ever live.
         uint32_t a0[W], a1[W];
-        // ---- R-phase ("proposal phase", node.ts:46-82)
-        tally_plane<W>(Xr, a0, a1);
-#if BENOR_P_SGPR
-        uint64_t p0s[W], p1s[W];
+#if BENOR_FUSED
+        Unroll<W>::run([&](auto wi) {
+          constexpr int w = decltype(wi)::value;
+          const uint64_t vm = (w == W - 1) ? tailm : ~0ull;
+          const uint64_t p1 = ballot_s(c1r[w] > hi_t + (uint32_t)w) & vm;   // c1 > c0  (node.ts:65-66)
+          const uint64_t p0 = ballot_s(c1r[w] < lo_t + (uint32_t)w) & vm;   // c0 > c1  (node.ts:63-64); else "?"
+          const uint32_t l0 = sgpr32((uint32_t)p0), h0 = sgpr32((uint32_t)(p0 >> 32));
+          const uint32_t l1 = sgpr32((uint32_t)p1), h1 = sgpr32((uint32_t)(p1 >> 32));
+          if constexpr (w == 0) {
+            Unroll<W>::run([&](auto gi) {
+              constexpr int g = decltype(gi)::value;
+              a0[g] = tally_first_s<g>(l0);
+              a1[g] = tally_first_s<g>(l1);
+            });
+          } else {
 #pragma unroll
-        for (int g = 0; g < W; ++g) {
-          const uint64_t vm = (g == W - 1) ? tailm : ~0ull;
-          p0s[g] = ballot(a0[g] > a1[g]) & vm;   // node.ts:63-64
-          p1s[g] = ballot(a1[g] > a0[g]) & vm;   // node.ts:65-66 (else "?")
-        }
-        uint32_t st = 0;
-        // ---- P-phase ("voting phase", node.ts:83-158)
-        tally_sgpr<W>(p0s, p1s, a0, a1);
+            for (int g = 0; g < W; ++g) {
+              a0[g] = tally_s(l0, a0[g]);
+              a1[g] = tally_s(l1, a1[g]);
+            }
+          }
+#pragma unroll
+          for (int g = 0; g < W; ++g) {
+            a0[g] = tally_s(h0, a0[g]);
+            a1[g] = tally_s(h1, a1[g]);
+          }
+        });
 #else
-        uint32_t st = 0;
+        uint64_t p0s[W], p1s[W];
         Unroll<W>::run([&](auto gi) {
           constexpr int g = decltype(gi)::value;
           const uint64_t vm = (g == W - 1) ? tailm : ~0ull;
-          const uint64_t p0 = ballot(a0[g] > a1[g]) & vm;   // node.ts:63-64
-          const uint64_t p1 = ballot(a1[g] > a0[g]) & vm;   // node.ts:65-66 (else "?")
-          st = stage4<g>(st, p0, p1);
+          p1s[g] = ballot_s(c1r[g] > hi_t + (uint32_t)g) & vm;
+          p0s[g] = ballot_s(c1r[g] < lo_t + (uint32_t)g) & vm;
         });
-        if (lane < 4u * W) reinterpret_cast<uint32_t *>(P)[lane] = st;
-        // ---- P-phase ("voting phase", node.ts:83-158)
-        tally_plane<W>(P, a0, a1);
+        Unroll<W>::run([&](auto wi) {
+          constexpr int w = decltype(wi)::value;
+          const uint32_t l0 = sgpr32((uint32_t)p0s[w]), h0 = sgpr32((uint32_t)(p0s[w] >> 32));
+          const uint32_t l1 = sgpr32((uint32_t)p1s[w]), h1 = sgpr32((uint32_t)(p1s[w] >> 32));
+          if constexpr (w == 0) {
+            Unroll<W>::run([&](auto gi) {
+              constexpr int g = decltype(gi)::value;
+              a0[g] = tally_first_s<g>(l0);
+              a1[g] = tally_first_s<g>(l1);
+            });
+          } else {
+#pragma unroll
+            for (int g = 0; g < W; ++g) {
+              a0[g] = tally_s(l0, a0[g]);
+              a1[g] = tally_s(l1, a1[g]);
+            }
+          }
+#pragma unroll
+          for (int g = 0; g < W; ++g) {
+            a0[g] = tally_s(h0, a0[g]);
+            a1[g] = tally_s(h1, a1[g]);
+          }
+        });
 #endif
         bool done = true;
+        uint32_t st = 0;
+        any0 = 0;
+        any1 = 0;
         Unroll<W>::run([&](auto gi) {
           constexpr int g = decltype(gi)::value;
           const uint64_t vm = (g == W - 1) ? tailm : ~0ull;
           const uint32_t Fg = F + (uint32_t)g;                        // chain bias g
-          const uint64_t d0 = ballot(a0[g] > Fg) & vm;                 // node.ts:99
-          const uint64_t d1 = ballot(a1[g] > Fg) & vm & ~d0;           // node.ts:102
+          const uint64_t d0 = ballot_s(a0[g] > Fg) & vm;                 // node.ts:99
+          const uint64_t d1 = ballot_s(a1[g] > Fg) & vm & ~d0;           // node.ts:102
           const uint64_t rest = vm & ~(d0 | d1);
           uint64_t x1 = d1;
           if (rest) {                                                   // some receiver did not decide
-            const uint64_t ad1 = ballot(a1[g] > a0[g]) & rest;         // node.ts:108-109
-            const uint64_t tie = ballot(a1[g] == a0[g]) & rest;        // node.ts:110-111
+            const uint64_t ad1 = ballot_s(a1[g] > a0[g]) & rest;         // node.ts:108-109
+            const uint64_t tie = ballot_s(a1[g] == a0[g]) & rest;        // node.ts:110-111
             x1 |= ad1;
-            if (tie) x1 |= (coin_ballot(k0, k1, tlo, thi, p.live_ids, g, r, tie));   // node.ts:111
+            if (tie) x1 |= (coin_ballot(k0, k1, tlo, thi, live_ids, g, r, tie));   // node.ts:111
           }
-          st = stage4<g>(st, vm & ~x1, x1);
+          // next round's x plane: only the is1 word (every x is 0 or 1 from here on)
+          st = writelane<2 * g>(st, (uint32_t)x1);
+          st = writelane<2 * g + 1>(st, (uint32_t)(x1 >> 32));
+          any1 |= x1;
+          any0 |= vm & ~x1;
           dec[g] |= d0 | d1;
           done = done && (dec[g] == vm);
         });
-        if (lane < 4u * W) reinterpret_cast<uint32_t *>(X)[lane] = st;
+        if (lane < 2u * W) reinterpret_cast<uint32_t *>(X)[lane] = st;
         Xr = X;
+        M = m;
         R = r;                                                        // node.ts:147  k = r + 1
         all_dec = done;                                               // all-decided auto-stop
-        if (all_dec) break;
+        if (all_dec || r >= k_max) break;
       }
       // ---- outcome
-      bool any0 = false, any1 = false;
-      if (lane < (uint32_t)W) {
-        const uint4 q = Xr[lane];
-        any0 = (q.x | q.y) != 0u;
-        any1 = (q.z | q.w) != 0u;
-      }
-      const bool g0 = __any(any0), g1 = __any(any1);
-      const uint32_t v = (g0 && g1) ? 2u : (g1 ? 1u : 0u);
+      const uint32_t v = (any0 && any1) ? 2u : (any1 ? 1u : 0u);
       if (lane == 0) {
         atomicAdd(&lhist[all_dec ? (R * 3u + v) : v], 1u);
-        if (all_dec && v == 2u) atomicAdd(&lhist[p.hist_len - 1u], 1u);
-        if (p.rounds_out) *p.rounds_out = all_dec ? R : 0u;
+        if (all_dec && v == 2u) atomicAdd(&lhist[hist_len - 1u], 1u);
+        if (rounds_out) *rounds_out = all_dec ? R : 0u;
       }
-      if (p.node_out) {                                               // GET /getState (node.ts:197-199)
+      if (node_out) {                                               // GET /getState (node.ts:197-199)
         Unroll<W>::run([&](auto gi) {
           constexpr int g = decltype(gi)::value;
           const uint32_t c = g * 64u + lane;
           if (c < m) {
-            const uint4 q = Xr[g];
-            const uint64_t x1 = (uint64_t)q.w << 32 | q.z;
+            const uint2 q = Xr[g];
             bo_node_state ns;
             ns.killed = 0;
-            ns.x = (int8_t)((x1 >> lane) & 1ull);
+            ns.x = (int8_t)(((lane < 32u ? q.x : q.y) >> (lane & 31u)) & 1u);
             ns.decided = (int8_t)((dec[g] >> lane) & 1ull);
             ns.pad = 0;
             ns.k = (int32_t)R + 1;
-            p.node_out[p.live_ids[c]] = ns;
+            node_out[live_ids[c]] = ns;
           }
         });
       }
@@ -369,7 +421,7 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
   }
 
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < p.hist_len; i += blockDim.x) {
+  for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) {
     const uint32_t c = lhist[i];
     if (c) atomicAdd(&p.hist[i], (unsigned long long)c);
   }
@@ -426,29 +478,64 @@ __device__ __forceinline__ void tally_groups(const uint4 *__restrict__ plane, ui
   }
 }
 
+// R-phase x1-only tally over the W words of a plane (runtime W, pairs of
+// groups per 16-byte read; WP = W rounded up to even, padding words zero).
+template <int G>
+__device__ __forceinline__ void tally_groups_x1(const uint2 *__restrict__ plane, uint32_t W, uint32_t (&a1)[G]) {
+  const uint4 *q4 = reinterpret_cast<const uint4 *>(plane);
+  const uint4 q = q4[0];
+  Unroll<G>::run([&](auto gi) {
+    constexpr int g = decltype(gi)::value;
+    a1[g] = tally_first<g>(q.x);
+  });
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    a1[g] = tally(q.y, a1[g]);
+    a1[g] = tally(q.z, a1[g]);
+    a1[g] = tally(q.w, a1[g]);
+  }
+  const uint32_t np = (W + 1u) >> 1;
+  for (uint32_t w = 1; w < np; ++w) {
+    const uint4 s = q4[w];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      a1[g] = tally(s.x, a1[g]);
+      a1[g] = tally(s.y, a1[g]);
+      a1[g] = tally(s.z, a1[g]);
+      a1[g] = tally(s.w, a1[g]);
+    }
+  }
+}
+
 template <int G>
 __global__ void __launch_bounds__(256) benor_lockstep_blocked_kernel(KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wv = threadIdx.x >> 6;
   const uint32_t m = p.m, F = p.F, W = p.W, NB = p.nblocks;
-  const uint32_t nph = (W + 1u) >> 1, tb = 64u / nph;
+  const uint32_t nph = (W + 1u) >> 1, tb = 64u / nph, WP = 2u * nph;
+  const uint32_t XW = ((NB * G > WP ? NB * G : WP) + 1u) & ~1u;   // x1 words of the staged plane (even, padding zero)
   const uint32_t tail_n = m - (W - 1u) * 64u;          // live receivers in the last group
 
   uint32_t *lhist = reinterpret_cast<uint32_t *>(smem);
-  uint4 *ring = reinterpret_cast<uint4 *>(smem + p.hist_bytes + wv * p.wave_bytes);   // [tb][W]
-  uint4 *X = ring + tb * W;                                                              // [NB*G]
-  uint4 *P = X + NB * G;                                                                 // [NB*G]
+  uint2 *ring = reinterpret_cast<uint2 *>(smem + p.hist_bytes + wv * p.wave_bytes);   // [tb][WP] x1 words
+  uint2 *X = ring + tb * WP;                                                            // [XW]
+  uint4 *P = reinterpret_cast<uint4 *>(X + XW);                                        // [NB*G]
   uint32_t *D = reinterpret_cast<uint32_t *>(P + NB * G);                               // [NB][64] decided bits
 
   for (uint32_t i = threadIdx.x; i < p.hist_len; i += blockDim.x) lhist[i] = 0u;
   if (p.init_mode != BO_INIT_RANDOM)
-    for (uint32_t w = lane; w < W; w += 64u) ring[w] = p.init_plane[w];
+    for (uint32_t w = lane; w < WP; w += 64u) {
+      const uint4 q = w < W ? p.init_plane[w] : make_uint4(0, 0, 0, 0);
+      ring[w] = make_uint2(q.z, q.w);
+    }
+  for (uint32_t w = lane; w < XW; w += 64u) X[w] = make_uint2(0u, 0u);
   __syncthreads();
 
   const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
   const uint64_t waves_total = (uint64_t)gridDim.x * kWavesPerBlock;
   const bool random_init = p.init_mode == BO_INIT_RANDOM;
+  const uint32_t m_first = m - p.init_q;
 
   for (uint64_t base = (uint64_t)blockIdx.x * kWavesPerBlock + wv; base < p.trial_count;
        base += waves_total * tb) {
@@ -460,14 +547,10 @@ __global__ void __launch_bounds__(256) benor_lockstep_blocked_kernel(KParams p) 
         uint32_t kk0 = k0, kk1 = k1;
         asm volatile("" : "+s"(kk0), "+s"(kk1));   // keep the round keys out of long-lived SGPRs
         const uint4 r = philox4x32_10(kk0, kk1, make_uint4((uint32_t)trial, (uint32_t)(trial >> 32), bk, kStreamInit << 24));
-        const uint32_t w0 = 2u * bk, w1 = w0 + 1u;
-        const uint64_t v0 = group_mask(w0, m), v1 = group_mask(w1, m);
-        const uint64_t x1a = ((uint64_t)r.y << 32 | r.x) & v0;
-        ring[s * W + w0] = rec(v0 & ~x1a, x1a);
-        if (w1 < W) {
-          const uint64_t x1b = ((uint64_t)r.w << 32 | r.z) & v1;
-          ring[s * W + w1] = rec(v1 & ~x1b, x1b);
-        }
+        const uint64_t v0 = group_mask(2u * bk, m), v1 = group_mask(2u * bk + 1u, m);
+        const uint64_t x1a = ((uint64_t)r.y << 32 | r.x) & v0, x1b = ((uint64_t)r.w << 32 | r.z) & v1;
+        reinterpret_cast<uint4 *>(ring + s * WP)[bk] =
+            make_uint4((uint32_t)x1a, (uint32_t)(x1a >> 32), (uint32_t)x1b, (uint32_t)(x1b >> 32));
       }
     }
     for (uint32_t s = 0; s < tb; ++s) {
@@ -475,22 +558,23 @@ __global__ void __launch_bounds__(256) benor_lockstep_blocked_kernel(KParams p) 
       if (t >= p.trial_count) break;
       const uint64_t trial = p.trial_begin + t;
       const uint32_t tlo = (uint32_t)trial, thi = (uint32_t)(trial >> 32);
-      const uint4 *Xr = random_init ? ring + s * W : ring;
+      const uint2 *Xr = random_init ? ring + s * WP : ring;
       for (uint32_t b = 0; b < NB; ++b) D[b * 64u + lane] = 0u;
-      uint32_t R = 0;
+      uint32_t R = 0, M = m_first;
       bool all_dec = false;
       for (uint32_t r = 1; r <= p.k_max; ++r) {
-        // ---- R-phase ("proposal phase", node.ts:46-82)
+        // ---- R-phase ("proposal phase", node.ts:46-82): c1 per receiver, c0 = M - c1
+        const uint32_t hi_t = M >> 1, lo_t = (M + 1u) >> 1;
 #pragma nounroll
         for (uint32_t b = 0; b < NB; ++b) {
-          uint32_t a0[G], a1[G];
-          tally_groups<G>(Xr, W, a0, a1);
+          uint32_t a1[G];
+          tally_groups_x1<G>(Xr, W, a1);
           uint32_t st = 0;
           Unroll<G>::run([&](auto gi) {
             constexpr int g = decltype(gi)::value;
             const uint64_t vm = group_mask(b * G + g, m);
-            const uint64_t p0 = ballot(a0[g] > a1[g]) & vm;   // node.ts:63-64
-            const uint64_t p1 = ballot(a1[g] > a0[g]) & vm;   // node.ts:65-66 (else "?")
+            const uint64_t p0 = ballot_s(a1[g] < lo_t + (uint32_t)g) & vm;   // node.ts:63-64
+            const uint64_t p1 = ballot_s(a1[g] > hi_t + (uint32_t)g) & vm;   // node.ts:65-66 (else "?")
             st = stage4<g>(st, p0, p1);
           });
           if (lane < 4u * G) reinterpret_cast<uint32_t *>(P + b * G)[lane] = st;
@@ -507,21 +591,22 @@ __global__ void __launch_bounds__(256) benor_lockstep_blocked_kernel(KParams p) 
             const uint64_t vm = group_mask(b * G + g, m);
             const uint32_t Fg = F + (uint32_t)g;
             const bool d0l = a0[g] > Fg, d1l = a1[g] > Fg;           // node.ts:99, :102
-            const uint64_t d0 = ballot(d0l) & vm;
-            const uint64_t d1 = ballot(d1l) & vm & ~d0;
+            const uint64_t d0 = ballot_s(d0l) & vm;
+            const uint64_t d1 = ballot_s(d1l) & vm & ~d0;
             const uint64_t rest = vm & ~(d0 | d1);
             uint64_t x1 = d1;
             if (rest) {
-              const uint64_t ad1 = ballot(a1[g] > a0[g]) & rest;     // node.ts:108-109
-              const uint64_t tie = ballot(a1[g] == a0[g]) & rest;    // node.ts:110-111
+              const uint64_t ad1 = ballot_s(a1[g] > a0[g]) & rest;     // node.ts:108-109
+              const uint64_t tie = ballot_s(a1[g] == a0[g]) & rest;    // node.ts:110-111
               x1 |= ad1;
               if (tie) x1 |= (coin_ballot(k0, k1, tlo, thi, p.live_ids, b * G + g, r, tie));   // node.ts:111
             }
-            st = stage4<g>(st, vm & ~x1, x1);
+            st = writelane<2 * g>(st, (uint32_t)x1);
+            st = writelane<2 * g + 1>(st, (uint32_t)(x1 >> 32));
             dbb = (d0l || d1l) ? (dbb | (1u << g)) : dbb;
           });
           D[b * 64u + lane] = dbb;
-          if (lane < 4u * G) reinterpret_cast<uint32_t *>(X + b * G)[lane] = st;
+          if (lane < 2u * G) reinterpret_cast<uint32_t *>(X + b * G)[lane] = st;
           // groups of this block that hold live receivers for this lane
           const uint32_t j0 = b * G;
           uint32_t expect = 0u;
@@ -533,6 +618,7 @@ __global__ void __launch_bounds__(256) benor_lockstep_blocked_kernel(KParams p) 
           done = done && __all((dbb & expect) == expect);
         }
         Xr = X;
+        M = m;
         R = r;
         all_dec = done;
         if (all_dec) break;
@@ -540,9 +626,10 @@ __global__ void __launch_bounds__(256) benor_lockstep_blocked_kernel(KParams p) 
       // ---- outcome
       bool any0 = false, any1 = false;
       if (lane < W) {
-        const uint4 q = Xr[lane];
-        any0 = (q.x | q.y) != 0u;
-        any1 = (q.z | q.w) != 0u;
+        const uint2 q = Xr[lane];
+        const uint64_t x1 = (uint64_t)q.y << 32 | q.x;
+        any1 = x1 != 0ull;
+        any0 = (group_mask(lane, m) & ~x1) != 0ull;
       }
       const bool g0 = __any(any0), g1 = __any(any1);
       const uint32_t v = (g0 && g1) ? 2u : (g1 ? 1u : 0u);
@@ -554,8 +641,8 @@ __global__ void __launch_bounds__(256) benor_lockstep_blocked_kernel(KParams p) 
       if (p.node_out) {
         for (uint32_t c = lane; c < m; c += 64u) {
           const uint32_t j = c >> 6;
-          const uint4 q = Xr[j];
-          const uint64_t x1 = (uint64_t)q.w << 32 | q.z;
+          const uint2 q = Xr[j];
+          const uint64_t x1 = (uint64_t)q.y << 32 | q.x;
           bo_node_state ns;
           ns.killed = 0;
           ns.x = (int8_t)((x1 >> lane) & 1ull);
@@ -666,9 +753,11 @@ __global__ void __launch_bounds__(256) benor_packed_kernel(KParams p) {
     }
     if (!__any(act)) break;
 
-    // ---- R-phase ("proposal phase", node.ts:46-82)
-    const uint64_t is0 = ballot(act && x == 0u), is1 = ballot(act && x == 1u);
-    const uint32_t c0 = seg_tally(is0, half_shift, segmask), c1 = seg_tally(is1, half_shift, segmask);
+    // ---- R-phase ("proposal phase", node.ts:46-82): c1 per receiver, c0 = M - c1
+    //      (M = m binary-valued senders; minus the "?" ones in round 1 of a fixed init)
+    const uint64_t is1 = ballot(act && x == 1u);
+    const uint32_t c1 = seg_tally(is1, half_shift, segmask);
+    const uint32_t c0 = (r == 0u ? m - p.init_q : m) - c1;
     // ---- P-phase ("voting phase", node.ts:83-158)
     const uint64_t p0 = ballot(act && c0 > c1), p1 = ballot(act && c1 > c0);   // node.ts:63-69 (else "?")
     const uint32_t v0 = seg_tally(p0, half_shift, segmask), v1 = seg_tally(p1, half_shift, segmask);
@@ -1183,18 +1272,20 @@ void plan_geometry(KParams &p) {
     return;
   }
   const uint32_t nph = (W + 1u) / 2u, tb = 64u / nph;   // init ring: tb trials per Philox pass
+  const uint32_t WP = 2u * nph;                         // x1 words per plane row (even)
   if (W <= (uint32_t)kMaxWSpecialised) {
     p.G = W;
     p.nblocks = 1;
     p.variant = 1;
-    p.wave_bytes = (tb * W + W) * 16u;
+    p.wave_bytes = (tb * WP + WP) * 8u;                 // init ring + staged x1 plane
   } else {
     const uint32_t nb = (W + 15u) / 16u;           // blocks of at most 16 groups
     const uint32_t G = (W + nb - 1u) / nb;         // balanced: padding < nb groups
+    const uint32_t XW = ((G * nb > WP ? G * nb : WP) + 1u) & ~1u;
     p.G = G;
     p.nblocks = nb;
     p.variant = 0;
-    p.wave_bytes = (tb * W + 2u * G * nb) * 16u + nb * 256u;
+    p.wave_bytes = (tb * WP + XW) * 8u + G * nb * 16u + nb * 256u;   // ring, x1 plane, {p0,p1} plane, decided bits
   }
   p.lds_bytes = p.hist_bytes + kWavesPerBlock * p.wave_bytes;
 }

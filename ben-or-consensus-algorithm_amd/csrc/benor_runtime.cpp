@@ -251,6 +251,7 @@ int bo_plan_create(const bo_trials_cfg *cfg, bo_plan **out) {
         uint32_t *r = reinterpret_cast<uint32_t *>(&plane[w]);
         if (v == 0) r[b >> 5] |= 1u << (b & 31u);
         if (v == 1) r[2 + (b >> 5)] |= 1u << (b & 31u);
+        if (v == 2) ++kp.init_q;
       }
     }
     hipError_t e = hipMalloc(&pl->d_live, sizeof(uint32_t) * m);
@@ -305,9 +306,13 @@ void bo_plan_destroy(bo_plan *pl) {
 
 uint32_t bo_plan_live_nodes(const bo_plan *pl) { return pl ? pl->kp.m : 0u; }
 
+// Lockstep: the R-phase needs c1 only (c0 = m - c1 - c?, node.ts:52,56-62),
+// the P-phase c0 and c1 (node.ts:92-98): 3 counts of ceil(m/32) words.
+// Random delivery counts both in both phases: 4.
 uint64_t bo_plan_popc_words_per_node_round(const bo_plan *pl) {
   if (!pl) return 0;
-  return 4ull * ((pl->kp.m + 31ull) / 32ull);
+  const uint64_t counts = pl->kp.mode == BO_MODE_RANDOM_DELIVERY ? 4ull : 3ull;
+  return counts * ((pl->kp.m + 31ull) / 32ull);
 }
 
 static int plan_launch_impl(bo_plan *pl, uint64_t trial_begin, uint64_t trial_count, uint64_t *hist_dev,

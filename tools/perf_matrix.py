@@ -2,7 +2,8 @@
 
 For each (N, F, f, mode) -- mode 0 lockstep, 1 random delivery, 2 event level -- runs `trials` trials once for warm-up and once timed
 with HIP events on the launch stream, and prints live node-rounds/s and the
-popcount-roofline fraction (4*ceil(m/32) words per live node-round vs the
+popcount-roofline fraction (the plan's algorithmic popcount words per live
+node-round -- 3*ceil(m/32) lockstep, 4*ceil(m/32) random delivery -- vs the
 v_bcnt issue peak, 39.3 T/s).  One JSON line per shape.
 
     python tools/perf_matrix.py [--quick]
@@ -59,7 +60,7 @@ def main():
         rounds = sum(r * int(hist[r * 3] + hist[r * 3 + 1] + hist[r * 3 + 2]) for r in range(1, k + 1))
         rounds += k * int(hist[0] + hist[1] + hist[2])
         nr = rounds * m
-        words = 4 * ((m + 31) // 32)
+        words = plan.popc_words_per_node_round
         rate = nr / (ms * 1e-3)
         print(json.dumps({"N": N, "F": F, "f": f, "mode": ["lockstep", "random", "event"][mode], "trials": trials,
                           "mean_rounds": rounds / trials, "ms": round(ms, 3), "node_rounds_per_s": rate,
