@@ -106,6 +106,23 @@ __device__ __forceinline__ uint64_t coin_ballot(uint32_t k0, uint32_t k1, uint32
   return ballot(c1) & tie;
 }
 
+// Philox key words re-read from LDS at the point of use.  The volatile load
+// cannot be hoisted, so the key schedule of a rare path (coins, the per-batch
+// init pass) is rebuilt there instead of being kept -- i.e. spilled -- in SGPRs
+// across the whole round loop.
+__device__ __forceinline__ uint2 lds_keys(const uint32_t *keys) {
+  const volatile uint32_t *k = keys;
+  return make_uint2((uint32_t)__builtin_amdgcn_readfirstlane((int)k[0]),
+                    (uint32_t)__builtin_amdgcn_readfirstlane((int)k[1]));
+}
+
+__device__ __forceinline__ uint64_t coin_ballot(const uint32_t *keys, uint32_t tlo, uint32_t thi,
+                                             const uint32_t *__restrict__ live_ids, uint32_t group,
+                                             uint32_t round, uint64_t tie) {
+  const uint2 k = lds_keys(keys);
+  return coin_ballot(k.x, k.y, tlo, thi, live_ids, group, round, tie);
+}
+
 // A call's result comes back in VGPRs; the ballot is wave-uniform, so move it
 // to SGPRs for the mask arithmetic that follows.
 __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
@@ -213,6 +230,23 @@ __device__ __forceinline__ uint32_t sgpr32(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
 }
 
+// Opaque wave compares (v_cmp -> SGPR lane mask).  asm volatile so that the
+// compiler neither merges the decision pass's compares with the adopt pass's
+// recomputation of them (which would keep 2W masks live across the pass and
+// spill SGPRs) nor speculates them out of their branches.  The trailing
+// s_nop 1 supplies the 2 wait states gfx950 needs between a VALU SGPR write
+// and a VALU read of it inside a later asm (v_bcnt with an SGPR operand).
+__device__ __forceinline__ uint64_t vcmp_gt(uint32_t v, uint32_t s) {   // lanes with v > s
+  uint64_t r;
+  asm volatile("v_cmp_gt_u32_e64 %0, %1, %2\n\ts_nop 1" : "=s"(r) : "v"(v), "s"(s));
+  return r;
+}
+__device__ __forceinline__ uint64_t vcmp_lt(uint32_t v, uint32_t s) {   // lanes with v < s
+  uint64_t r;
+  asm volatile("v_cmp_lt_u32_e64 %0, %1, %2\n\ts_nop 1" : "=s"(r) : "v"(v), "s"(s));
+  return r;
+}
+
 
 template <int L>
 __device__ __forceinline__ uint32_t writelane(uint32_t v, uint32_t val) {
@@ -230,6 +264,43 @@ __device__ __forceinline__ uint32_t stage4(uint32_t v, uint64_t is0, uint64_t is
   return v;
 }
 
+// One round's R-phase proposals (node.ts:63-69, from each receiver's c1 and the
+// vote count M) fused with the P-phase tallies (node.ts:92-98): sender group
+// w's proposal masks are added to every receiver group's counts as soon as
+// they exist, so only one group's proposal planes (two SGPR pairs) is live.
+template <bool ODD, int W>
+__device__ __forceinline__ void p_phase(const uint32_t (&c1r)[W], uint32_t M, uint64_t tailm, uint32_t (&a0)[W],
+                                        uint32_t (&a1)[W]) {
+  const uint32_t hi_t = M >> 1, lo_t = (M + 1u) >> 1;
+  Unroll<W>::run([&](auto wi) {
+    constexpr int w = decltype(wi)::value;
+    const uint64_t vm = (w == W - 1) ? tailm : ~0ull;
+    const uint64_t p1 = vcmp_gt(c1r[w], hi_t + (uint32_t)w) & vm;         // c1 > c0  (node.ts:65-66)
+    const uint64_t p0 = ODD ? (vm & ~p1)                                   // c0 > c1  (node.ts:63-64)
+                            : (vcmp_lt(c1r[w], lo_t + (uint32_t)w) & vm);  // else "?"
+    const uint32_t l0 = (uint32_t)p0, h0 = (uint32_t)(p0 >> 32);
+    const uint32_t l1 = (uint32_t)p1, h1 = (uint32_t)(p1 >> 32);
+    if constexpr (w == 0) {
+      Unroll<W>::run([&](auto gi) {
+        constexpr int g = decltype(gi)::value;
+        a0[g] = tally_first_s<g>(l0);
+        a1[g] = tally_first_s<g>(l1);
+      });
+    } else {
+#pragma unroll
+      for (int g = 0; g < W; ++g) {
+        a0[g] = tally_s(l0, a0[g]);
+        a1[g] = tally_s(l1, a1[g]);
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < W; ++g) {
+      a0[g] = tally_s(h0, a0[g]);
+      a1[g] = tally_s(h1, a1[g]);
+    }
+  });
+}
+
 template <int W>
 __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
   constexpr int NPH = (W + 1) / 2;          // Philox blocks per trial (2 plane words each)
@@ -240,24 +311,37 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
   const uint32_t wv = threadIdx.x >> 6;
   // Kernel arguments are copied to locals once: nothing below (lambdas
   // included) refers to `p`, so the struct is never materialised in SGPRs.
-  const uint32_t m = p.m, F = p.F, k_max = p.k_max, hist_len = p.hist_len;
-  const uint64_t trial_begin = p.trial_begin, trial_count = p.trial_count;
+  // The empty asm splits them out of the s_load_dwordx16 tuple the kernarg
+  // loads come in: a live tuple is spilled and reloaded as a whole (16
+  // v_readlane per reload) wherever any one field is needed.
+  uint32_t m = p.m, F = p.F, k_max = p.k_max, hist_len = p.hist_len;
+  uint64_t trial_begin = p.trial_begin, trial_count = p.trial_count;
   const uint32_t *__restrict__ live_ids = p.live_ids;
   bo_node_state *node_out = p.node_out;
   uint32_t *rounds_out = p.rounds_out;
+  asm volatile("" : "+s"(m), "+s"(F), "+s"(k_max), "+s"(hist_len));
+  asm volatile("" : "+s"(trial_begin), "+s"(trial_count), "+s"(live_ids), "+s"(node_out), "+s"(rounds_out));
+  unsigned long long *ghist = p.hist;
+  uint64_t seed = p.seed;
+  asm volatile("" : "+s"(ghist), "+s"(seed));
 
   uint32_t *lhist = reinterpret_cast<uint32_t *>(smem);
   uint2 *ring = reinterpret_cast<uint2 *>(smem + p.hist_bytes + wv * p.wave_bytes);   // [TB][WP] x1 words
-  uint2 *X = ring + TB * WP;                                                            // [WP]
+  uint2 *X = ring + TB * WP;       // [WP] final x1 plane (GET /getState only)
+  uint2 *D = X + WP;               // [WP] sticky decided bits, kept only while some receiver is undecided
+  uint32_t *keys = reinterpret_cast<uint32_t *>(smem + p.hist_bytes - 16u);   // Philox key (seed)
 
   for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) lhist[i] = 0u;
+  if (threadIdx.x == 0) {
+    keys[0] = (uint32_t)seed;
+    keys[1] = (uint32_t)(seed >> 32);
+  }
   if (p.init_mode != BO_INIT_RANDOM && lane < (uint32_t)W) {
     const uint4 q = p.init_plane[lane];
     ring[lane] = make_uint2(q.z, q.w);
   }
   __syncthreads();
 
-  const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
   const uint64_t waves_total = (uint64_t)gridDim.x * kWavesPerBlock;
   const uint64_t tailm = group_mask(W - 1, m);
   const bool random_init = p.init_mode == BO_INIT_RANDOM;
@@ -271,9 +355,8 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
       const uint64_t t = base + (uint64_t)s * waves_total;
       if (s < (uint32_t)TB && t < trial_count) {
         const uint64_t trial = trial_begin + t;
-        uint32_t kk0 = k0, kk1 = k1;
-        asm volatile("" : "+s"(kk0), "+s"(kk1));   // keep the round keys out of long-lived SGPRs
-        const uint4 r = philox4x32_10(kk0, kk1, make_uint4((uint32_t)trial, (uint32_t)(trial >> 32), b, kStreamInit << 24));
+        const uint2 kk = lds_keys(keys);           // keep the round keys out of long-lived SGPRs
+        const uint4 r = philox4x32_10(kk.x, kk.y, make_uint4((uint32_t)trial, (uint32_t)(trial >> 32), b, kStreamInit << 24));
         const uint64_t v0 = group_mask(2u * b, m), v1 = group_mask(2u * b + 1u, m);
         const uint64_t x1a = ((uint64_t)r.y << 32 | r.x) & v0, x1b = ((uint64_t)r.w << 32 | r.z) & v1;
         reinterpret_cast<uint4 *>(ring + s * WP)[b] =
@@ -285,114 +368,103 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
       if (t >= trial_count) break;
       const uint64_t trial = trial_begin + t;
       const uint32_t tlo = (uint32_t)trial, thi = (uint32_t)(trial >> 32);
-      const uint2 *Xr = random_init ? ring + s * WP : ring;
-      uint64_t dec[W];
+      // ---- round-1 R-phase tallies over the /start broadcast (node.ts:167-188)
+      uint32_t c1r[W];
+      tally_x1<W>(random_init ? ring + s * WP : ring, c1r);
       uint64_t any0 = 0, any1 = 0;            // final round's x: some live node 0 / some 1
-#pragma unroll
-      for (int g = 0; g < W; ++g) dec[g] = 0ull;
       uint32_t R = 0, M = m_first;
-      bool all_dec = false;
+      bool all_dec = false, have_hist = false;
       for (uint32_t r = 1;; ++r) {
-        // ---- R-phase ("proposal phase", node.ts:46-82): c1 per receiver, c0 = M - c1
-        uint32_t c1r[W];
-        tally_x1<W>(Xr, c1r);
-        const uint32_t hi_t = M >> 1, lo_t = (M + 1u) >> 1;
-        // ---- P-phase ("voting phase", node.ts:83-158) tallies, fused with the R-phase
-        // ballots: sender group w's proposals (two SGPR pairs) are added to every
-        // receiver group's P-phase counts as soon as they exist, so only one
-        // group's proposal planes is ever live.
+        // ---- R-phase ("proposal phase", node.ts:46-82) proposals from c1 (c0 = M - c1)
+        // fused with the P-phase ("voting phase", node.ts:83-158) tallies.  With an
+        // odd number M of binary votes c0 == c1 is impossible, so "c0 > c1" is the
+        // complement of "c1 > c0" and costs no second compare (ODD: one copy of the
+        // phase per parity, no branch inside it).
         uint32_t a0[W], a1[W];
-#if BENOR_FUSED
-        Unroll<W>::run([&](auto wi) {
-          constexpr int w = decltype(wi)::value;
-          const uint64_t vm = (w == W - 1) ? tailm : ~0ull;
-          const uint64_t p1 = ballot_s(c1r[w] > hi_t + (uint32_t)w) & vm;   // c1 > c0  (node.ts:65-66)
-          const uint64_t p0 = ballot_s(c1r[w] < lo_t + (uint32_t)w) & vm;   // c0 > c1  (node.ts:63-64); else "?"
-          const uint32_t l0 = sgpr32((uint32_t)p0), h0 = sgpr32((uint32_t)(p0 >> 32));
-          const uint32_t l1 = sgpr32((uint32_t)p1), h1 = sgpr32((uint32_t)(p1 >> 32));
-          if constexpr (w == 0) {
-            Unroll<W>::run([&](auto gi) {
-              constexpr int g = decltype(gi)::value;
-              a0[g] = tally_first_s<g>(l0);
-              a1[g] = tally_first_s<g>(l1);
-            });
-          } else {
-#pragma unroll
-            for (int g = 0; g < W; ++g) {
-              a0[g] = tally_s(l0, a0[g]);
-              a1[g] = tally_s(l1, a1[g]);
-            }
-          }
-#pragma unroll
-          for (int g = 0; g < W; ++g) {
-            a0[g] = tally_s(h0, a0[g]);
-            a1[g] = tally_s(h1, a1[g]);
-          }
-        });
-#else
-        uint64_t p0s[W], p1s[W];
-        Unroll<W>::run([&](auto gi) {
-          constexpr int g = decltype(gi)::value;
-          const uint64_t vm = (g == W - 1) ? tailm : ~0ull;
-          p1s[g] = ballot_s(c1r[g] > hi_t + (uint32_t)g) & vm;
-          p0s[g] = ballot_s(c1r[g] < lo_t + (uint32_t)g) & vm;
-        });
-        Unroll<W>::run([&](auto wi) {
-          constexpr int w = decltype(wi)::value;
-          const uint32_t l0 = sgpr32((uint32_t)p0s[w]), h0 = sgpr32((uint32_t)(p0s[w] >> 32));
-          const uint32_t l1 = sgpr32((uint32_t)p1s[w]), h1 = sgpr32((uint32_t)(p1s[w] >> 32));
-          if constexpr (w == 0) {
-            Unroll<W>::run([&](auto gi) {
-              constexpr int g = decltype(gi)::value;
-              a0[g] = tally_first_s<g>(l0);
-              a1[g] = tally_first_s<g>(l1);
-            });
-          } else {
-#pragma unroll
-            for (int g = 0; g < W; ++g) {
-              a0[g] = tally_s(l0, a0[g]);
-              a1[g] = tally_s(l1, a1[g]);
-            }
-          }
-#pragma unroll
-          for (int g = 0; g < W; ++g) {
-            a0[g] = tally_s(h0, a0[g]);
-            a1[g] = tally_s(h1, a1[g]);
-          }
-        });
-#endif
-        bool done = true;
-        uint32_t st = 0;
+        if (M & 1u) p_phase<true, W>(c1r, M, tailm, a0, a1);
+        else p_phase<false, W>(c1r, M, tailm, a0, a1);
+        R = r;                                                        // node.ts:147  k = r + 1
+        // ---- decisions (node.ts:99-105).  When every live receiver decides in this
+        // round the trial halts (decided is sticky) and x = the decided value, so
+        // neither the adopt/coin branch nor the next round's planes are needed.
+        uint64_t rest_any = 0;
         any0 = 0;
         any1 = 0;
         Unroll<W>::run([&](auto gi) {
           constexpr int g = decltype(gi)::value;
           const uint64_t vm = (g == W - 1) ? tailm : ~0ull;
-          const uint32_t Fg = F + (uint32_t)g;                        // chain bias g
-          const uint64_t d0 = ballot_s(a0[g] > Fg) & vm;                 // node.ts:99
-          const uint64_t d1 = ballot_s(a1[g] > Fg) & vm & ~d0;           // node.ts:102
+          const uint32_t Fg = F + (uint32_t)g;                          // chain bias g
+          const uint64_t d0 = vcmp_gt(a0[g], Fg) & vm;                   // node.ts:99
+          const uint64_t d1 = vcmp_gt(a1[g], Fg) & vm & ~d0;             // node.ts:102
+          rest_any |= vm & ~(d0 | d1);
+          any0 |= d0;
+          any1 |= d1;
+          // fold now: otherwise the ORs sink to the loop exit and all 2W masks stay live
+          asm volatile("" : "+s"(rest_any), "+s"(any0), "+s"(any1));
+        });
+        if (!rest_any && !node_out) {
+          all_dec = true;                                             // all-decided auto-stop
+          break;
+        }
+        // ---- some receiver did not decide: adopt / coin (node.ts:106-113), the
+        // sticky decided history (LDS, only on this path), and the next round's
+        // R-phase tallies fused with the new x ballots (no staged plane).
+        const bool more = r < k_max;
+        bool done = true;
+        uint32_t sx = 0, sd = 0;
+        any0 = 0;
+        any1 = 0;
+        Unroll<W>::run([&](auto gi) {
+          constexpr int g = decltype(gi)::value;
+          const uint64_t vm = (g == W - 1) ? tailm : ~0ull;
+          const uint32_t Fg = F + (uint32_t)g;
+          const uint64_t d0 = vcmp_gt(a0[g], Fg) & vm;
+          const uint64_t d1 = vcmp_gt(a1[g], Fg) & vm & ~d0;
           const uint64_t rest = vm & ~(d0 | d1);
           uint64_t x1 = d1;
-          if (rest) {                                                   // some receiver did not decide
+          if (rest) {
             const uint64_t ad1 = ballot_s(a1[g] > a0[g]) & rest;         // node.ts:108-109
             const uint64_t tie = ballot_s(a1[g] == a0[g]) & rest;        // node.ts:110-111
             x1 |= ad1;
-            if (tie) x1 |= (coin_ballot(k0, k1, tlo, thi, live_ids, g, r, tie));   // node.ts:111
+            if (tie) x1 |= (coin_ballot(keys, tlo, thi, live_ids, g, r, tie));   // node.ts:111
           }
-          // next round's x plane: only the is1 word (every x is 0 or 1 from here on)
-          st = writelane<2 * g>(st, (uint32_t)x1);
-          st = writelane<2 * g + 1>(st, (uint32_t)(x1 >> 32));
+          uint64_t dg = d0 | d1;
+          if (have_hist) {
+            const uint2 h = D[g];
+            dg |= (uint64_t)sgpr32(h.y) << 32 | sgpr32(h.x);
+          }
+          sd = writelane<2 * g>(sd, (uint32_t)dg);
+          sd = writelane<2 * g + 1>(sd, (uint32_t)(dg >> 32));
+          done = done && (dg == vm);
           any1 |= x1;
           any0 |= vm & ~x1;
-          dec[g] |= d0 | d1;
-          done = done && (dec[g] == vm);
+          const uint32_t xl = sgpr32((uint32_t)x1), xh = sgpr32((uint32_t)(x1 >> 32));
+          if (more) {                                                 // round r+1 R-phase (node.ts:149-157)
+            if constexpr (g == 0) {
+              Unroll<W>::run([&](auto hi) {
+                constexpr int h = decltype(hi)::value;
+                c1r[h] = tally_first_s<h>(xl);
+              });
+            } else {
+#pragma unroll
+              for (int h = 0; h < W; ++h) c1r[h] = tally_s(xl, c1r[h]);
+            }
+#pragma unroll
+            for (int h = 0; h < W; ++h) c1r[h] = tally_s(xh, c1r[h]);
+          }
+          if (node_out) {
+            sx = writelane<2 * g>(sx, xl);
+            sx = writelane<2 * g + 1>(sx, xh);
+          }
         });
-        if (lane < 2u * W) reinterpret_cast<uint32_t *>(X)[lane] = st;
-        Xr = X;
+        if (lane < 2u * W) {
+          reinterpret_cast<uint32_t *>(D)[lane] = sd;
+          if (node_out) reinterpret_cast<uint32_t *>(X)[lane] = sx;
+        }
+        have_hist = true;
         M = m;
-        R = r;                                                        // node.ts:147  k = r + 1
-        all_dec = done;                                               // all-decided auto-stop
-        if (all_dec || r >= k_max) break;
+        all_dec = done;
+        if (done || !more) break;
       }
       // ---- outcome
       const uint32_t v = (any0 && any1) ? 2u : (any1 ? 1u : 0u);
@@ -406,11 +478,11 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
           constexpr int g = decltype(gi)::value;
           const uint32_t c = g * 64u + lane;
           if (c < m) {
-            const uint2 q = Xr[g];
+            const uint2 q = X[g], d = D[g];
             bo_node_state ns;
             ns.killed = 0;
             ns.x = (int8_t)(((lane < 32u ? q.x : q.y) >> (lane & 31u)) & 1u);
-            ns.decided = (int8_t)((dec[g] >> lane) & 1ull);
+            ns.decided = (int8_t)(((lane < 32u ? d.x : d.y) >> (lane & 31u)) & 1u);
             ns.pad = 0;
             ns.k = (int32_t)R + 1;
             node_out[live_ids[c]] = ns;
@@ -423,7 +495,7 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) {
     const uint32_t c = lhist[i];
-    if (c) atomicAdd(&p.hist[i], (unsigned long long)c);
+    if (c) atomicAdd(&ghist[i], (unsigned long long)c);
   }
 }
 
@@ -1242,7 +1314,7 @@ __global__ void __launch_bounds__(256) popc_peak_kernel(uint32_t *sink, int iter
 void plan_geometry(KParams &p) {
   const uint32_t W = p.W;
   p.hist_len = (p.k_max + 1u) * 3u + 1u;
-  p.hist_bytes = ((p.hist_len * 4u) + 15u) & ~15u;
+  p.hist_bytes = (((p.hist_len * 4u) + 15u) & ~15u) + 16u;   // histogram + Philox key slot
   if (p.mode == BO_MODE_EVENT) {
     p.G = 1;
     p.nblocks = 1;
@@ -1277,7 +1349,7 @@ void plan_geometry(KParams &p) {
     p.G = W;
     p.nblocks = 1;
     p.variant = 1;
-    p.wave_bytes = (tb * WP + WP) * 8u;                 // init ring + staged x1 plane
+    p.wave_bytes = (tb * WP + 2u * WP) * 8u;            // init ring, final x1 plane, decided bits
   } else {
     const uint32_t nb = (W + 15u) / 16u;           // blocks of at most 16 groups
     const uint32_t G = (W + nb - 1u) / nb;         // balanced: padding < nb groups
