@@ -120,6 +120,9 @@ __device__ __forceinline__ uint64_t coin_ballot(const uint32_t *keys, uint32_t t
                                              const uint32_t *__restrict__ live_ids, uint32_t group,
                                              uint32_t round, uint64_t tie) {
   const uint2 k = lds_keys(keys);
+  tlo = (uint32_t)__builtin_amdgcn_readfirstlane((int)tlo);   // wave-uniform trial id; the asm keeps
+  thi = (uint32_t)__builtin_amdgcn_readfirstlane((int)thi);   // Philox's first product on this path
+  asm volatile("" : "+s"(tlo), "+s"(thi));
   return coin_ballot(k.x, k.y, tlo, thi, live_ids, group, round, tie);
 }
 
@@ -301,14 +304,17 @@ __device__ __forceinline__ void p_phase(const uint32_t (&c1r)[W], uint32_t M, ui
   });
 }
 
-template <int W>
+// STATE: the network API's single-trial launch that also reports per-node
+// state and the halting round (GET /getState); the batch path is compiled
+// without that code, which keeps its register allocation free of it.
+template <int W, bool STATE>
 __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
   constexpr int NPH = (W + 1) / 2;          // Philox blocks per trial (2 plane words each)
   constexpr int TB = 64 / NPH;              // trials per init batch
   constexpr int WP = 2 * NPH;               // x1 words per plane row, padded to 16 bytes
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wv = threadIdx.x >> 6;
+  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // uniform: scalar trial loop
   // Kernel arguments are copied to locals once: nothing below (lambdas
   // included) refers to `p`, so the struct is never materialised in SGPRs.
   // The empty asm splits them out of the s_load_dwordx16 tuple the kernarg
@@ -317,8 +323,8 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
   uint32_t m = p.m, F = p.F, k_max = p.k_max, hist_len = p.hist_len;
   uint64_t trial_begin = p.trial_begin, trial_count = p.trial_count;
   const uint32_t *__restrict__ live_ids = p.live_ids;
-  bo_node_state *node_out = p.node_out;
-  uint32_t *rounds_out = p.rounds_out;
+  bo_node_state *node_out = STATE ? p.node_out : nullptr;
+  uint32_t *rounds_out = STATE ? p.rounds_out : nullptr;
   asm volatile("" : "+s"(m), "+s"(F), "+s"(k_max), "+s"(hist_len));
   asm volatile("" : "+s"(trial_begin), "+s"(trial_count), "+s"(live_ids), "+s"(node_out), "+s"(rounds_out));
   unsigned long long *ghist = p.hist;
@@ -347,6 +353,7 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
   const bool random_init = p.init_mode == BO_INIT_RANDOM;
   const uint32_t m_first = m - p.init_q;      // binary-valued senders in round 1 ("?" excluded)
 
+  uint32_t hc = 0;                            // this wave's outcome counts, lane = bin (hist_len <= 64)
   for (uint64_t base = (uint64_t)blockIdx.x * kWavesPerBlock + wv; base < trial_count;
        base += waves_total * TB) {
     // ---- /start (node.ts:167-188): round-1 x planes of TB trials at once.
@@ -402,7 +409,7 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
           // fold now: otherwise the ORs sink to the loop exit and all 2W masks stay live
           asm volatile("" : "+s"(rest_any), "+s"(any0), "+s"(any1));
         });
-        if (!rest_any && !node_out) {
+        if (!rest_any && !STATE) {
           all_dec = true;                                             // all-decided auto-stop
           break;
         }
@@ -452,14 +459,14 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
 #pragma unroll
             for (int h = 0; h < W; ++h) c1r[h] = tally_s(xh, c1r[h]);
           }
-          if (node_out) {
+          if constexpr (STATE) {
             sx = writelane<2 * g>(sx, xl);
             sx = writelane<2 * g + 1>(sx, xh);
           }
         });
         if (lane < 2u * W) {
           reinterpret_cast<uint32_t *>(D)[lane] = sd;
-          if (node_out) reinterpret_cast<uint32_t *>(X)[lane] = sx;
+          if (STATE) reinterpret_cast<uint32_t *>(X)[lane] = sx;
         }
         have_hist = true;
         M = m;
@@ -468,12 +475,18 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
       }
       // ---- outcome
       const uint32_t v = (any0 && any1) ? 2u : (any1 ? 1u : 0u);
-      if (lane == 0) {
-        atomicAdd(&lhist[all_dec ? (R * 3u + v) : v], 1u);
+      const uint32_t bin = all_dec ? (R * 3u + v) : v;
+      if (hist_len <= 64u) {                                        // lane `bin` of the wave's counter
+        hc += (lane == bin) ? 1u : 0u;
+        if (all_dec && v == 2u) hc += (lane == hist_len - 1u) ? 1u : 0u;
+      } else if (lane == 0) {
+        atomicAdd(&lhist[bin], 1u);
         if (all_dec && v == 2u) atomicAdd(&lhist[hist_len - 1u], 1u);
-        if (rounds_out) *rounds_out = all_dec ? R : 0u;
       }
-      if (node_out) {                                               // GET /getState (node.ts:197-199)
+      if constexpr (STATE) {
+        if (lane == 0 && rounds_out) *rounds_out = all_dec ? R : 0u;
+      }
+      if (STATE && node_out) {                                               // GET /getState (node.ts:197-199)
         Unroll<W>::run([&](auto gi) {
           constexpr int g = decltype(gi)::value;
           const uint32_t c = g * 64u + lane;
@@ -492,6 +505,7 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
     }
   }
 
+  if (hist_len <= 64u && hc) atomicAdd(&lhist[lane], hc);
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) {
     const uint32_t c = lhist[i];
@@ -1364,7 +1378,10 @@ void plan_geometry(KParams &p) {
 
 template <int W>
 static hipError_t launch_w(const KParams &p, int grid, hipStream_t s) {
-  hipLaunchKernelGGL(benor_lockstep_w_kernel<W>, dim3(grid), dim3(64 * kWavesPerBlock), p.lds_bytes, s, p);
+  if (p.node_out || p.rounds_out)
+    hipLaunchKernelGGL((benor_lockstep_w_kernel<W, true>), dim3(grid), dim3(64 * kWavesPerBlock), p.lds_bytes, s, p);
+  else
+    hipLaunchKernelGGL((benor_lockstep_w_kernel<W, false>), dim3(grid), dim3(64 * kWavesPerBlock), p.lds_bytes, s, p);
   return hipGetLastError();
 }
 
