@@ -353,7 +353,7 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
   const bool random_init = p.init_mode == BO_INIT_RANDOM;
   const uint32_t m_first = m - p.init_q;      // binary-valued senders in round 1 ("?" excluded)
 
-  uint32_t hc = 0;                            // this wave's outcome counts, lane = bin (hist_len <= 64)
+  uint32_t hc = 0;                            // this wave's outcome counts of bins 0..63, lane = bin
   for (uint64_t base = (uint64_t)blockIdx.x * kWavesPerBlock + wv; base < trial_count;
        base += waves_total * TB) {
     // ---- /start (node.ts:167-188): round-1 x planes of TB trials at once.
@@ -476,13 +476,11 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
       // ---- outcome
       const uint32_t v = (any0 && any1) ? 2u : (any1 ? 1u : 0u);
       const uint32_t bin = all_dec ? (R * 3u + v) : v;
-      if (hist_len <= 64u) {                                        // lane `bin` of the wave's counter
-        hc += (lane == bin) ? 1u : 0u;
-        if (all_dec && v == 2u) hc += (lane == hist_len - 1u) ? 1u : 0u;
-      } else if (lane == 0) {
-        atomicAdd(&lhist[bin], 1u);
-        if (all_dec && v == 2u) atomicAdd(&lhist[hist_len - 1u], 1u);
-      }
+      // bins 0..63 (undecided, and halting rounds <= 20): lane `bin` of the
+      // wave's counter, one VALU op; the rest: an LDS atomic
+      if (bin < 64u) hc += (lane == bin) ? 1u : 0u;
+      else if (lane == 0) atomicAdd(&lhist[bin], 1u);
+      if (all_dec && v == 2u && lane == 0) atomicAdd(&lhist[hist_len - 1u], 1u);
       if constexpr (STATE) {
         if (lane == 0 && rounds_out) *rounds_out = all_dec ? R : 0u;
       }
@@ -505,7 +503,7 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
     }
   }
 
-  if (hist_len <= 64u && hc) atomicAdd(&lhist[lane], hc);
+  if (hc) atomicAdd(&lhist[lane], hc);
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) {
     const uint32_t c = lhist[i];

@@ -53,10 +53,11 @@ def main(tag, trials, N=1024, F=341):
     for k in sorted(c):
         lines.append(f"| {k} | {c[k]:.6g} | {c[k] / trials:.4g} |")
     if "SQ_INSTS_VALU" in c:
-        bcnt = 4 * ((m + 31) // 32) * m / 64 * 1.0
-        lines += ["", f"- v_bcnt per trial (algorithmic, 4*ceil(m/32) words x ceil(m/64) groups): "
-                      f"{4 * ((m + 31) // 32) * ((m + 63) // 64)}",
-                  f"- VALU instructions per trial: {c['SQ_INSTS_VALU'] / trials:.1f}"]
+        W = (m + 63) // 64
+        bcnt = 6 * W * W     # per receiver group: 2W words (R-phase c1) + 4W words (P-phase c0, c1)
+        lines += ["", f"- v_bcnt per trial (one round; 6W words per receiver group x W groups, W = ceil(m/64)): {bcnt}",
+                  f"- VALU instructions per trial: {c['SQ_INSTS_VALU'] / trials:.1f} "
+                  f"(non-v_bcnt: {c['SQ_INSTS_VALU'] / trials - bcnt:.1f})"]
     if "GRBM_GUI_ACTIVE" in c and stats:
         for r in csv.DictReader(open(stats[0])):
             if "lockstep" in r["Name"]:
