@@ -21,6 +21,7 @@ constexpr int kWavesPerBlock = 4;          // 256-thread workgroups, one trial p
 constexpr uint32_t kMaxW = BO_MAX_N / 64;  // u64 words per bit plane at N = 4096
 constexpr int kMaxWSpecialised = 16;       // m <= 1024: fully unrolled W-specialised kernel
 constexpr uint32_t kMaxPackedM = 32;       // m <= 32: packed kernel, floor(32/m) trials per half-wave
+constexpr uint64_t kMaxTrialsPerLaunch = 1ull << 31;   // trial offsets within a launch fit 32 bits
 
 struct KParams {
   uint32_t N, F;            // network size, fault parameter

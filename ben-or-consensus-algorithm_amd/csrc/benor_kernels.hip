@@ -229,6 +229,12 @@ __device__ __forceinline__ uint32_t tally_s(uint32_t word, uint32_t acc) {
   return r;
 }
 
+// Fresh scalar load of a kernel argument at the point of use (see the W kernel).
+template <class T>
+__device__ __forceinline__ T kload(const T &arg) {
+  return *const_cast<const volatile T *>(&arg);
+}
+
 __device__ __forceinline__ uint32_t sgpr32(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
 }
@@ -315,21 +321,15 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // uniform: scalar trial loop
-  // Kernel arguments are copied to locals once: nothing below (lambdas
-  // included) refers to `p`, so the struct is never materialised in SGPRs.
-  // The empty asm splits them out of the s_load_dwordx16 tuple the kernarg
-  // loads come in: a live tuple is spilled and reloaded as a whole (16
-  // v_readlane per reload) wherever any one field is needed.
+  // Only the round loop's own scalars are kept in registers.  Everything a
+  // rare path needs (trial id base, live ids, outputs) is re-read from the
+  // kernarg segment where it is used (kload: a volatile scalar load, no
+  // VALU), so the register allocator never holds -- and spills -- a
+  // kernarg tuple across the trial loop.
   uint32_t m = p.m, F = p.F, k_max = p.k_max, hist_len = p.hist_len;
-  uint64_t trial_begin = p.trial_begin, trial_count = p.trial_count;
-  const uint32_t *__restrict__ live_ids = p.live_ids;
-  bo_node_state *node_out = STATE ? p.node_out : nullptr;
-  uint32_t *rounds_out = STATE ? p.rounds_out : nullptr;
-  asm volatile("" : "+s"(m), "+s"(F), "+s"(k_max), "+s"(hist_len));
-  asm volatile("" : "+s"(trial_begin), "+s"(trial_count), "+s"(live_ids), "+s"(node_out), "+s"(rounds_out));
-  unsigned long long *ghist = p.hist;
-  uint64_t seed = p.seed;
-  asm volatile("" : "+s"(ghist), "+s"(seed));
+  // trial offsets within the launch are 32-bit (the host splits launches at 2^31)
+  uint32_t trial_count = (uint32_t)p.trial_count;
+  asm volatile("" : "+s"(m), "+s"(F), "+s"(k_max), "+s"(hist_len), "+s"(trial_count));
 
   uint32_t *lhist = reinterpret_cast<uint32_t *>(smem);
   uint2 *ring = reinterpret_cast<uint2 *>(smem + p.hist_bytes + wv * p.wave_bytes);   // [TB][WP] x1 words
@@ -339,6 +339,7 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
 
   for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) lhist[i] = 0u;
   if (threadIdx.x == 0) {
+    const uint64_t seed = kload(p.seed);
     keys[0] = (uint32_t)seed;
     keys[1] = (uint32_t)(seed >> 32);
   }
@@ -348,20 +349,19 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
   }
   __syncthreads();
 
-  const uint64_t waves_total = (uint64_t)gridDim.x * kWavesPerBlock;
+  const uint32_t waves_total = gridDim.x * kWavesPerBlock;
   const uint64_t tailm = group_mask(W - 1, m);
   const bool random_init = p.init_mode == BO_INIT_RANDOM;
   const uint32_t m_first = m - p.init_q;      // binary-valued senders in round 1 ("?" excluded)
 
   uint32_t hc = 0;                            // this wave's outcome counts of bins 0..63, lane = bin
-  for (uint64_t base = (uint64_t)blockIdx.x * kWavesPerBlock + wv; base < trial_count;
-       base += waves_total * TB) {
+  for (uint32_t base = blockIdx.x * kWavesPerBlock + wv; base < trial_count; base += waves_total * TB) {
     // ---- /start (node.ts:167-188): round-1 x planes of TB trials at once.
     if (random_init) {
       const uint32_t s = lane / NPH, b = lane - s * NPH;
-      const uint64_t t = base + (uint64_t)s * waves_total;
+      const uint32_t t = base + s * waves_total;
       if (s < (uint32_t)TB && t < trial_count) {
-        const uint64_t trial = trial_begin + t;
+        const uint64_t trial = kload(p.trial_begin) + t;
         const uint2 kk = lds_keys(keys);           // keep the round keys out of long-lived SGPRs
         const uint4 r = philox4x32_10(kk.x, kk.y, make_uint4((uint32_t)trial, (uint32_t)(trial >> 32), b, kStreamInit << 24));
         const uint64_t v0 = group_mask(2u * b, m), v1 = group_mask(2u * b + 1u, m);
@@ -371,10 +371,8 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
       }
     }
     for (int s = 0; s < TB; ++s) {
-      const uint64_t t = base + (uint64_t)s * waves_total;
+      const uint32_t t = base + (uint32_t)s * waves_total;
       if (t >= trial_count) break;
-      const uint64_t trial = trial_begin + t;
-      const uint32_t tlo = (uint32_t)trial, thi = (uint32_t)(trial >> 32);
       // ---- round-1 R-phase tallies over the /start broadcast (node.ts:167-188)
       uint32_t c1r[W];
       tally_x1<W>(random_init ? ring + s * WP : ring, c1r);
@@ -417,7 +415,7 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
         // sticky decided history (LDS, only on this path), and the next round's
         // R-phase tallies fused with the new x ballots (no staged plane).
         const bool more = r < k_max;
-        bool done = true;
+        uint64_t undone = 0;
         uint32_t sx = 0, sd = 0;
         any0 = 0;
         any1 = 0;
@@ -433,7 +431,10 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
             const uint64_t ad1 = ballot_s(a1[g] > a0[g]) & rest;         // node.ts:108-109
             const uint64_t tie = ballot_s(a1[g] == a0[g]) & rest;        // node.ts:110-111
             x1 |= ad1;
-            if (tie) x1 |= (coin_ballot(keys, tlo, thi, live_ids, g, r, tie));   // node.ts:111
+            if (tie) {                                                  // node.ts:111
+              const uint64_t trial = kload(p.trial_begin) + t;
+              x1 |= coin_ballot(keys, (uint32_t)trial, (uint32_t)(trial >> 32), kload(p.live_ids), g, r, tie);
+            }
           }
           uint64_t dg = d0 | d1;
           if (have_hist) {
@@ -442,9 +443,10 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
           }
           sd = writelane<2 * g>(sd, (uint32_t)dg);
           sd = writelane<2 * g + 1>(sd, (uint32_t)(dg >> 32));
-          done = done && (dg == vm);
+          undone |= vm & ~dg;
           any1 |= x1;
           any0 |= vm & ~x1;
+          asm volatile("" : "+s"(undone), "+s"(any0), "+s"(any1));   // fold per group (as in the decisions)
           const uint32_t xl = sgpr32((uint32_t)x1), xh = sgpr32((uint32_t)(x1 >> 32));
           if (more) {                                                 // round r+1 R-phase (node.ts:149-157)
             if constexpr (g == 0) {
@@ -470,8 +472,8 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
         }
         have_hist = true;
         M = m;
-        all_dec = done;
-        if (done || !more) break;
+        all_dec = undone == 0;
+        if (all_dec || !more) break;
       }
       // ---- outcome
       const uint32_t v = (any0 && any1) ? 2u : (any1 ? 1u : 0u);
@@ -482,8 +484,10 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
       else if (lane == 0) atomicAdd(&lhist[bin], 1u);
       if (all_dec && v == 2u && lane == 0) atomicAdd(&lhist[hist_len - 1u], 1u);
       if constexpr (STATE) {
+        uint32_t *rounds_out = kload(p.rounds_out);
         if (lane == 0 && rounds_out) *rounds_out = all_dec ? R : 0u;
       }
+      bo_node_state *node_out = STATE ? kload(p.node_out) : nullptr;
       if (STATE && node_out) {                                               // GET /getState (node.ts:197-199)
         Unroll<W>::run([&](auto gi) {
           constexpr int g = decltype(gi)::value;
@@ -496,7 +500,7 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
             ns.decided = (int8_t)(((lane < 32u ? d.x : d.y) >> (lane & 31u)) & 1u);
             ns.pad = 0;
             ns.k = (int32_t)R + 1;
-            node_out[live_ids[c]] = ns;
+            node_out[kload(p.live_ids)[c]] = ns;
           }
         });
       }
@@ -507,7 +511,7 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) {
     const uint32_t c = lhist[i];
-    if (c) atomicAdd(&ghist[i], (unsigned long long)c);
+    if (c) atomicAdd(&p.hist[i], (unsigned long long)c);
   }
 }
 

@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <algorithm>
 #include <vector>
 
 #include "benor.h"
@@ -325,13 +326,18 @@ static int plan_launch_impl(bo_plan *pl, uint64_t trial_begin, uint64_t trial_co
     HIP_TRY(hipGetLastError());
     return BO_OK;
   }
-  kp.trial_begin = trial_begin;
-  kp.trial_count = trial_count;
   kp.hist = reinterpret_cast<unsigned long long *>(hist_dev);
   kp.node_out = node_out;
   kp.rounds_out = rounds_out;
-  const int grid = benor::lockstep_grid(kp, pl->device);
-  HIP_TRY(benor::launch_lockstep(kp, grid, s));
+  // Launches of at most 2^31 trials: the kernels index trials within a launch in 32 bits.
+  for (uint64_t done = 0; done < trial_count;) {
+    const uint64_t n = std::min<uint64_t>(trial_count - done, benor::kMaxTrialsPerLaunch);
+    kp.trial_begin = trial_begin + done;
+    kp.trial_count = n;
+    const int grid = benor::lockstep_grid(kp, pl->device);
+    HIP_TRY(benor::launch_lockstep(kp, grid, s));
+    done += n;
+  }
   return BO_OK;
 }
 
