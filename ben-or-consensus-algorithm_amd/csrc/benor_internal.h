@@ -22,6 +22,7 @@ constexpr uint32_t kMaxW = BO_MAX_N / 64;  // u64 words per bit plane at N = 409
 constexpr int kMaxWSpecialised = 16;       // m <= 1024: fully unrolled W-specialised kernel
 constexpr uint32_t kMaxPackedM = 32;       // m <= 32: packed kernel, floor(32/m) trials per half-wave
 constexpr uint64_t kMaxTrialsPerLaunch = 1ull << 31;   // trial offsets within a launch fit 32 bits
+constexpr uint32_t kParamBytes = 32;       // LDS parameter block after the histogram (W kernel)
 
 struct KParams {
   uint32_t N, F;            // network size, fault parameter

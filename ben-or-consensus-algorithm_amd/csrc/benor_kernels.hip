@@ -111,7 +111,8 @@ __device__ __forceinline__ uint64_t coin_ballot(uint32_t k0, uint32_t k1, uint32
 // init pass) is rebuilt there instead of being kept -- i.e. spilled -- in SGPRs
 // across the whole round loop.
 __device__ __forceinline__ uint2 lds_keys(const uint32_t *keys) {
-  const volatile uint32_t *k = keys;
+  const volatile __attribute__((address_space(3))) uint32_t *k =
+      (const volatile __attribute__((address_space(3))) uint32_t *)keys;   // ds_read, not a flat load
   return make_uint2((uint32_t)__builtin_amdgcn_readfirstlane((int)k[0]),
                     (uint32_t)__builtin_amdgcn_readfirstlane((int)k[1]));
 }
@@ -229,10 +230,15 @@ __device__ __forceinline__ uint32_t tally_s(uint32_t word, uint32_t acc) {
   return r;
 }
 
-// Fresh scalar load of a kernel argument at the point of use (see the W kernel).
-template <class T>
-__device__ __forceinline__ T kload(const T &arg) {
-  return *const_cast<const volatile T *>(&arg);
+// Wave-uniform 64-bit value re-read from LDS at the point of use (volatile:
+// the read stays where it is written, see the W kernel's parameter block).
+typedef const volatile __attribute__((address_space(3))) uint32_t lds_cv_u32;
+
+__device__ __forceinline__ uint64_t lds_u64(const uint32_t *w) {
+  lds_cv_u32 *k = (lds_cv_u32 *)w;   // ds_read, not a flat load
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)k[0]);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)k[1]);
+  return (uint64_t)hi << 32 | lo;
 }
 
 __device__ __forceinline__ uint32_t sgpr32(uint32_t v) {
@@ -321,11 +327,11 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // uniform: scalar trial loop
-  // Only the round loop's own scalars are kept in registers.  Everything a
-  // rare path needs (trial id base, live ids, outputs) is re-read from the
-  // kernarg segment where it is used (kload: a volatile scalar load, no
-  // VALU), so the register allocator never holds -- and spills -- a
-  // kernarg tuple across the trial loop.
+  // Only the round loop's own scalars are kept in registers.  What a rare
+  // path needs (Philox key, trial id base, live ids) sits in a small LDS
+  // parameter block and is re-read where it is used, so the register
+  // allocator never holds -- and spills -- a kernarg tuple across the
+  // trial loop.
   uint32_t m = p.m, F = p.F, k_max = p.k_max, hist_len = p.hist_len;
   // trial offsets within the launch are 32-bit (the host splits launches at 2^31)
   uint32_t trial_count = (uint32_t)p.trial_count;
@@ -335,13 +341,17 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
   uint2 *ring = reinterpret_cast<uint2 *>(smem + p.hist_bytes + wv * p.wave_bytes);   // [TB][WP] x1 words
   uint2 *X = ring + TB * WP;       // [WP] final x1 plane (GET /getState only)
   uint2 *D = X + WP;               // [WP] sticky decided bits, kept only while some receiver is undecided
-  uint32_t *keys = reinterpret_cast<uint32_t *>(smem + p.hist_bytes - 16u);   // Philox key (seed)
+  // parameter block: [0,1] Philox key (seed), [2,3] trial_begin, [4,5] live_ids
+  uint32_t *keys = reinterpret_cast<uint32_t *>(smem + p.hist_bytes - kParamBytes);
 
   for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) lhist[i] = 0u;
   if (threadIdx.x == 0) {
-    const uint64_t seed = kload(p.seed);
-    keys[0] = (uint32_t)seed;
-    keys[1] = (uint32_t)(seed >> 32);
+    keys[0] = (uint32_t)p.seed;
+    keys[1] = (uint32_t)(p.seed >> 32);
+    keys[2] = (uint32_t)p.trial_begin;
+    keys[3] = (uint32_t)(p.trial_begin >> 32);
+    keys[4] = (uint32_t)(uintptr_t)p.live_ids;
+    keys[5] = (uint32_t)((uintptr_t)p.live_ids >> 32);
   }
   if (p.init_mode != BO_INIT_RANDOM && lane < (uint32_t)W) {
     const uint4 q = p.init_plane[lane];
@@ -361,7 +371,7 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
       const uint32_t s = lane / NPH, b = lane - s * NPH;
       const uint32_t t = base + s * waves_total;
       if (s < (uint32_t)TB && t < trial_count) {
-        const uint64_t trial = kload(p.trial_begin) + t;
+        const uint64_t trial = lds_u64(keys + 2) + t;
         const uint2 kk = lds_keys(keys);           // keep the round keys out of long-lived SGPRs
         const uint4 r = philox4x32_10(kk.x, kk.y, make_uint4((uint32_t)trial, (uint32_t)(trial >> 32), b, kStreamInit << 24));
         const uint64_t v0 = group_mask(2u * b, m), v1 = group_mask(2u * b + 1u, m);
@@ -432,8 +442,9 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
             const uint64_t tie = ballot_s(a1[g] == a0[g]) & rest;        // node.ts:110-111
             x1 |= ad1;
             if (tie) {                                                  // node.ts:111
-              const uint64_t trial = kload(p.trial_begin) + t;
-              x1 |= coin_ballot(keys, (uint32_t)trial, (uint32_t)(trial >> 32), kload(p.live_ids), g, r, tie);
+              const uint64_t trial = lds_u64(keys + 2) + t;
+              const uint32_t *ids = reinterpret_cast<const uint32_t *>((uintptr_t)lds_u64(keys + 4));
+              x1 |= coin_ballot(keys, (uint32_t)trial, (uint32_t)(trial >> 32), ids, g, r, tie);
             }
           }
           uint64_t dg = d0 | d1;
@@ -484,10 +495,10 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
       else if (lane == 0) atomicAdd(&lhist[bin], 1u);
       if (all_dec && v == 2u && lane == 0) atomicAdd(&lhist[hist_len - 1u], 1u);
       if constexpr (STATE) {
-        uint32_t *rounds_out = kload(p.rounds_out);
+        uint32_t *rounds_out = p.rounds_out;
         if (lane == 0 && rounds_out) *rounds_out = all_dec ? R : 0u;
       }
-      bo_node_state *node_out = STATE ? kload(p.node_out) : nullptr;
+      bo_node_state *node_out = STATE ? p.node_out : nullptr;
       if (STATE && node_out) {                                               // GET /getState (node.ts:197-199)
         Unroll<W>::run([&](auto gi) {
           constexpr int g = decltype(gi)::value;
@@ -500,7 +511,7 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
             ns.decided = (int8_t)(((lane < 32u ? d.x : d.y) >> (lane & 31u)) & 1u);
             ns.pad = 0;
             ns.k = (int32_t)R + 1;
-            node_out[kload(p.live_ids)[c]] = ns;
+            node_out[p.live_ids[c]] = ns;
           }
         });
       }
@@ -1330,7 +1341,7 @@ __global__ void __launch_bounds__(256) popc_peak_kernel(uint32_t *sink, int iter
 void plan_geometry(KParams &p) {
   const uint32_t W = p.W;
   p.hist_len = (p.k_max + 1u) * 3u + 1u;
-  p.hist_bytes = (((p.hist_len * 4u) + 15u) & ~15u) + 16u;   // histogram + Philox key slot
+  p.hist_bytes = (((p.hist_len * 4u) + 15u) & ~15u) + kParamBytes;   // histogram + parameter block
   if (p.mode == BO_MODE_EVENT) {
     p.G = 1;
     p.nblocks = 1;
