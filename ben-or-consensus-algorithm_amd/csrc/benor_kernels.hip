@@ -606,23 +606,55 @@ __device__ __forceinline__ void tally_groups_x1(const uint2 *__restrict__ plane,
   }
 }
 
-template <int G>
+// One block's R-phase proposals (node.ts:63-69) from the receivers' c1
+// counts, staged as {p0.lo, p0.hi, p1.lo, p1.hi} records for the P-phase
+// tallies of every block.  ODD: an odd number of binary votes cannot tie,
+// so p0 is the complement of p1 (one compare per group).
+template <bool ODD, int G>
+__device__ __forceinline__ uint32_t stage_proposals(const uint32_t (&a1)[G], uint32_t b, uint32_t m, uint32_t M) {
+  const uint32_t hi_t = M >> 1, lo_t = (M + 1u) >> 1;
+  uint32_t st = 0;
+  Unroll<G>::run([&](auto gi) {
+    constexpr int g = decltype(gi)::value;
+    const uint64_t vm = group_mask(b * G + g, m);
+    const uint64_t p1 = vcmp_gt(a1[g], hi_t + (uint32_t)g) & vm;          // c1 > c0  (node.ts:65-66)
+    const uint64_t p0 = ODD ? (vm & ~p1)                                   // c0 > c1  (node.ts:63-64)
+                            : (vcmp_lt(a1[g], lo_t + (uint32_t)g) & vm);   // else "?"
+    st = stage4<g>(st, p0, p1);
+  });
+  return st;
+}
+
+template <int G, bool STATE>
 __global__ void __launch_bounds__(256) benor_lockstep_blocked_kernel(KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wv = threadIdx.x >> 6;
-  const uint32_t m = p.m, F = p.F, W = p.W, NB = p.nblocks;
+  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // scalar trial loop
+  // Round-loop scalars in registers; the rest re-read where used (as the W kernel).
+  uint32_t m = p.m, F = p.F, W = p.W, NB = p.nblocks, k_max = p.k_max, hist_len = p.hist_len;
+  uint32_t trial_count = (uint32_t)p.trial_count;     // launches are split at 2^31 trials
+  asm volatile("" : "+s"(m), "+s"(F), "+s"(W), "+s"(NB));
+  asm volatile("" : "+s"(k_max), "+s"(hist_len), "+s"(trial_count));
   const uint32_t nph = (W + 1u) >> 1, tb = 64u / nph, WP = 2u * nph;
   const uint32_t XW = ((NB * G > WP ? NB * G : WP) + 1u) & ~1u;   // x1 words of the staged plane (even, padding zero)
   const uint32_t tail_n = m - (W - 1u) * 64u;          // live receivers in the last group
 
   uint32_t *lhist = reinterpret_cast<uint32_t *>(smem);
+  uint32_t *keys = reinterpret_cast<uint32_t *>(smem + p.hist_bytes - kParamBytes);   // see the W kernel
   uint2 *ring = reinterpret_cast<uint2 *>(smem + p.hist_bytes + wv * p.wave_bytes);   // [tb][WP] x1 words
   uint2 *X = ring + tb * WP;                                                            // [XW]
   uint4 *P = reinterpret_cast<uint4 *>(X + XW);                                        // [NB*G]
   uint32_t *D = reinterpret_cast<uint32_t *>(P + NB * G);                               // [NB][64] decided bits
 
-  for (uint32_t i = threadIdx.x; i < p.hist_len; i += blockDim.x) lhist[i] = 0u;
+  for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) lhist[i] = 0u;
+  if (threadIdx.x == 0) {
+    keys[0] = (uint32_t)p.seed;
+    keys[1] = (uint32_t)(p.seed >> 32);
+    keys[2] = (uint32_t)p.trial_begin;
+    keys[3] = (uint32_t)(p.trial_begin >> 32);
+    keys[4] = (uint32_t)(uintptr_t)p.live_ids;
+    keys[5] = (uint32_t)((uintptr_t)p.live_ids >> 32);
+  }
   if (p.init_mode != BO_INIT_RANDOM)
     for (uint32_t w = lane; w < WP; w += 64u) {
       const uint4 q = w < W ? p.init_plane[w] : make_uint4(0, 0, 0, 0);
@@ -631,21 +663,19 @@ __global__ void __launch_bounds__(256) benor_lockstep_blocked_kernel(KParams p) 
   for (uint32_t w = lane; w < XW; w += 64u) X[w] = make_uint2(0u, 0u);
   __syncthreads();
 
-  const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
-  const uint64_t waves_total = (uint64_t)gridDim.x * kWavesPerBlock;
+  const uint32_t waves_total = gridDim.x * kWavesPerBlock;
   const bool random_init = p.init_mode == BO_INIT_RANDOM;
   const uint32_t m_first = m - p.init_q;
 
-  for (uint64_t base = (uint64_t)blockIdx.x * kWavesPerBlock + wv; base < p.trial_count;
-       base += waves_total * tb) {
+  uint32_t hc = 0;                            // this wave's outcome counts of bins 0..63, lane = bin
+  for (uint32_t base = blockIdx.x * kWavesPerBlock + wv; base < trial_count; base += waves_total * tb) {
     if (random_init) {                       // /start (node.ts:167-188), tb trials per Philox pass
       const uint32_t s = lane / nph, bk = lane - s * nph;
-      const uint64_t t = base + (uint64_t)s * waves_total;
-      if (s < tb && t < p.trial_count) {
-        const uint64_t trial = p.trial_begin + t;
-        uint32_t kk0 = k0, kk1 = k1;
-        asm volatile("" : "+s"(kk0), "+s"(kk1));   // keep the round keys out of long-lived SGPRs
-        const uint4 r = philox4x32_10(kk0, kk1, make_uint4((uint32_t)trial, (uint32_t)(trial >> 32), bk, kStreamInit << 24));
+      const uint32_t t = base + s * waves_total;
+      if (s < tb && t < trial_count) {
+        const uint64_t trial = lds_u64(keys + 2) + t;
+        const uint2 kk = lds_keys(keys);
+        const uint4 r = philox4x32_10(kk.x, kk.y, make_uint4((uint32_t)trial, (uint32_t)(trial >> 32), bk, kStreamInit << 24));
         const uint64_t v0 = group_mask(2u * bk, m), v1 = group_mask(2u * bk + 1u, m);
         const uint64_t x1a = ((uint64_t)r.y << 32 | r.x) & v0, x1b = ((uint64_t)r.w << 32 | r.z) & v1;
         reinterpret_cast<uint4 *>(ring + s * WP)[bk] =
@@ -653,33 +683,27 @@ __global__ void __launch_bounds__(256) benor_lockstep_blocked_kernel(KParams p) 
       }
     }
     for (uint32_t s = 0; s < tb; ++s) {
-      const uint64_t t = base + (uint64_t)s * waves_total;
-      if (t >= p.trial_count) break;
-      const uint64_t trial = p.trial_begin + t;
-      const uint32_t tlo = (uint32_t)trial, thi = (uint32_t)(trial >> 32);
+      const uint32_t t = base + s * waves_total;
+      if (t >= trial_count) break;
       const uint2 *Xr = random_init ? ring + s * WP : ring;
       for (uint32_t b = 0; b < NB; ++b) D[b * 64u + lane] = 0u;
       uint32_t R = 0, M = m_first;
       bool all_dec = false;
-      for (uint32_t r = 1; r <= p.k_max; ++r) {
+      uint64_t any0 = 0, any1 = 0;            // final round's x: some live node 0 / some 1
+      for (uint32_t r = 1; r <= k_max; ++r) {
         // ---- R-phase ("proposal phase", node.ts:46-82): c1 per receiver, c0 = M - c1
-        const uint32_t hi_t = M >> 1, lo_t = (M + 1u) >> 1;
+        const bool odd = M & 1u;
 #pragma nounroll
         for (uint32_t b = 0; b < NB; ++b) {
           uint32_t a1[G];
           tally_groups_x1<G>(Xr, W, a1);
-          uint32_t st = 0;
-          Unroll<G>::run([&](auto gi) {
-            constexpr int g = decltype(gi)::value;
-            const uint64_t vm = group_mask(b * G + g, m);
-            const uint64_t p0 = ballot_s(a1[g] < lo_t + (uint32_t)g) & vm;   // node.ts:63-64
-            const uint64_t p1 = ballot_s(a1[g] > hi_t + (uint32_t)g) & vm;   // node.ts:65-66 (else "?")
-            st = stage4<g>(st, p0, p1);
-          });
+          const uint32_t st = odd ? stage_proposals<true, G>(a1, b, m, M) : stage_proposals<false, G>(a1, b, m, M);
           if (lane < 4u * G) reinterpret_cast<uint32_t *>(P + b * G)[lane] = st;
         }
         // ---- P-phase ("voting phase", node.ts:83-158)
         bool done = true;
+        any0 = 0;
+        any1 = 0;
 #pragma nounroll
         for (uint32_t b = 0; b < NB; ++b) {
           uint32_t a0[G], a1[G];
@@ -689,20 +713,26 @@ __global__ void __launch_bounds__(256) benor_lockstep_blocked_kernel(KParams p) 
             constexpr int g = decltype(gi)::value;
             const uint64_t vm = group_mask(b * G + g, m);
             const uint32_t Fg = F + (uint32_t)g;
-            const bool d0l = a0[g] > Fg, d1l = a1[g] > Fg;           // node.ts:99, :102
-            const uint64_t d0 = ballot_s(d0l) & vm;
-            const uint64_t d1 = ballot_s(d1l) & vm & ~d0;
+            const uint64_t d0 = vcmp_gt(a0[g], Fg) & vm;                 // node.ts:99
+            const uint64_t d1 = vcmp_gt(a1[g], Fg) & vm & ~d0;           // node.ts:102
             const uint64_t rest = vm & ~(d0 | d1);
             uint64_t x1 = d1;
             if (rest) {
-              const uint64_t ad1 = ballot_s(a1[g] > a0[g]) & rest;     // node.ts:108-109
-              const uint64_t tie = ballot_s(a1[g] == a0[g]) & rest;    // node.ts:110-111
+              const uint64_t ad1 = ballot_s(a1[g] > a0[g]) & rest;       // node.ts:108-109
+              const uint64_t tie = ballot_s(a1[g] == a0[g]) & rest;      // node.ts:110-111
               x1 |= ad1;
-              if (tie) x1 |= (coin_ballot(k0, k1, tlo, thi, p.live_ids, b * G + g, r, tie));   // node.ts:111
+              if (tie) {                                                // node.ts:111
+                const uint64_t trial = lds_u64(keys + 2) + t;
+                const uint32_t *ids = reinterpret_cast<const uint32_t *>((uintptr_t)lds_u64(keys + 4));
+                x1 |= coin_ballot(keys, (uint32_t)trial, (uint32_t)(trial >> 32), ids, b * G + g, r, tie);
+              }
             }
             st = writelane<2 * g>(st, (uint32_t)x1);
             st = writelane<2 * g + 1>(st, (uint32_t)(x1 >> 32));
-            dbb = (d0l || d1l) ? (dbb | (1u << g)) : dbb;
+            dbb = ((((d0 | d1) >> lane) & 1ull) != 0ull) ? (dbb | (1u << g)) : dbb;
+            any1 |= x1;
+            any0 |= vm & ~x1;
+            asm volatile("" : "+s"(any0), "+s"(any1));                   // fold per group
           });
           D[b * 64u + lane] = dbb;
           if (lane < 2u * G) reinterpret_cast<uint32_t *>(X + b * G)[lane] = st;
@@ -723,39 +753,34 @@ __global__ void __launch_bounds__(256) benor_lockstep_blocked_kernel(KParams p) 
         if (all_dec) break;
       }
       // ---- outcome
-      bool any0 = false, any1 = false;
-      if (lane < W) {
-        const uint2 q = Xr[lane];
-        const uint64_t x1 = (uint64_t)q.y << 32 | q.x;
-        any1 = x1 != 0ull;
-        any0 = (group_mask(lane, m) & ~x1) != 0ull;
-      }
-      const bool g0 = __any(any0), g1 = __any(any1);
-      const uint32_t v = (g0 && g1) ? 2u : (g1 ? 1u : 0u);
-      if (lane == 0) {
-        atomicAdd(&lhist[all_dec ? (R * 3u + v) : v], 1u);
-        if (all_dec && v == 2u) atomicAdd(&lhist[p.hist_len - 1u], 1u);
-        if (p.rounds_out) *p.rounds_out = all_dec ? R : 0u;
-      }
-      if (p.node_out) {
-        for (uint32_t c = lane; c < m; c += 64u) {
-          const uint32_t j = c >> 6;
-          const uint2 q = Xr[j];
-          const uint64_t x1 = (uint64_t)q.y << 32 | q.x;
-          bo_node_state ns;
-          ns.killed = 0;
-          ns.x = (int8_t)((x1 >> lane) & 1ull);
-          ns.decided = (int8_t)((D[(j / G) * 64u + lane] >> (j % G)) & 1u);
-          ns.pad = 0;
-          ns.k = (int32_t)R + 1;
-          p.node_out[p.live_ids[c]] = ns;
+      const uint32_t v = (any0 && any1) ? 2u : (any1 ? 1u : 0u);
+      const uint32_t bin = all_dec ? (R * 3u + v) : v;
+      if (bin < 64u) hc += (lane == bin) ? 1u : 0u;
+      else if (lane == 0) atomicAdd(&lhist[bin], 1u);
+      if (all_dec && v == 2u && lane == 0) atomicAdd(&lhist[hist_len - 1u], 1u);
+      if constexpr (STATE) {
+        if (lane == 0 && p.rounds_out) *p.rounds_out = all_dec ? R : 0u;
+        if (p.node_out) {
+          for (uint32_t c = lane; c < m; c += 64u) {
+            const uint32_t j = c >> 6;
+            const uint2 q = Xr[j];
+            const uint64_t x1 = (uint64_t)q.y << 32 | q.x;
+            bo_node_state ns;
+            ns.killed = 0;
+            ns.x = (int8_t)((x1 >> lane) & 1ull);
+            ns.decided = (int8_t)((D[(j / G) * 64u + lane] >> (j % G)) & 1u);
+            ns.pad = 0;
+            ns.k = (int32_t)R + 1;
+            p.node_out[p.live_ids[c]] = ns;
+          }
         }
       }
     }
   }
 
+  if (hc) atomicAdd(&lhist[lane], hc);
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < p.hist_len; i += blockDim.x) {
+  for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) {
     const uint32_t c = lhist[i];
     if (c) atomicAdd(&p.hist[i], (unsigned long long)c);
   }
@@ -1400,7 +1425,10 @@ static hipError_t launch_w(const KParams &p, int grid, hipStream_t s) {
 
 template <int G>
 static hipError_t launch_b(const KParams &p, int grid, hipStream_t s) {
-  hipLaunchKernelGGL(benor_lockstep_blocked_kernel<G>, dim3(grid), dim3(64 * kWavesPerBlock), p.lds_bytes, s, p);
+  if (p.node_out || p.rounds_out)
+    hipLaunchKernelGGL((benor_lockstep_blocked_kernel<G, true>), dim3(grid), dim3(64 * kWavesPerBlock), p.lds_bytes, s, p);
+  else
+    hipLaunchKernelGGL((benor_lockstep_blocked_kernel<G, false>), dim3(grid), dim3(64 * kWavesPerBlock), p.lds_bytes, s, p);
   return hipGetLastError();
 }
 
