@@ -49,6 +49,10 @@ def test_golden_histograms(oracle_vectors):
     (70, 2, 20_000, 32), (128, 0, 20_000, 32), (256, 85, 20_000, 16), (1024, 341, 5_000, 16),
     (1088, 0, 500, 32), (1100, 40, 1_000, 32), (2047, 0, 200, 32), (4096, 0, 100, 16), (4096, 2047, 100, 16),
     (3, 1, 10_000, 8), (1, 0, 1000, 4), (2, 1, 1000, 4), (33, 16, 5000, 16),
+    # even m at W = 5, 8, 16: multi-round trials through the fused next-round R-phase
+    (300, 0, 4000, 24), (600, 100, 3000, 24), (1024, 0, 2000, 24),
+    # m <= F, W = 1, 2, 8: never decide, every trial runs to k_max
+    (100, 50, 2000, 12), (200, 100, 1000, 12), (1000, 500, 100, 12),
 ])
 def test_random_batches_match_oracle(N, F, trials, k_max):
     seed = 0x9E3779B97F4A7C15 ^ (N * 7919 + F)
