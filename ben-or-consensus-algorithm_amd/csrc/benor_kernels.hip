@@ -316,14 +316,55 @@ __device__ __forceinline__ void p_phase(const uint32_t (&c1r)[W], uint32_t M, ui
   });
 }
 
+// Round 1 of K trials at once (small W): the same phase as p_phase for K
+// independent trials, interleaved sender group by sender group so that one
+// trial's compares and tallies fill the other's dependency stalls.
+template <bool ODD, int W, int K>
+__device__ __forceinline__ void p_phase_k(const uint32_t (&c1r)[K][W], uint32_t M, uint64_t tailm,
+                                          uint32_t (&a0)[K][W], uint32_t (&a1)[K][W]) {
+  const uint32_t hi_t = M >> 1, lo_t = (M + 1u) >> 1;
+  Unroll<W>::run([&](auto wi) {
+    constexpr int w = decltype(wi)::value;
+    const uint64_t vm = (w == W - 1) ? tailm : ~0ull;
+    Unroll<K>::run([&](auto ki) {
+      constexpr int k = decltype(ki)::value;
+      const uint64_t p1 = vcmp_gt(c1r[k][w], hi_t + (uint32_t)w) & vm;         // node.ts:65-66
+      const uint64_t p0 = ODD ? (vm & ~p1) : (vcmp_lt(c1r[k][w], lo_t + (uint32_t)w) & vm);   // node.ts:63-64
+      const uint32_t l0 = (uint32_t)p0, h0 = (uint32_t)(p0 >> 32);
+      const uint32_t l1 = (uint32_t)p1, h1 = (uint32_t)(p1 >> 32);
+      if constexpr (w == 0) {
+        Unroll<W>::run([&](auto gi) {
+          constexpr int g = decltype(gi)::value;
+          a0[k][g] = tally_first_s<g>(l0);
+          a1[k][g] = tally_first_s<g>(l1);
+        });
+      } else {
+#pragma unroll
+        for (int g = 0; g < W; ++g) {
+          a0[k][g] = tally_s(l0, a0[k][g]);
+          a1[k][g] = tally_s(l1, a1[k][g]);
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < W; ++g) {
+        a0[k][g] = tally_s(h0, a0[k][g]);
+        a1[k][g] = tally_s(h1, a1[k][g]);
+      }
+    });
+  });
+}
+
 // STATE: the network API's single-trial launch that also reports per-node
 // state and the halting round (GET /getState); the batch path is compiled
 // without that code, which keeps its register allocation free of it.
+constexpr int kPairMaxW = 8;               // W kernel: pair trials' round 1 up to this W
+
 template <int W, bool STATE>
 __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
   constexpr int NPH = (W + 1) / 2;          // Philox blocks per trial (2 plane words each)
   constexpr int TB = 64 / NPH;              // trials per init batch
   constexpr int WP = 2 * NPH;               // x1 words per plane row, padded to 16 bytes
+  constexpr int K = W <= 2 ? 4 : (W <= kPairMaxW ? 2 : 1);   // trials whose round 1 runs interleaved
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // uniform: scalar trial loop
@@ -380,9 +421,17 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
             make_uint4((uint32_t)x1a, (uint32_t)(x1a >> 32), (uint32_t)x1b, (uint32_t)(x1b >> 32));
       }
     }
-    for (int s = 0; s < TB; ++s) {
-      const uint32_t t = base + (uint32_t)s * waves_total;
-      if (t >= trial_count) break;
+    // One trial's outcome: bins 0..63 (undecided, and halting rounds <= 20) in
+    // lane `bin` of the wave's counter (one VALU op), the rest as LDS atomics.
+    auto record = [&](uint64_t any0, uint64_t any1, uint32_t R, bool all_dec) {
+      const uint32_t v = (any0 && any1) ? 2u : (any1 ? 1u : 0u);
+      const uint32_t bin = all_dec ? (R * 3u + v) : v;
+      if (bin < 64u) hc += (lane == bin) ? 1u : 0u;
+      else if (lane == 0) atomicAdd(&lhist[bin], 1u);
+      if (all_dec && v == 2u && lane == 0) atomicAdd(&lhist[hist_len - 1u], 1u);
+    };
+    // One whole trial, round after round.
+    auto single = [&](int s, uint32_t t) {
       // ---- round-1 R-phase tallies over the /start broadcast (node.ts:167-188)
       uint32_t c1r[W];
       tally_x1<W>(random_init ? ring + s * WP : ring, c1r);
@@ -487,13 +536,7 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
         if (all_dec || !more) break;
       }
       // ---- outcome
-      const uint32_t v = (any0 && any1) ? 2u : (any1 ? 1u : 0u);
-      const uint32_t bin = all_dec ? (R * 3u + v) : v;
-      // bins 0..63 (undecided, and halting rounds <= 20): lane `bin` of the
-      // wave's counter, one VALU op; the rest: an LDS atomic
-      if (bin < 64u) hc += (lane == bin) ? 1u : 0u;
-      else if (lane == 0) atomicAdd(&lhist[bin], 1u);
-      if (all_dec && v == 2u && lane == 0) atomicAdd(&lhist[hist_len - 1u], 1u);
+      record(any0, any1, R, all_dec);
       if constexpr (STATE) {
         uint32_t *rounds_out = p.rounds_out;
         if (lane == 0 && rounds_out) *rounds_out = all_dec ? R : 0u;
@@ -515,6 +558,53 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
           }
         });
       }
+    };
+    for (int s = 0; s < TB;) {
+      const uint32_t t = base + (uint32_t)s * waves_total;
+      if (t >= trial_count) break;
+      uint32_t slow = 1u, nk = 1u;              // trials (bit k: s + k) to run alone; trials consumed
+      if constexpr (K > 1 && !STATE) {
+        if (s + K - 1 < TB && t + (uint32_t)(K - 1) * waves_total < trial_count) {
+          // ---- round 1 of K trials interleaved; a trial that does not halt in
+          // round 1 (some receiver undecided) is re-run alone from round 1.
+          uint32_t c1[K][W], a0[K][W], a1[K][W];
+          Unroll<K>::run([&](auto ki) {
+            constexpr int k = decltype(ki)::value;
+            tally_x1<W>(random_init ? ring + (s + k) * WP : ring, c1[k]);
+          });
+          if (m_first & 1u) p_phase_k<true, W, K>(c1, m_first, tailm, a0, a1);
+          else p_phase_k<false, W, K>(c1, m_first, tailm, a0, a1);
+          uint64_t rest_any[K], any0[K], any1[K];
+#pragma unroll
+          for (int k = 0; k < K; ++k) rest_any[k] = any0[k] = any1[k] = 0;
+          Unroll<W>::run([&](auto gi) {
+            constexpr int g = decltype(gi)::value;
+            const uint64_t vm = (g == W - 1) ? tailm : ~0ull;
+            const uint32_t Fg = F + (uint32_t)g;
+            Unroll<K>::run([&](auto ki) {
+              constexpr int k = decltype(ki)::value;
+              const uint64_t d0 = vcmp_gt(a0[k][g], Fg) & vm;             // node.ts:99
+              const uint64_t d1 = vcmp_gt(a1[k][g], Fg) & vm & ~d0;       // node.ts:102
+              rest_any[k] |= vm & ~(d0 | d1);
+              any0[k] |= d0;
+              any1[k] |= d1;
+              asm volatile("" : "+s"(rest_any[k]), "+s"(any0[k]), "+s"(any1[k]));
+            });
+          });
+          slow = 0u;
+          nk = K;
+          Unroll<K>::run([&](auto ki) {
+            constexpr int k = decltype(ki)::value;
+            if (!rest_any[k]) record(any0[k], any1[k], 1u, true);
+            else slow |= 1u << k;
+          });
+        }
+      }
+      for (; slow; slow &= slow - 1u) {         // one call site: the whole-trial loop is inlined once
+        const uint32_t k = (uint32_t)__builtin_ctz(slow);
+        single(s + (int)k, t + k * waves_total);
+      }
+      s += (int)nk;
     }
   }
 

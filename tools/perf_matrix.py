@@ -32,7 +32,9 @@ SHAPES = [
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--shapes", default=None, help="'N,F,f,mode,trials;...' instead of the built-in list")
     a = ap.parse_args()
+    shapes = SHAPES if not a.shapes else [tuple(int(x) for x in t.split(",")) for t in a.shapes.split(";")]
     import numpy as np
     import torch
 
@@ -40,7 +42,7 @@ def main():
 
     torch.cuda.set_device(0)
     stream = torch.cuda.current_stream()
-    for (N, F, f, mode, trials) in SHAPES:
+    for (N, F, f, mode, trials) in shapes:
         if a.quick:
             trials = max(1, trials // 10)
         plan = benor.TrialsPlan(N, F, [i < f for i in range(N)], seed=0x1234 + N, k_max=32, mode=mode)

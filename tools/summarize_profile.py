@@ -67,12 +67,15 @@ def main(tag, trials, N=1024, F=341):
     if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
         hbm = (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0
         lines.append(f"- HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, KiB -> B): {hbm:.0f}")
-        json.dump({"N": N, "F": F, "trials": trials, "hbm_bytes_per_launch": hbm,
-                   "fetch_kib": c["FETCH_SIZE"], "write_kib": c["WRITE_SIZE"], "source": f"profiles/{tag}_summary.md"},
-                  open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
+        if (N, F) == (1024, 341):   # bench.py reads the bench shape's traffic only
+            json.dump({"N": N, "F": F, "trials": trials, "hbm_bytes_per_launch": hbm,
+                       "fetch_kib": c["FETCH_SIZE"], "write_kib": c["WRITE_SIZE"],
+                       "source": f"profiles/{tag}_summary.md"},
+                      open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
     open(os.path.join(dst, f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 10_000_000)
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 10_000_000,
+         *(int(x) for x in sys.argv[3:5]))
