@@ -12,9 +12,11 @@ of the GPU count.
 value  = live node-rounds simulated by all ranks / timed seconds (max over ranks)
          (a live node-round = one live node executing one R-phase and one
          P-phase: SURVEY §8d primary count)
-roofline: per-receiver tally popcount words (4 * ceil(m/32) per live
-         node-round, m = N - F live nodes) / average kernel duration, against
-         the gfx950 VALU popcount peak (256 CU x 4 SIMD x 32 lanes x 2.4 GHz).
+roofline: per-receiver tally popcount words (3 * ceil(m/32) per live
+         node-round, m = N - F live nodes: c1 in the R-phase, c0 and c1 in the
+         P-phase) / average kernel duration from HIP events on the
+         launch stream, against the gfx950 v_bcnt_u32_b32 issue peak
+         (256 CU x 4 SIMD x 16 lanes x 2.4 GHz = 39.3 T words/s).
 cpu_baseline: the oracle's bit-plane restatement (oracle/benor_oracle.c,
          OpenMP over trials) on a bounded sample, rank 0 at N = 1 only.
 
@@ -33,7 +35,7 @@ sys.path.insert(0, PKG)
 
 METRIC = "simulated node-rounds/sec at N=1024,F=341, 1–8 GPUs; % of INT/popcount roofline"
 # v_bcnt_u32_b32 issues one wave64 instruction per 4 cycles per SIMD (16 lanes/clk;
-# tools/valu_probe.hip, profiles/r01-v1_valu_probe.txt: 4.15 cyc at full occupancy,
+# tools/valu_probe.hip, profiles/r01-v8_valu_probe.txt: 4.15-4.2 cyc at full occupancy,
 # vs 2.4-2.5 for v_and_b32 / v_add_u32), so the popcount roofline of the chip is
 # 256 CU x 4 SIMD x 16 lanes x 2.4 GHz.
 SPEC_PEAK_POPC = 256 * 4 * 16 * 2.4e9
