@@ -1063,6 +1063,15 @@ struct DStream {
   }
 };
 
+// One Floyd step: sender t, else (t already in the subset) sender jj, joins
+// the lane's bitset ([word][lane] in LDS).  ds_or: LDS ops of a wave retire
+// in order, so the next step's read sees this one.
+__device__ __forceinline__ void floyd_insert(uint32_t *__restrict__ B, uint32_t lane, uint32_t t, uint32_t jj) {
+  const uint32_t cur = B[(t >> 5) * 64u + lane];
+  const uint32_t idx = ((cur >> (t & 31u)) & 1u) ? jj : t;
+  atomicOr(&B[(idx >> 5) * 64u + lane], 1u << (idx & 31u));
+}
+
 __device__ __forceinline__ void random_tally(const uint4 *__restrict__ plane, uint32_t *__restrict__ B,
                                              uint32_t W, uint32_t m, uint32_t q, bool active, uint32_t k0,
                                              uint32_t k1, uint32_t tlo, uint32_t thi, uint32_t node, uint32_t r,
@@ -1071,16 +1080,45 @@ __device__ __forceinline__ void random_tally(const uint4 *__restrict__ plane, ui
   const uint32_t e = m - q;
   const bool deliver_T = q <= e;
   const uint32_t k = deliver_T ? q : e;
-  if (active && k) {
-    DStream ds;
-    ds.k0 = k0; ds.k1 = k1; ds.c0 = tlo; ds.c1 = thi; ds.c2 = node & 0xFFFu;
-    ds.c3 = (r & 0xFFFFFu) | ((phase & 1u) << 20) | (kStreamDelivery << 24);
-    ds.widx = 0;
-    for (uint32_t jj = m - k; jj < m; ++jj) {                    // Floyd: uniform k-subset of [0, m)
+  // Floyd over [0, m): for jj = m-k .. m-1, t = uniform(jj + 1) (Lemire, exact).
+  // Words come from Philox stream 2 in order (DStream above: word i is element
+  // i & 3 of block i >> 2).  Fast path: one block = 4 draws, taken while the
+  // lane's stream position is block-aligned and none of the 4 products needs
+  // Lemire's exact rejection test; otherwise one exact DStream step (same
+  // words, same result -- the oracle's definition).
+  const uint32_t c2 = node & 0xFFFu, c3 = (r & 0xFFFFFu) | ((phase & 1u) << 20) | (kStreamDelivery << 24);
+  uint32_t jj = m - k, widx = 0;
+  for (;;) {
+    const bool go = active && jj < m;
+    if (!__any(go)) break;
+    bool fast = go && (widx & 3u) == 0u;
+    if (fast) {
+      const uint4 b = philox4x32_10(k0, k1, make_uint4(tlo, thi, c2 | ((widx >> 2) << 12), c3));
+      const uint32_t n = m - jj < 4u ? m - jj : 4u;            // draws left in this subset
+      const uint64_t q0 = (uint64_t)b.x * (jj + 1u), q1 = (uint64_t)b.y * (jj + 2u);
+      const uint64_t q2 = (uint64_t)b.z * (jj + 3u), q3 = (uint64_t)b.w * (jj + 4u);
+      const bool rej = (uint32_t)q0 < jj + 1u || (n > 1u && (uint32_t)q1 < jj + 2u) ||
+                       (n > 2u && (uint32_t)q2 < jj + 3u) || (n > 3u && (uint32_t)q3 < jj + 4u);
+      if (!rej) {
+        floyd_insert(B, lane, (uint32_t)(q0 >> 32), jj);
+        if (n > 1u) floyd_insert(B, lane, (uint32_t)(q1 >> 32), jj + 1u);
+        if (n > 2u) floyd_insert(B, lane, (uint32_t)(q2 >> 32), jj + 2u);
+        if (n > 3u) floyd_insert(B, lane, (uint32_t)(q3 >> 32), jj + 3u);
+        jj += n;
+        widx += n;
+      } else {
+        fast = false;
+      }
+    }
+    if (go && !fast) {
+      DStream ds;
+      ds.k0 = k0; ds.k1 = k1; ds.c0 = tlo; ds.c1 = thi; ds.c2 = c2; ds.c3 = c3;
+      ds.widx = widx & ~3u;                                      // refill the current block, then skip to widx
+      for (uint32_t i = ds.widx; i < widx; ++i) (void)ds.next();
       const uint32_t t = ds.uniform(jj + 1u);
-      const uint32_t cur = B[(t >> 5) * 64u + lane];
-      const uint32_t idx = ((cur >> (t & 31u)) & 1u) ? jj : t;
-      B[(idx >> 5) * 64u + lane] |= 1u << (idx & 31u);
+      floyd_insert(B, lane, t, jj);
+      widx = ds.widx;
+      ++jj;
     }
   }
   uint32_t a0 = 0, a1 = 0;
