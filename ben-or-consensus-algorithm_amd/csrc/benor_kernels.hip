@@ -245,6 +245,15 @@ __device__ __forceinline__ uint32_t sgpr32(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
 }
 
+// Per-lane select by a wave lane mask: lanes whose bit is set take `b`
+// (one v_cndmask_b32 with an SGPR mask; a C select would shift the mask by
+// the lane id in 64-bit VALU ops).
+__device__ __forceinline__ uint32_t select_lanes(uint32_t a, uint32_t b, uint64_t mask) {
+  uint32_t r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(mask));
+  return r;
+}
+
 // Opaque wave compares (v_cmp -> SGPR lane mask).  asm volatile so that the
 // compiler neither merges the decision pass's compares with the adopt pass's
 // recomputation of them (which would keep 2W masks live across the pass and
@@ -819,7 +828,7 @@ __global__ void __launch_bounds__(256) benor_lockstep_blocked_kernel(KParams p) 
             }
             st = writelane<2 * g>(st, (uint32_t)x1);
             st = writelane<2 * g + 1>(st, (uint32_t)(x1 >> 32));
-            dbb = ((((d0 | d1) >> lane) & 1ull) != 0ull) ? (dbb | (1u << g)) : dbb;
+            dbb = select_lanes(dbb, dbb | (1u << g), d0 | d1);           // sticky decided bit (node.ts:100-105)
             any1 |= x1;
             any0 |= vm & ~x1;
             asm volatile("" : "+s"(any0), "+s"(any1));                   // fold per group

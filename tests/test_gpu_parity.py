@@ -148,6 +148,22 @@ def test_full_size_sharding_invariance_and_law():
     np.testing.assert_array_equal(plan.run(1_999_000, 1000), ref.hist)
 
 
+def test_launch_split_past_2_31_trials():
+    """The host splits launches at 2^31 trials (the kernels index trials within
+    a launch in 32 bits): a 2^31 + 3000-trial run loses no trial, its last
+    3000 trials equal a separate launch of that range, and m = 39 (odd) halts
+    every trial in round 1 with a Bernoulli(1/2) value."""
+    N, F, k = 40, 1, 8
+    plan = benor.TrialsPlan(N, F, first_f(N, F), seed=77, k_max=k)
+    T = (1 << 31) + 3000
+    h = plan.run(5, T)
+    assert h.sum() == T and h[3] + h[4] == T
+    assert analytic.chi2_pvalue(h[:-1], analytic.hist_probs(N, F, k)) > 1e-3
+    tail = plan.run(5 + (1 << 31), 3000)
+    ref = oracle.run_trials(N, F, first_f(N, F), seed=77, trial_begin=5 + (1 << 31), trial_count=3000, k_max=k)
+    np.testing.assert_array_equal(tail, ref.hist)
+
+
 @pytest.mark.parametrize("N,F,k_max", [(10, 4, 24), (10, 5, 11), (64, 0, 32), (100, 30, 32)])
 def test_analytic_law_1e6(N, F, k_max):
     plan = benor.TrialsPlan(N, F, first_f(N, F), seed=0xA11CE + N, k_max=k_max)
