@@ -53,6 +53,8 @@ def test_golden_histograms(oracle_vectors):
     (300, 0, 4000, 24), (600, 100, 3000, 24), (1024, 0, 2000, 24),
     # m <= F, W = 1, 2, 8: never decide, every trial runs to k_max
     (100, 50, 2000, 12), (200, 100, 1000, 12), (1000, 500, 100, 12),
+    # k_max = BO_MAX_K: histogram of 3076 bins (bins >= 64 through LDS atomics)
+    (10, 5, 500, 1024), (130, 65, 100, 1024), (2, 0, 20000, 1024), (70, 4, 3000, 1024),
 ])
 def test_random_batches_match_oracle(N, F, trials, k_max):
     seed = 0x9E3779B97F4A7C15 ^ (N * 7919 + F)
