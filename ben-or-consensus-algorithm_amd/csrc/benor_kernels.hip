@@ -289,45 +289,17 @@ __device__ __forceinline__ uint32_t stage4(uint32_t v, uint64_t is0, uint64_t is
 }
 
 // One round's R-phase proposals (node.ts:63-69, from each receiver's c1 and the
-// vote count M) fused with the P-phase tallies (node.ts:92-98): sender group
-// w's proposal masks are added to every receiver group's counts as soon as
-// they exist, so only one group's proposal planes (two SGPR pairs) is live.
-template <bool ODD, int W>
-__device__ __forceinline__ void p_phase(const uint32_t (&c1r)[W], uint32_t M, uint64_t tailm, uint32_t (&a0)[W],
-                                        uint32_t (&a1)[W]) {
-  const uint32_t hi_t = M >> 1, lo_t = (M + 1u) >> 1;
-  Unroll<W>::run([&](auto wi) {
-    constexpr int w = decltype(wi)::value;
-    const uint64_t vm = (w == W - 1) ? tailm : ~0ull;
-    const uint64_t p1 = vcmp_gt(c1r[w], hi_t + (uint32_t)w) & vm;         // c1 > c0  (node.ts:65-66)
-    const uint64_t p0 = ODD ? (vm & ~p1)                                   // c0 > c1  (node.ts:63-64)
-                            : (vcmp_lt(c1r[w], lo_t + (uint32_t)w) & vm);  // else "?"
-    const uint32_t l0 = (uint32_t)p0, h0 = (uint32_t)(p0 >> 32);
-    const uint32_t l1 = (uint32_t)p1, h1 = (uint32_t)(p1 >> 32);
-    if constexpr (w == 0) {
-      Unroll<W>::run([&](auto gi) {
-        constexpr int g = decltype(gi)::value;
-        a0[g] = tally_first_s<g>(l0);
-        a1[g] = tally_first_s<g>(l1);
-      });
-    } else {
-#pragma unroll
-      for (int g = 0; g < W; ++g) {
-        a0[g] = tally_s(l0, a0[g]);
-        a1[g] = tally_s(l1, a1[g]);
-      }
-    }
-#pragma unroll
-    for (int g = 0; g < W; ++g) {
-      a0[g] = tally_s(h0, a0[g]);
-      a1[g] = tally_s(h1, a1[g]);
-    }
-  });
-}
-
-// Round 1 of K trials at once (small W): the same phase as p_phase for K
-// independent trials, interleaved sender group by sender group so that one
-// trial's compares and tallies fill the other's dependency stalls.
+// binary vote count M) fused with the P-phase tallies (node.ts:92-98), for K
+// independent trials at once (K > 1: small W, interleaved sender group by
+// sender group so one trial's compares and tallies fill the other's
+// dependency stalls).  Sender group w's proposal masks are added to every
+// receiver group's counts as soon as they exist, so only one group's
+// proposal planes (SGPR pairs) is live.
+//
+// ODD (M odd): c0 == c1 is impossible in the R-phase, so "c0 > c1" is the
+// complement of "c1 > c0" (one compare) and no proposal is "?".  Every
+// P-phase vote is then 0 or 1, so a receiver's c0 = m - c1 and only the c1
+// tally is made (a0 is left unset; decide_k / the adopt pass derive it).
 template <bool ODD, int W, int K>
 __device__ __forceinline__ void p_phase_k(const uint32_t (&c1r)[K][W], uint32_t M, uint64_t tailm,
                                           uint32_t (&a0)[K][W], uint32_t (&a1)[K][W]) {
@@ -337,28 +309,61 @@ __device__ __forceinline__ void p_phase_k(const uint32_t (&c1r)[K][W], uint32_t 
     const uint64_t vm = (w == W - 1) ? tailm : ~0ull;
     Unroll<K>::run([&](auto ki) {
       constexpr int k = decltype(ki)::value;
-      const uint64_t p1 = vcmp_gt(c1r[k][w], hi_t + (uint32_t)w) & vm;         // node.ts:65-66
-      const uint64_t p0 = ODD ? (vm & ~p1) : (vcmp_lt(c1r[k][w], lo_t + (uint32_t)w) & vm);   // node.ts:63-64
-      const uint32_t l0 = (uint32_t)p0, h0 = (uint32_t)(p0 >> 32);
+      const uint64_t p1 = vcmp_gt(c1r[k][w], hi_t + (uint32_t)w) & vm;         // c1 > c0  (node.ts:65-66)
       const uint32_t l1 = (uint32_t)p1, h1 = (uint32_t)(p1 >> 32);
+      if constexpr (!ODD) {
+        const uint64_t p0 = vcmp_lt(c1r[k][w], lo_t + (uint32_t)w) & vm;       // c0 > c1  (node.ts:63-64), else "?"
+        const uint32_t l0 = (uint32_t)p0, h0 = (uint32_t)(p0 >> 32);
+        if constexpr (w == 0) {
+          Unroll<W>::run([&](auto gi) {
+            constexpr int g = decltype(gi)::value;
+            a0[k][g] = tally_first_s<g>(l0);
+          });
+        } else {
+#pragma unroll
+          for (int g = 0; g < W; ++g) a0[k][g] = tally_s(l0, a0[k][g]);
+        }
+#pragma unroll
+        for (int g = 0; g < W; ++g) a0[k][g] = tally_s(h0, a0[k][g]);
+      }
       if constexpr (w == 0) {
         Unroll<W>::run([&](auto gi) {
           constexpr int g = decltype(gi)::value;
-          a0[k][g] = tally_first_s<g>(l0);
           a1[k][g] = tally_first_s<g>(l1);
         });
       } else {
 #pragma unroll
-        for (int g = 0; g < W; ++g) {
-          a0[k][g] = tally_s(l0, a0[k][g]);
-          a1[k][g] = tally_s(l1, a1[k][g]);
-        }
+        for (int g = 0; g < W; ++g) a1[k][g] = tally_s(l1, a1[k][g]);
       }
 #pragma unroll
-      for (int g = 0; g < W; ++g) {
-        a0[k][g] = tally_s(h0, a0[k][g]);
-        a1[k][g] = tally_s(h1, a1[k][g]);
-      }
+      for (int g = 0; g < W; ++g) a1[k][g] = tally_s(h1, a1[k][g]);
+    });
+  });
+}
+
+// Decisions (node.ts:99-105) of K trials: whether some live receiver stays
+// undecided, and which values were decided.  ODD: c0 = m - c1, so
+// "c0 > F" is "c1 < m - F" (no c0 tally exists).  Chain bias g throughout.
+template <bool ODD, int W, int K>
+__device__ __forceinline__ void decide_k(const uint32_t (&a0)[K][W], const uint32_t (&a1)[K][W], uint32_t m,
+                                         uint32_t F, uint64_t tailm, uint64_t (&rest_any)[K], uint64_t (&any0)[K],
+                                         uint64_t (&any1)[K]) {
+  const uint32_t mF = m > F ? m - F : 0u;
+#pragma unroll
+  for (int k = 0; k < K; ++k) rest_any[k] = any0[k] = any1[k] = 0;
+  Unroll<W>::run([&](auto gi) {
+    constexpr int g = decltype(gi)::value;
+    const uint64_t vm = (g == W - 1) ? tailm : ~0ull;
+    Unroll<K>::run([&](auto ki) {
+      constexpr int k = decltype(ki)::value;
+      const uint64_t d0 = (ODD ? vcmp_lt(a1[k][g], mF + (uint32_t)g)           // node.ts:99
+                               : vcmp_gt(a0[k][g], F + (uint32_t)g)) & vm;
+      const uint64_t d1 = vcmp_gt(a1[k][g], F + (uint32_t)g) & vm & ~d0;      // node.ts:102
+      rest_any[k] |= vm & ~(d0 | d1);
+      any0[k] |= d0;
+      any1[k] |= d1;
+      // fold now: otherwise the ORs sink to the loop exit and all 2W masks stay live
+      asm volatile("" : "+s"(rest_any[k]), "+s"(any0[k]), "+s"(any1[k]));
     });
   });
 }
@@ -453,29 +458,24 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
         // odd number M of binary votes c0 == c1 is impossible, so "c0 > c1" is the
         // complement of "c1 > c0" and costs no second compare (ODD: one copy of the
         // phase per parity, no branch inside it).
-        uint32_t a0[W], a1[W];
-        if (M & 1u) p_phase<true, W>(c1r, M, tailm, a0, a1);
-        else p_phase<false, W>(c1r, M, tailm, a0, a1);
+        uint32_t a0[1][W], a1[1][W];
+        uint64_t rest_any[1], any0_[1], any1_[1];
+        auto& c1v = reinterpret_cast<uint32_t(&)[1][W]>(c1r);
+        const bool odd = M & 1u;
+        if (odd) {
+          p_phase_k<true, W, 1>(c1v, M, tailm, a0, a1);
+          decide_k<true, W, 1>(a0, a1, m, F, tailm, rest_any, any0_, any1_);
+        } else {
+          p_phase_k<false, W, 1>(c1v, M, tailm, a0, a1);
+          decide_k<false, W, 1>(a0, a1, m, F, tailm, rest_any, any0_, any1_);
+        }
         R = r;                                                        // node.ts:147  k = r + 1
-        // ---- decisions (node.ts:99-105).  When every live receiver decides in this
-        // round the trial halts (decided is sticky) and x = the decided value, so
-        // neither the adopt/coin branch nor the next round's planes are needed.
-        uint64_t rest_any = 0;
-        any0 = 0;
-        any1 = 0;
-        Unroll<W>::run([&](auto gi) {
-          constexpr int g = decltype(gi)::value;
-          const uint64_t vm = (g == W - 1) ? tailm : ~0ull;
-          const uint32_t Fg = F + (uint32_t)g;                          // chain bias g
-          const uint64_t d0 = vcmp_gt(a0[g], Fg) & vm;                   // node.ts:99
-          const uint64_t d1 = vcmp_gt(a1[g], Fg) & vm & ~d0;             // node.ts:102
-          rest_any |= vm & ~(d0 | d1);
-          any0 |= d0;
-          any1 |= d1;
-          // fold now: otherwise the ORs sink to the loop exit and all 2W masks stay live
-          asm volatile("" : "+s"(rest_any), "+s"(any0), "+s"(any1));
-        });
-        if (!rest_any && !STATE) {
+        any0 = any0_[0];
+        any1 = any1_[0];
+        // ---- when every live receiver decides in this round the trial halts
+        // (decided is sticky) and x = the decided value, so neither the
+        // adopt/coin branch nor the next round's planes are needed.
+        if (!rest_any[0] && !STATE) {
           all_dec = true;                                             // all-decided auto-stop
           break;
         }
@@ -491,13 +491,16 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
           constexpr int g = decltype(gi)::value;
           const uint64_t vm = (g == W - 1) ? tailm : ~0ull;
           const uint32_t Fg = F + (uint32_t)g;
-          const uint64_t d0 = vcmp_gt(a0[g], Fg) & vm;
-          const uint64_t d1 = vcmp_gt(a1[g], Fg) & vm & ~d0;
+          // ODD round: no c0 tally was made; c0 = m - c1 (all votes binary), bias g
+          const uint32_t a0g = odd ? (m + 2u * (uint32_t)g) - a1[0][g] : a0[0][g];
+          const uint32_t a1g = a1[0][g];
+          const uint64_t d0 = vcmp_gt(a0g, Fg) & vm;
+          const uint64_t d1 = vcmp_gt(a1g, Fg) & vm & ~d0;
           const uint64_t rest = vm & ~(d0 | d1);
           uint64_t x1 = d1;
           if (rest) {
-            const uint64_t ad1 = ballot_s(a1[g] > a0[g]) & rest;         // node.ts:108-109
-            const uint64_t tie = ballot_s(a1[g] == a0[g]) & rest;        // node.ts:110-111
+            const uint64_t ad1 = ballot_s(a1g > a0g) & rest;             // node.ts:108-109
+            const uint64_t tie = ballot_s(a1g == a0g) & rest;            // node.ts:110-111
             x1 |= ad1;
             if (tie) {                                                  // node.ts:111
               const uint64_t trial = lds_u64(keys + 2) + t;
@@ -581,25 +584,14 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
             constexpr int k = decltype(ki)::value;
             tally_x1<W>(random_init ? ring + (s + k) * WP : ring, c1[k]);
           });
-          if (m_first & 1u) p_phase_k<true, W, K>(c1, m_first, tailm, a0, a1);
-          else p_phase_k<false, W, K>(c1, m_first, tailm, a0, a1);
           uint64_t rest_any[K], any0[K], any1[K];
-#pragma unroll
-          for (int k = 0; k < K; ++k) rest_any[k] = any0[k] = any1[k] = 0;
-          Unroll<W>::run([&](auto gi) {
-            constexpr int g = decltype(gi)::value;
-            const uint64_t vm = (g == W - 1) ? tailm : ~0ull;
-            const uint32_t Fg = F + (uint32_t)g;
-            Unroll<K>::run([&](auto ki) {
-              constexpr int k = decltype(ki)::value;
-              const uint64_t d0 = vcmp_gt(a0[k][g], Fg) & vm;             // node.ts:99
-              const uint64_t d1 = vcmp_gt(a1[k][g], Fg) & vm & ~d0;       // node.ts:102
-              rest_any[k] |= vm & ~(d0 | d1);
-              any0[k] |= d0;
-              any1[k] |= d1;
-              asm volatile("" : "+s"(rest_any[k]), "+s"(any0[k]), "+s"(any1[k]));
-            });
-          });
+          if (m_first & 1u) {
+            p_phase_k<true, W, K>(c1, m_first, tailm, a0, a1);
+            decide_k<true, W, K>(a0, a1, m, F, tailm, rest_any, any0, any1);
+          } else {
+            p_phase_k<false, W, K>(c1, m_first, tailm, a0, a1);
+            decide_k<false, W, K>(a0, a1, m, F, tailm, rest_any, any0, any1);
+          }
           slow = 0u;
           nk = K;
           Unroll<K>::run([&](auto ki) {
@@ -790,61 +782,88 @@ __global__ void __launch_bounds__(256) benor_lockstep_blocked_kernel(KParams p) 
       bool all_dec = false;
       uint64_t any0 = 0, any1 = 0;            // final round's x: some live node 0 / some 1
       for (uint32_t r = 1; r <= k_max; ++r) {
-        // ---- R-phase ("proposal phase", node.ts:46-82): c1 per receiver, c0 = M - c1
-        const bool odd = M & 1u;
-#pragma nounroll
-        for (uint32_t b = 0; b < NB; ++b) {
-          uint32_t a1[G];
-          tally_groups_x1<G>(Xr, W, a1);
-          const uint32_t st = odd ? stage_proposals<true, G>(a1, b, m, M) : stage_proposals<false, G>(a1, b, m, M);
-          if (lane < 4u * G) reinterpret_cast<uint32_t *>(P + b * G)[lane] = st;
-        }
-        // ---- P-phase ("voting phase", node.ts:83-158)
         bool done = true;
-        any0 = 0;
-        any1 = 0;
+        // One round; ODD (M odd): no R-phase tie, so no "?" proposal and a
+        // receiver's P-phase c0 = m - c1 -- only the p1 plane is staged and
+        // counted (see p_phase_k).
+        auto round = [&](auto odd_c) {
+          constexpr bool ODD = decltype(odd_c)::value;
+          uint2 *P1 = reinterpret_cast<uint2 *>(P);   // ODD: x1-style p1 plane [XW] in P's space
+          // ---- R-phase ("proposal phase", node.ts:46-82): c1 per receiver, c0 = M - c1
 #pragma nounroll
-        for (uint32_t b = 0; b < NB; ++b) {
-          uint32_t a0[G], a1[G];
-          tally_groups<G>(P, W, a0, a1);
-          uint32_t st = 0, dbb = D[b * 64u + lane];
-          Unroll<G>::run([&](auto gi) {
-            constexpr int g = decltype(gi)::value;
-            const uint64_t vm = group_mask(b * G + g, m);
-            const uint32_t Fg = F + (uint32_t)g;
-            const uint64_t d0 = vcmp_gt(a0[g], Fg) & vm;                 // node.ts:99
-            const uint64_t d1 = vcmp_gt(a1[g], Fg) & vm & ~d0;           // node.ts:102
-            const uint64_t rest = vm & ~(d0 | d1);
-            uint64_t x1 = d1;
-            if (rest) {
-              const uint64_t ad1 = ballot_s(a1[g] > a0[g]) & rest;       // node.ts:108-109
-              const uint64_t tie = ballot_s(a1[g] == a0[g]) & rest;      // node.ts:110-111
-              x1 |= ad1;
-              if (tie) {                                                // node.ts:111
-                const uint64_t trial = lds_u64(keys + 2) + t;
-                const uint32_t *ids = reinterpret_cast<const uint32_t *>((uintptr_t)lds_u64(keys + 4));
-                x1 |= coin_ballot(keys, (uint32_t)trial, (uint32_t)(trial >> 32), ids, b * G + g, r, tie);
-              }
+          for (uint32_t b = 0; b < NB; ++b) {
+            uint32_t a1[G];
+            tally_groups_x1<G>(Xr, W, a1);
+            if constexpr (ODD) {
+              const uint32_t hi_t = M >> 1;
+              uint32_t st = 0;
+              Unroll<G>::run([&](auto gi) {
+                constexpr int g = decltype(gi)::value;
+                const uint64_t p1 = vcmp_gt(a1[g], hi_t + (uint32_t)g) & group_mask(b * G + g, m);   // node.ts:63-69
+                st = writelane<2 * g>(st, (uint32_t)p1);
+                st = writelane<2 * g + 1>(st, (uint32_t)(p1 >> 32));
+              });
+              if (lane < 2u * G) reinterpret_cast<uint32_t *>(P1 + b * G)[lane] = st;
+            } else {
+              const uint32_t st = stage_proposals<false, G>(a1, b, m, M);
+              if (lane < 4u * G) reinterpret_cast<uint32_t *>(P + b * G)[lane] = st;
             }
-            st = writelane<2 * g>(st, (uint32_t)x1);
-            st = writelane<2 * g + 1>(st, (uint32_t)(x1 >> 32));
-            dbb = select_lanes(dbb, dbb | (1u << g), d0 | d1);           // sticky decided bit (node.ts:100-105)
-            any1 |= x1;
-            any0 |= vm & ~x1;
-            asm volatile("" : "+s"(any0), "+s"(any1));                   // fold per group
-          });
-          D[b * 64u + lane] = dbb;
-          if (lane < 2u * G) reinterpret_cast<uint32_t *>(X + b * G)[lane] = st;
-          // groups of this block that hold live receivers for this lane
-          const uint32_t j0 = b * G;
-          uint32_t expect = 0u;
-          if (j0 + 1u < W) {
-            const uint32_t nfull = (W - 1u - j0) < (uint32_t)G ? (W - 1u - j0) : (uint32_t)G;
-            expect = nfull >= 32u ? ~0u : ((1u << nfull) - 1u);
           }
-          if (W - 1u >= j0 && W - 1u < j0 + G && lane < tail_n) expect |= 1u << (W - 1u - j0);
-          done = done && __all((dbb & expect) == expect);
-        }
+          if constexpr (ODD) {                         // padding group read by the pairwise tally
+            if (lane < XW - NB * G) P1[NB * G + lane] = make_uint2(0u, 0u);
+          }
+          // ---- P-phase ("voting phase", node.ts:83-158)
+          const uint32_t mF = m > F ? m - F : 0u;
+          any0 = 0;
+          any1 = 0;
+#pragma nounroll
+          for (uint32_t b = 0; b < NB; ++b) {
+            uint32_t a0[G], a1[G];
+            if constexpr (ODD) tally_groups_x1<G>(P1, W, a1);
+            else tally_groups<G>(P, W, a0, a1);
+            uint32_t st = 0, dbb = D[b * 64u + lane];
+            Unroll<G>::run([&](auto gi) {
+              constexpr int g = decltype(gi)::value;
+              const uint64_t vm = group_mask(b * G + g, m);
+              const uint32_t Fg = F + (uint32_t)g;
+              const uint64_t d0 = (ODD ? vcmp_lt(a1[g], mF + (uint32_t)g)   // c0 = m - c1 > F
+                                       : vcmp_gt(a0[g], Fg)) & vm;          // node.ts:99
+              const uint64_t d1 = vcmp_gt(a1[g], Fg) & vm & ~d0;           // node.ts:102
+              const uint64_t rest = vm & ~(d0 | d1);
+              uint64_t x1 = d1;
+              if (rest) {
+                const uint32_t a0g = ODD ? (m + 2u * (uint32_t)g) - a1[g] : a0[g];   // bias g
+                const uint64_t ad1 = ballot_s(a1[g] > a0g) & rest;         // node.ts:108-109
+                const uint64_t tie = ballot_s(a1[g] == a0g) & rest;        // node.ts:110-111
+                x1 |= ad1;
+                if (tie) {                                                // node.ts:111
+                  const uint64_t trial = lds_u64(keys + 2) + t;
+                  const uint32_t *ids = reinterpret_cast<const uint32_t *>((uintptr_t)lds_u64(keys + 4));
+                  x1 |= coin_ballot(keys, (uint32_t)trial, (uint32_t)(trial >> 32), ids, b * G + g, r, tie);
+                }
+              }
+              st = writelane<2 * g>(st, (uint32_t)x1);
+              st = writelane<2 * g + 1>(st, (uint32_t)(x1 >> 32));
+              dbb = select_lanes(dbb, dbb | (1u << g), d0 | d1);           // sticky decided bit (node.ts:100-105)
+              any1 |= x1;
+              any0 |= vm & ~x1;
+              asm volatile("" : "+s"(any0), "+s"(any1));                   // fold per group
+            });
+            D[b * 64u + lane] = dbb;
+            if (lane < 2u * G) reinterpret_cast<uint32_t *>(X + b * G)[lane] = st;
+            // groups of this block that hold live receivers for this lane
+            const uint32_t j0 = b * G;
+            uint32_t expect = 0u;
+            if (j0 + 1u < W) {
+              const uint32_t nfull = (W - 1u - j0) < (uint32_t)G ? (W - 1u - j0) : (uint32_t)G;
+              expect = nfull >= 32u ? ~0u : ((1u << nfull) - 1u);
+            }
+            if (W - 1u >= j0 && W - 1u < j0 + G && lane < tail_n) expect |= 1u << (W - 1u - j0);
+            done = done && __all((dbb & expect) == expect);
+          }
+        };
+        if (M & 1u) round(std::true_type{});
+        else round(std::false_type{});
         Xr = X;
         M = m;
         R = r;

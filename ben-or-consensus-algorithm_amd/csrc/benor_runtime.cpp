@@ -307,12 +307,16 @@ void bo_plan_destroy(bo_plan *pl) {
 
 uint32_t bo_plan_live_nodes(const bo_plan *pl) { return pl ? pl->kp.m : 0u; }
 
-// Lockstep: the R-phase needs c1 only (c0 = m - c1 - c?, node.ts:52,56-62),
-// the P-phase c0 and c1 (node.ts:92-98): 3 counts of ceil(m/32) words.
-// Random delivery counts both in both phases: 4.
+// Lockstep: the R-phase needs c1 only (c0 = M - c1, M binary votes,
+// node.ts:52,56-62).  The P-phase needs c0 and c1 (node.ts:92-98) unless M
+// is odd: then no R-phase count can tie, no proposal is "?" (node.ts:63-69),
+// and c0 = m - c1.  So 2 counts of ceil(m/32) words for odd M (the bench's
+// m = 683), 3 for even M (round-1 parity: M = m - init_q).  Random delivery
+// counts both values in both phases: 4.
 uint64_t bo_plan_popc_words_per_node_round(const bo_plan *pl) {
   if (!pl) return 0;
-  const uint64_t counts = pl->kp.mode == BO_MODE_RANDOM_DELIVERY ? 4ull : 3ull;
+  uint64_t counts = 4ull;
+  if (pl->kp.mode != BO_MODE_RANDOM_DELIVERY) counts = ((pl->kp.m - pl->kp.init_q) & 1u) ? 2ull : 3ull;
   return counts * ((pl->kp.m + 31ull) / 32ull);
 }
 
