@@ -54,8 +54,9 @@ def main(tag, trials, N=1024, F=341):
         lines.append(f"| {k} | {c[k]:.6g} | {c[k] / trials:.4g} |")
     if "SQ_INSTS_VALU" in c:
         W = (m + 63) // 64
-        bcnt = 6 * W * W     # per receiver group: 2W words (R-phase c1) + 4W words (P-phase c0, c1)
-        lines += ["", f"- v_bcnt per trial (one round; 6W words per receiver group x W groups, W = ceil(m/64)): {bcnt}",
+        per = 4 if m % 2 else 6   # words per receiver group / W: 2 (R-phase c1) + 2 (P c1, odd m) or 4 (P c0, c1)
+        bcnt = per * W * W
+        lines += ["", f"- v_bcnt per trial (one round; {per}W words per receiver group x W groups, W = ceil(m/64)): {bcnt}",
                   f"- VALU instructions per trial: {c['SQ_INSTS_VALU'] / trials:.1f} "
                   f"(non-v_bcnt: {c['SQ_INSTS_VALU'] / trials - bcnt:.1f})"]
     if "GRBM_GUI_ACTIVE" in c and stats:
