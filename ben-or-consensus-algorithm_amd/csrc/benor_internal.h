@@ -19,7 +19,7 @@ constexpr uint32_t kStreamCrash = 4u;
 
 constexpr int kWavesPerBlock = 4;          // 256-thread workgroups, one trial per wave
 constexpr uint32_t kMaxW = BO_MAX_N / 64;  // u64 words per bit plane at N = 4096
-constexpr int kMaxWSpecialised = 16;       // m <= 1024: fully unrolled W-specialised kernel
+constexpr int kMaxWSpecialised = 32;       // m <= 2048: fully unrolled W-specialised kernel
 constexpr uint32_t kMaxPackedM = 32;       // m <= 32: packed kernel, floor(32/m) trials per half-wave
 constexpr uint64_t kMaxTrialsPerLaunch = 1ull << 31;   // trial offsets within a launch fit 32 bits
 constexpr uint32_t kParamBytes = 32;       // LDS parameter block after the histogram (W kernel)
@@ -63,6 +63,13 @@ struct KParams {
 void plan_geometry(KParams &p);
 
 hipError_t launch_lockstep(const KParams &p, int grid_blocks, hipStream_t stream);
+
+// Per-shape launchers, explicitly instantiated in benor_w_*.hip (W = 1..32)
+// and benor_blocked.hip (G = 11..16).
+template <int W>
+hipError_t launch_w(const KParams &p, int grid_blocks, hipStream_t stream);
+template <int G>
+hipError_t launch_b(const KParams &p, int grid_blocks, hipStream_t stream);
 
 // Grid size that fills the current device for this configuration.
 int lockstep_grid(const KParams &p, int device);

@@ -27,883 +27,14 @@
 // an opaque `v_bcnt_u32_b32` and each receiver group's chain starts from a
 // distinct constant (subtracted afterwards) so that every live node's count is
 // executed by its own lane, as the reference executes it in its own handler.
-#include <hip/hip_runtime.h>
-#include <stdint.h>
-
-#include <type_traits>
-
-#include "benor_internal.h"
-
-#ifndef BENOR_FUSED
-#define BENOR_FUSED 1
-#endif
+//
+// This file: the packed (m <= 32), random-delivery and event-level kernels,
+// the popcount probe, and the host-side planning / dispatch.  The lockstep
+// W kernel lives in benor_w_kernel.h (instantiated by benor_w_*.hip) and the
+// blocked kernel in benor_blocked.hip.
+#include "benor_device.h"
 
 namespace benor {
-
-// ------------------------------------------------------------------ Philox
-__device__ __forceinline__ uint4 philox4x32_10(uint32_t k0, uint32_t k1, uint4 c) {
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    const uint32_t lo0 = 0xD2511F53u * c.x;
-    const uint32_t hi0 = __umulhi(0xD2511F53u, c.x);
-    const uint32_t lo1 = 0xCD9E8D57u * c.z;
-    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z);
-    c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
-    k0 += 0x9E3779B9u;
-    k1 += 0xBB67AE85u;
-  }
-  return c;
-}
-
-// One receiver's tally step: acc + popcount(word).  Opaque on purpose (see
-// the header comment): the per-receiver count must execute per receiver.
-__device__ __forceinline__ uint32_t tally(uint32_t word, uint32_t acc) {
-  uint32_t r;
-  asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(word), "v"(acc));
-  return r;
-}
-
-__device__ __forceinline__ uint64_t group_mask(uint32_t j, uint32_t m) {
-  const uint32_t lo = j * 64u;
-  if (lo >= m) return 0ull;
-  const uint32_t n = m - lo;
-  return n >= 64u ? ~0ull : ((1ull << n) - 1ull);
-}
-
-__device__ __forceinline__ uint4 rec(uint64_t is0, uint64_t is1) {
-  return make_uint4((uint32_t)is0, (uint32_t)(is0 >> 32), (uint32_t)is1, (uint32_t)(is1 >> 32));
-}
-
-__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
-
-// Ballot whose SGPR result may feed an inline-asm VALU (v_bcnt / v_writelane
-// with an SGPR operand).  gfx950 needs 2 wait states between a VALU write of
-// an SGPR/VCC and a VALU read of it; the compiler inserts them for its own
-// instructions (s_nop 1 after v_cmp) but cannot see the read inside an asm
-// statement.  The dependent s_nop below supplies them: every consumer of the
-// returned mask is ordered after it.
-__device__ __forceinline__ uint64_t ballot_s(bool p) {
-  uint64_t b = __ballot(p);
-  asm volatile("s_nop 1" : "+s"(b));
-  return b;
-}
-
-
-// Coins of the tied receivers of one group (node.ts:111).  The key words are
-// laundered through an empty asm so that Philox's ten round keys are not
-// hoisted out of the round loop into permanently live SGPRs.
-__device__ __forceinline__ uint64_t coin_ballot(uint32_t k0, uint32_t k1, uint32_t tlo, uint32_t thi,
-                                             const uint32_t *__restrict__ live_ids, uint32_t group,
-                                             uint32_t round, uint64_t tie) {
-  const uint32_t lane = threadIdx.x & 63u;
-  asm volatile("" : "+s"(k0), "+s"(k1));
-  bool c1 = false;
-  if ((tie >> lane) & 1ull) {
-    const uint32_t node = live_ids[group * 64u + lane];
-    const uint4 rr = philox4x32_10(k0, k1, make_uint4(tlo, thi, node, (round & 0x00FFFFFFu) | (kStreamCoin << 24)));
-    c1 = !(rr.x > 0x80000000u);                 // Math.random() > 0.5 ? 0 : 1
-  }
-  return ballot(c1) & tie;
-}
-
-// Philox key words re-read from LDS at the point of use.  The volatile load
-// cannot be hoisted, so the key schedule of a rare path (coins, the per-batch
-// init pass) is rebuilt there instead of being kept -- i.e. spilled -- in SGPRs
-// across the whole round loop.
-__device__ __forceinline__ uint2 lds_keys(const uint32_t *keys) {
-  const volatile __attribute__((address_space(3))) uint32_t *k =
-      (const volatile __attribute__((address_space(3))) uint32_t *)keys;   // ds_read, not a flat load
-  return make_uint2((uint32_t)__builtin_amdgcn_readfirstlane((int)k[0]),
-                    (uint32_t)__builtin_amdgcn_readfirstlane((int)k[1]));
-}
-
-__device__ __forceinline__ uint64_t coin_ballot(const uint32_t *keys, uint32_t tlo, uint32_t thi,
-                                             const uint32_t *__restrict__ live_ids, uint32_t group,
-                                             uint32_t round, uint64_t tie) {
-  const uint2 k = lds_keys(keys);
-  tlo = (uint32_t)__builtin_amdgcn_readfirstlane((int)tlo);   // wave-uniform trial id; the asm keeps
-  thi = (uint32_t)__builtin_amdgcn_readfirstlane((int)thi);   // Philox's first product on this path
-  asm volatile("" : "+s"(tlo), "+s"(thi));
-  return coin_ballot(k.x, k.y, tlo, thi, live_ids, group, round, tie);
-}
-
-// A call's result comes back in VGPRs; the ballot is wave-uniform, so move it
-// to SGPRs for the mask arithmetic that follows.
-__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
-  return (uint64_t)hi << 32 | lo;
-}
-
-// ------------------------------------------- W-specialised kernel (m <= 1024)
-// For networks of at most 1024 live nodes (W <= 16 receiver groups) the whole
-// round is unrolled at compile time: every receiver group's tally chain is a
-// register, the plane records are read with immediate LDS offsets, a phase's
-// ballots are staged into one VGPR with v_writelane and stored by one
-// ds_write_b32, and the per-group `decided` masks live in SGPRs.  Initial
-// values of TB = 64 / ceil(W/2) consecutive trials of the wave are drawn by
-// one Philox pass (every lane busy) into an LDS ring.
-template <int N, int I = 0>
-struct Unroll {
-  template <class Fn>
-  __device__ __forceinline__ static void run(Fn &&f) {
-    if constexpr (I < N) {
-      f(std::integral_constant<int, I>{});
-      Unroll<N, I + 1>::run(f);
-    }
-  }
-};
-
-// First step of receiver group C's chain: popcount(word) + C.  The distinct
-// immediate per group keeps the groups' (identical, in lockstep) chains from
-// being merged; comparisons are bias-invariant and thresholds add C.
-template <int C>
-__device__ __forceinline__ uint32_t tally_first(uint32_t word) {
-  uint32_t r;
-  asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(word), "i"(C));
-  return r;
-}
-
-
-
-// R-phase tally of one receiver group set: c1 only.  A receiver's R-phase
-// trigger fires with exactly m messages in its inbox (node.ts:52, len >= N-F,
-// m = N-F live senders in lockstep); each is 0, 1 or "?", so
-// c0 = m - c1 - c? (node.ts:56-62) and c? is 0 in every round but the first
-// of a fixed-init run with "?" initial values (a plan constant there).  The x
-// planes therefore carry only the is1 word: 2 dwords per group, read as
-// 16-byte pairs of groups.
-template <int W>
-__device__ __forceinline__ void tally_x1(const uint2 *__restrict__ plane, uint32_t (&a1)[W]) {
-  const uint4 *q4 = reinterpret_cast<const uint4 *>(plane);
-  {
-    const uint4 q = q4[0];
-    Unroll<W>::run([&](auto gi) {
-      constexpr int g = decltype(gi)::value;
-      a1[g] = tally_first<g>(q.x);
-    });
-#pragma unroll
-    for (int g = 0; g < W; ++g) a1[g] = tally(q.y, a1[g]);
-    if constexpr (W > 1) {
-#pragma unroll
-      for (int g = 0; g < W; ++g) {
-        a1[g] = tally(q.z, a1[g]);
-        a1[g] = tally(q.w, a1[g]);
-      }
-    }
-  }
-#pragma unroll
-  for (int w = 1; w < W / 2; ++w) {
-    const uint4 s = q4[w];
-#pragma unroll
-    for (int g = 0; g < W; ++g) {
-      a1[g] = tally(s.x, a1[g]);
-      a1[g] = tally(s.y, a1[g]);
-      a1[g] = tally(s.z, a1[g]);
-      a1[g] = tally(s.w, a1[g]);
-    }
-  }
-  if constexpr (W > 1 && (W & 1)) {
-    const uint2 s = plane[W - 1];
-#pragma unroll
-    for (int g = 0; g < W; ++g) {
-      a1[g] = tally(s.x, a1[g]);
-      a1[g] = tally(s.y, a1[g]);
-    }
-  }
-}
-
-// Proposal planes can stay in SGPRs for the few hundred cycles between the
-// R-phase ballots that produce them and the P-phase tallies that read them:
-// v_bcnt_u32_b32 takes its word from an SGPR at the same issue rate, so this
-// saves the four staging moves per receiver group of the R-phase.
-template <int C>
-__device__ __forceinline__ uint32_t tally_first_s(uint32_t word) {
-  uint32_t r;
-  asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "s"(word), "i"(C));
-  return r;
-}
-
-__device__ __forceinline__ uint32_t tally_s(uint32_t word, uint32_t acc) {
-  uint32_t r;
-  asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "s"(word), "v"(acc));
-  return r;
-}
-
-// Wave-uniform 64-bit value re-read from LDS at the point of use (volatile:
-// the read stays where it is written, see the W kernel's parameter block).
-typedef const volatile __attribute__((address_space(3))) uint32_t lds_cv_u32;
-
-__device__ __forceinline__ uint64_t lds_u64(const uint32_t *w) {
-  lds_cv_u32 *k = (lds_cv_u32 *)w;   // ds_read, not a flat load
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)k[0]);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)k[1]);
-  return (uint64_t)hi << 32 | lo;
-}
-
-__device__ __forceinline__ uint32_t sgpr32(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
-}
-
-// Per-lane select by a wave lane mask: lanes whose bit is set take `b`
-// (one v_cndmask_b32 with an SGPR mask; a C select would shift the mask by
-// the lane id in 64-bit VALU ops).
-__device__ __forceinline__ uint32_t select_lanes(uint32_t a, uint32_t b, uint64_t mask) {
-  uint32_t r;
-  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(mask));
-  return r;
-}
-
-// Opaque wave compares (v_cmp -> SGPR lane mask).  asm volatile so that the
-// compiler neither merges the decision pass's compares with the adopt pass's
-// recomputation of them (which would keep 2W masks live across the pass and
-// spill SGPRs) nor speculates them out of their branches.  The trailing
-// s_nop 1 supplies the 2 wait states gfx950 needs between a VALU SGPR write
-// and a VALU read of it inside a later asm (v_bcnt with an SGPR operand).
-__device__ __forceinline__ uint64_t vcmp_gt(uint32_t v, uint32_t s) {   // lanes with v > s
-  uint64_t r;
-  asm volatile("v_cmp_gt_u32_e64 %0, %1, %2\n\ts_nop 1" : "=s"(r) : "v"(v), "s"(s));
-  return r;
-}
-__device__ __forceinline__ uint64_t vcmp_lt(uint32_t v, uint32_t s) {   // lanes with v < s
-  uint64_t r;
-  asm volatile("v_cmp_lt_u32_e64 %0, %1, %2\n\ts_nop 1" : "=s"(r) : "v"(v), "s"(s));
-  return r;
-}
-
-
-template <int L>
-__device__ __forceinline__ uint32_t writelane(uint32_t v, uint32_t val) {
-  asm("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(val), "i"(L));
-  return v;
-}
-
-// Stage one group's two ballot words (4 dwords) into lanes 4g..4g+3 of v.
-template <int G>
-__device__ __forceinline__ uint32_t stage4(uint32_t v, uint64_t is0, uint64_t is1) {
-  v = writelane<4 * G + 0>(v, (uint32_t)is0);
-  v = writelane<4 * G + 1>(v, (uint32_t)(is0 >> 32));
-  v = writelane<4 * G + 2>(v, (uint32_t)is1);
-  v = writelane<4 * G + 3>(v, (uint32_t)(is1 >> 32));
-  return v;
-}
-
-// One round's R-phase proposals (node.ts:63-69, from each receiver's c1 and the
-// binary vote count M) fused with the P-phase tallies (node.ts:92-98), for K
-// independent trials at once (K > 1: small W, interleaved sender group by
-// sender group so one trial's compares and tallies fill the other's
-// dependency stalls).  Sender group w's proposal masks are added to every
-// receiver group's counts as soon as they exist, so only one group's
-// proposal planes (SGPR pairs) is live.
-//
-// ODD (M odd): c0 == c1 is impossible in the R-phase, so "c0 > c1" is the
-// complement of "c1 > c0" (one compare) and no proposal is "?".  Every
-// P-phase vote is then 0 or 1, so a receiver's c0 = m - c1 and only the c1
-// tally is made (a0 is left unset; decide_k / the adopt pass derive it).
-template <bool ODD, int W, int K>
-__device__ __forceinline__ void p_phase_k(const uint32_t (&c1r)[K][W], uint32_t M, uint64_t tailm,
-                                          uint32_t (&a0)[K][W], uint32_t (&a1)[K][W]) {
-  const uint32_t hi_t = M >> 1, lo_t = (M + 1u) >> 1;
-  Unroll<W>::run([&](auto wi) {
-    constexpr int w = decltype(wi)::value;
-    const uint64_t vm = (w == W - 1) ? tailm : ~0ull;
-    Unroll<K>::run([&](auto ki) {
-      constexpr int k = decltype(ki)::value;
-      const uint64_t p1 = vcmp_gt(c1r[k][w], hi_t + (uint32_t)w) & vm;         // c1 > c0  (node.ts:65-66)
-      const uint32_t l1 = (uint32_t)p1, h1 = (uint32_t)(p1 >> 32);
-      if constexpr (!ODD) {
-        const uint64_t p0 = vcmp_lt(c1r[k][w], lo_t + (uint32_t)w) & vm;       // c0 > c1  (node.ts:63-64), else "?"
-        const uint32_t l0 = (uint32_t)p0, h0 = (uint32_t)(p0 >> 32);
-        if constexpr (w == 0) {
-          Unroll<W>::run([&](auto gi) {
-            constexpr int g = decltype(gi)::value;
-            a0[k][g] = tally_first_s<g>(l0);
-          });
-        } else {
-#pragma unroll
-          for (int g = 0; g < W; ++g) a0[k][g] = tally_s(l0, a0[k][g]);
-        }
-#pragma unroll
-        for (int g = 0; g < W; ++g) a0[k][g] = tally_s(h0, a0[k][g]);
-      }
-      if constexpr (w == 0) {
-        Unroll<W>::run([&](auto gi) {
-          constexpr int g = decltype(gi)::value;
-          a1[k][g] = tally_first_s<g>(l1);
-        });
-      } else {
-#pragma unroll
-        for (int g = 0; g < W; ++g) a1[k][g] = tally_s(l1, a1[k][g]);
-      }
-#pragma unroll
-      for (int g = 0; g < W; ++g) a1[k][g] = tally_s(h1, a1[k][g]);
-    });
-  });
-}
-
-// Decisions (node.ts:99-105) of K trials: whether some live receiver stays
-// undecided, and which values were decided.  ODD: c0 = m - c1, so
-// "c0 > F" is "c1 < m - F" (no c0 tally exists).  Chain bias g throughout.
-template <bool ODD, int W, int K>
-__device__ __forceinline__ void decide_k(const uint32_t (&a0)[K][W], const uint32_t (&a1)[K][W], uint32_t m,
-                                         uint32_t F, uint64_t tailm, uint64_t (&rest_any)[K], uint64_t (&any0)[K],
-                                         uint64_t (&any1)[K]) {
-  const uint32_t mF = m > F ? m - F : 0u;
-#pragma unroll
-  for (int k = 0; k < K; ++k) rest_any[k] = any0[k] = any1[k] = 0;
-  Unroll<W>::run([&](auto gi) {
-    constexpr int g = decltype(gi)::value;
-    const uint64_t vm = (g == W - 1) ? tailm : ~0ull;
-    Unroll<K>::run([&](auto ki) {
-      constexpr int k = decltype(ki)::value;
-      const uint64_t d0 = (ODD ? vcmp_lt(a1[k][g], mF + (uint32_t)g)           // node.ts:99
-                               : vcmp_gt(a0[k][g], F + (uint32_t)g)) & vm;
-      const uint64_t d1 = vcmp_gt(a1[k][g], F + (uint32_t)g) & vm & ~d0;      // node.ts:102
-      rest_any[k] |= vm & ~(d0 | d1);
-      any0[k] |= d0;
-      any1[k] |= d1;
-      // fold now: otherwise the ORs sink to the loop exit and all 2W masks stay live
-      asm volatile("" : "+s"(rest_any[k]), "+s"(any0[k]), "+s"(any1[k]));
-    });
-  });
-}
-
-// STATE: the network API's single-trial launch that also reports per-node
-// state and the halting round (GET /getState); the batch path is compiled
-// without that code, which keeps its register allocation free of it.
-constexpr int kPairMaxW = 8;               // W kernel: pair trials' round 1 up to this W
-
-template <int W, bool STATE>
-__global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
-  constexpr int NPH = (W + 1) / 2;          // Philox blocks per trial (2 plane words each)
-  constexpr int TB = 64 / NPH;              // trials per init batch
-  constexpr int WP = 2 * NPH;               // x1 words per plane row, padded to 16 bytes
-  constexpr int K = W <= 2 ? 4 : (W <= kPairMaxW ? 2 : 1);   // trials whose round 1 runs interleaved
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // uniform: scalar trial loop
-  // Only the round loop's own scalars are kept in registers.  What a rare
-  // path needs (Philox key, trial id base, live ids) sits in a small LDS
-  // parameter block and is re-read where it is used, so the register
-  // allocator never holds -- and spills -- a kernarg tuple across the
-  // trial loop.
-  uint32_t m = p.m, F = p.F, k_max = p.k_max, hist_len = p.hist_len;
-  // trial offsets within the launch are 32-bit (the host splits launches at 2^31)
-  uint32_t trial_count = (uint32_t)p.trial_count;
-  asm volatile("" : "+s"(m), "+s"(F), "+s"(k_max), "+s"(hist_len), "+s"(trial_count));
-
-  uint32_t *lhist = reinterpret_cast<uint32_t *>(smem);
-  uint2 *ring = reinterpret_cast<uint2 *>(smem + p.hist_bytes + wv * p.wave_bytes);   // [TB][WP] x1 words
-  uint2 *X = ring + TB * WP;       // [WP] final x1 plane (GET /getState only)
-  uint2 *D = X + WP;               // [WP] sticky decided bits, kept only while some receiver is undecided
-  // parameter block: [0,1] Philox key (seed), [2,3] trial_begin, [4,5] live_ids
-  uint32_t *keys = reinterpret_cast<uint32_t *>(smem + p.hist_bytes - kParamBytes);
-
-  for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) lhist[i] = 0u;
-  if (threadIdx.x == 0) {
-    keys[0] = (uint32_t)p.seed;
-    keys[1] = (uint32_t)(p.seed >> 32);
-    keys[2] = (uint32_t)p.trial_begin;
-    keys[3] = (uint32_t)(p.trial_begin >> 32);
-    keys[4] = (uint32_t)(uintptr_t)p.live_ids;
-    keys[5] = (uint32_t)((uintptr_t)p.live_ids >> 32);
-  }
-  if (p.init_mode != BO_INIT_RANDOM && lane < (uint32_t)W) {
-    const uint4 q = p.init_plane[lane];
-    ring[lane] = make_uint2(q.z, q.w);
-  }
-  __syncthreads();
-
-  const uint32_t waves_total = gridDim.x * kWavesPerBlock;
-  const uint64_t tailm = group_mask(W - 1, m);
-  const bool random_init = p.init_mode == BO_INIT_RANDOM;
-  const uint32_t m_first = m - p.init_q;      // binary-valued senders in round 1 ("?" excluded)
-
-  uint32_t hc = 0;                            // this wave's outcome counts of bins 0..63, lane = bin
-  for (uint32_t base = blockIdx.x * kWavesPerBlock + wv; base < trial_count; base += waves_total * TB) {
-    // ---- /start (node.ts:167-188): round-1 x planes of TB trials at once.
-    if (random_init) {
-      const uint32_t s = lane / NPH, b = lane - s * NPH;
-      const uint32_t t = base + s * waves_total;
-      if (s < (uint32_t)TB && t < trial_count) {
-        const uint64_t trial = lds_u64(keys + 2) + t;
-        const uint2 kk = lds_keys(keys);           // keep the round keys out of long-lived SGPRs
-        const uint4 r = philox4x32_10(kk.x, kk.y, make_uint4((uint32_t)trial, (uint32_t)(trial >> 32), b, kStreamInit << 24));
-        const uint64_t v0 = group_mask(2u * b, m), v1 = group_mask(2u * b + 1u, m);
-        const uint64_t x1a = ((uint64_t)r.y << 32 | r.x) & v0, x1b = ((uint64_t)r.w << 32 | r.z) & v1;
-        reinterpret_cast<uint4 *>(ring + s * WP)[b] =
-            make_uint4((uint32_t)x1a, (uint32_t)(x1a >> 32), (uint32_t)x1b, (uint32_t)(x1b >> 32));
-      }
-    }
-    // One trial's outcome: bins 0..63 (undecided, and halting rounds <= 20) in
-    // lane `bin` of the wave's counter (one VALU op), the rest as LDS atomics.
-    auto record = [&](uint64_t any0, uint64_t any1, uint32_t R, bool all_dec) {
-      const uint32_t v = (any0 && any1) ? 2u : (any1 ? 1u : 0u);
-      const uint32_t bin = all_dec ? (R * 3u + v) : v;
-      if (bin < 64u) hc += (lane == bin) ? 1u : 0u;
-      else if (lane == 0) atomicAdd(&lhist[bin], 1u);
-      if (all_dec && v == 2u && lane == 0) atomicAdd(&lhist[hist_len - 1u], 1u);
-    };
-    // One whole trial, round after round.
-    auto single = [&](int s, uint32_t t) {
-      // ---- round-1 R-phase tallies over the /start broadcast (node.ts:167-188)
-      uint32_t c1r[W];
-      tally_x1<W>(random_init ? ring + s * WP : ring, c1r);
-      uint64_t any0 = 0, any1 = 0;            // final round's x: some live node 0 / some 1
-      uint32_t R = 0, M = m_first;
-      bool all_dec = false, have_hist = false;
-      for (uint32_t r = 1;; ++r) {
-        // ---- R-phase ("proposal phase", node.ts:46-82) proposals from c1 (c0 = M - c1)
-        // fused with the P-phase ("voting phase", node.ts:83-158) tallies.  With an
-        // odd number M of binary votes c0 == c1 is impossible, so "c0 > c1" is the
-        // complement of "c1 > c0" and costs no second compare (ODD: one copy of the
-        // phase per parity, no branch inside it).
-        uint32_t a0[1][W], a1[1][W];
-        uint64_t rest_any[1], any0_[1], any1_[1];
-        auto& c1v = reinterpret_cast<uint32_t(&)[1][W]>(c1r);
-        const bool odd = M & 1u;
-        if (odd) {
-          p_phase_k<true, W, 1>(c1v, M, tailm, a0, a1);
-          decide_k<true, W, 1>(a0, a1, m, F, tailm, rest_any, any0_, any1_);
-        } else {
-          p_phase_k<false, W, 1>(c1v, M, tailm, a0, a1);
-          decide_k<false, W, 1>(a0, a1, m, F, tailm, rest_any, any0_, any1_);
-        }
-        R = r;                                                        // node.ts:147  k = r + 1
-        any0 = any0_[0];
-        any1 = any1_[0];
-        // ---- when every live receiver decides in this round the trial halts
-        // (decided is sticky) and x = the decided value, so neither the
-        // adopt/coin branch nor the next round's planes are needed.
-        if (!rest_any[0] && !STATE) {
-          all_dec = true;                                             // all-decided auto-stop
-          break;
-        }
-        // ---- some receiver did not decide: adopt / coin (node.ts:106-113), the
-        // sticky decided history (LDS, only on this path), and the next round's
-        // R-phase tallies fused with the new x ballots (no staged plane).
-        const bool more = r < k_max;
-        uint64_t undone = 0;
-        uint32_t sx = 0, sd = 0;
-        any0 = 0;
-        any1 = 0;
-        Unroll<W>::run([&](auto gi) {
-          constexpr int g = decltype(gi)::value;
-          const uint64_t vm = (g == W - 1) ? tailm : ~0ull;
-          const uint32_t Fg = F + (uint32_t)g;
-          // ODD round: no c0 tally was made; c0 = m - c1 (all votes binary), bias g
-          const uint32_t a0g = odd ? (m + 2u * (uint32_t)g) - a1[0][g] : a0[0][g];
-          const uint32_t a1g = a1[0][g];
-          const uint64_t d0 = vcmp_gt(a0g, Fg) & vm;
-          const uint64_t d1 = vcmp_gt(a1g, Fg) & vm & ~d0;
-          const uint64_t rest = vm & ~(d0 | d1);
-          uint64_t x1 = d1;
-          if (rest) {
-            const uint64_t ad1 = ballot_s(a1g > a0g) & rest;             // node.ts:108-109
-            const uint64_t tie = ballot_s(a1g == a0g) & rest;            // node.ts:110-111
-            x1 |= ad1;
-            if (tie) {                                                  // node.ts:111
-              const uint64_t trial = lds_u64(keys + 2) + t;
-              const uint32_t *ids = reinterpret_cast<const uint32_t *>((uintptr_t)lds_u64(keys + 4));
-              x1 |= coin_ballot(keys, (uint32_t)trial, (uint32_t)(trial >> 32), ids, g, r, tie);
-            }
-          }
-          uint64_t dg = d0 | d1;
-          if (have_hist) {
-            const uint2 h = D[g];
-            dg |= (uint64_t)sgpr32(h.y) << 32 | sgpr32(h.x);
-          }
-          sd = writelane<2 * g>(sd, (uint32_t)dg);
-          sd = writelane<2 * g + 1>(sd, (uint32_t)(dg >> 32));
-          undone |= vm & ~dg;
-          any1 |= x1;
-          any0 |= vm & ~x1;
-          asm volatile("" : "+s"(undone), "+s"(any0), "+s"(any1));   // fold per group (as in the decisions)
-          const uint32_t xl = sgpr32((uint32_t)x1), xh = sgpr32((uint32_t)(x1 >> 32));
-          if (more) {                                                 // round r+1 R-phase (node.ts:149-157)
-            if constexpr (g == 0) {
-              Unroll<W>::run([&](auto hi) {
-                constexpr int h = decltype(hi)::value;
-                c1r[h] = tally_first_s<h>(xl);
-              });
-            } else {
-#pragma unroll
-              for (int h = 0; h < W; ++h) c1r[h] = tally_s(xl, c1r[h]);
-            }
-#pragma unroll
-            for (int h = 0; h < W; ++h) c1r[h] = tally_s(xh, c1r[h]);
-          }
-          if constexpr (STATE) {
-            sx = writelane<2 * g>(sx, xl);
-            sx = writelane<2 * g + 1>(sx, xh);
-          }
-        });
-        if (lane < 2u * W) {
-          reinterpret_cast<uint32_t *>(D)[lane] = sd;
-          if (STATE) reinterpret_cast<uint32_t *>(X)[lane] = sx;
-        }
-        have_hist = true;
-        M = m;
-        all_dec = undone == 0;
-        if (all_dec || !more) break;
-      }
-      // ---- outcome
-      record(any0, any1, R, all_dec);
-      if constexpr (STATE) {
-        uint32_t *rounds_out = p.rounds_out;
-        if (lane == 0 && rounds_out) *rounds_out = all_dec ? R : 0u;
-      }
-      bo_node_state *node_out = STATE ? p.node_out : nullptr;
-      if (STATE && node_out) {                                               // GET /getState (node.ts:197-199)
-        Unroll<W>::run([&](auto gi) {
-          constexpr int g = decltype(gi)::value;
-          const uint32_t c = g * 64u + lane;
-          if (c < m) {
-            const uint2 q = X[g], d = D[g];
-            bo_node_state ns;
-            ns.killed = 0;
-            ns.x = (int8_t)(((lane < 32u ? q.x : q.y) >> (lane & 31u)) & 1u);
-            ns.decided = (int8_t)(((lane < 32u ? d.x : d.y) >> (lane & 31u)) & 1u);
-            ns.pad = 0;
-            ns.k = (int32_t)R + 1;
-            node_out[p.live_ids[c]] = ns;
-          }
-        });
-      }
-    };
-    for (int s = 0; s < TB;) {
-      const uint32_t t = base + (uint32_t)s * waves_total;
-      if (t >= trial_count) break;
-      uint32_t slow = 1u, nk = 1u;              // trials (bit k: s + k) to run alone; trials consumed
-      if constexpr (K > 1 && !STATE) {
-        if (s + K - 1 < TB && t + (uint32_t)(K - 1) * waves_total < trial_count) {
-          // ---- round 1 of K trials interleaved; a trial that does not halt in
-          // round 1 (some receiver undecided) is re-run alone from round 1.
-          uint32_t c1[K][W], a0[K][W], a1[K][W];
-          Unroll<K>::run([&](auto ki) {
-            constexpr int k = decltype(ki)::value;
-            tally_x1<W>(random_init ? ring + (s + k) * WP : ring, c1[k]);
-          });
-          uint64_t rest_any[K], any0[K], any1[K];
-          if (m_first & 1u) {
-            p_phase_k<true, W, K>(c1, m_first, tailm, a0, a1);
-            decide_k<true, W, K>(a0, a1, m, F, tailm, rest_any, any0, any1);
-          } else {
-            p_phase_k<false, W, K>(c1, m_first, tailm, a0, a1);
-            decide_k<false, W, K>(a0, a1, m, F, tailm, rest_any, any0, any1);
-          }
-          slow = 0u;
-          nk = K;
-          Unroll<K>::run([&](auto ki) {
-            constexpr int k = decltype(ki)::value;
-            if (!rest_any[k]) record(any0[k], any1[k], 1u, true);
-            else slow |= 1u << k;
-          });
-        }
-      }
-      for (; slow; slow &= slow - 1u) {         // one call site: the whole-trial loop is inlined once
-        const uint32_t k = (uint32_t)__builtin_ctz(slow);
-        single(s + (int)k, t + k * waves_total);
-      }
-      s += (int)nk;
-    }
-  }
-
-  if (hc) atomicAdd(&lhist[lane], hc);
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) {
-    const uint32_t c = lhist[i];
-    if (c) atomicAdd(&p.hist[i], (unsigned long long)c);
-  }
-}
-
-
-// --------------------------------------------- blocked kernel (1024 < m <= 4096)
-// Receiver groups are processed in NB blocks of G (NB = ceil(W/16), G =
-// ceil(W/NB), padding < NB groups); the record loop over the W plane words is
-// a runtime loop.  Per-lane `decided` bits live in registers (one word per
-// block).  Otherwise as the W-specialised kernel.
-template <int G>
-__device__ __forceinline__ void tally_groups(const uint4 *__restrict__ plane, uint32_t W, uint32_t (&a0)[G],
-                                             uint32_t (&a1)[G]) {
-  const uint4 q = plane[0];
-  Unroll<G>::run([&](auto gi) {
-    constexpr int g = decltype(gi)::value;
-    a0[g] = tally_first<g>(q.x);
-    a1[g] = tally_first<g>(q.z);
-  });
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    a0[g] = tally(q.y, a0[g]);
-    a1[g] = tally(q.w, a1[g]);
-  }
-  uint32_t w = 1;
-  for (; w + 1 < W; w += 2) {
-    const uint4 u = plane[w];
-    const uint4 v = plane[w + 1];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      a0[g] = tally(u.x, a0[g]);
-      a1[g] = tally(u.z, a1[g]);
-      a0[g] = tally(u.y, a0[g]);
-      a1[g] = tally(u.w, a1[g]);
-    }
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      a0[g] = tally(v.x, a0[g]);
-      a1[g] = tally(v.z, a1[g]);
-      a0[g] = tally(v.y, a0[g]);
-      a1[g] = tally(v.w, a1[g]);
-    }
-  }
-  if (w < W) {
-    const uint4 u = plane[w];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      a0[g] = tally(u.x, a0[g]);
-      a1[g] = tally(u.z, a1[g]);
-      a0[g] = tally(u.y, a0[g]);
-      a1[g] = tally(u.w, a1[g]);
-    }
-  }
-}
-
-// R-phase x1-only tally over the W words of a plane (runtime W, pairs of
-// groups per 16-byte read; WP = W rounded up to even, padding words zero).
-template <int G>
-__device__ __forceinline__ void tally_groups_x1(const uint2 *__restrict__ plane, uint32_t W, uint32_t (&a1)[G]) {
-  const uint4 *q4 = reinterpret_cast<const uint4 *>(plane);
-  const uint4 q = q4[0];
-  Unroll<G>::run([&](auto gi) {
-    constexpr int g = decltype(gi)::value;
-    a1[g] = tally_first<g>(q.x);
-  });
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    a1[g] = tally(q.y, a1[g]);
-    a1[g] = tally(q.z, a1[g]);
-    a1[g] = tally(q.w, a1[g]);
-  }
-  const uint32_t np = (W + 1u) >> 1;
-  for (uint32_t w = 1; w < np; ++w) {
-    const uint4 s = q4[w];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      a1[g] = tally(s.x, a1[g]);
-      a1[g] = tally(s.y, a1[g]);
-      a1[g] = tally(s.z, a1[g]);
-      a1[g] = tally(s.w, a1[g]);
-    }
-  }
-}
-
-// One block's R-phase proposals (node.ts:63-69) from the receivers' c1
-// counts, staged as {p0.lo, p0.hi, p1.lo, p1.hi} records for the P-phase
-// tallies of every block.  ODD: an odd number of binary votes cannot tie,
-// so p0 is the complement of p1 (one compare per group).
-template <bool ODD, int G>
-__device__ __forceinline__ uint32_t stage_proposals(const uint32_t (&a1)[G], uint32_t b, uint32_t m, uint32_t M) {
-  const uint32_t hi_t = M >> 1, lo_t = (M + 1u) >> 1;
-  uint32_t st = 0;
-  Unroll<G>::run([&](auto gi) {
-    constexpr int g = decltype(gi)::value;
-    const uint64_t vm = group_mask(b * G + g, m);
-    const uint64_t p1 = vcmp_gt(a1[g], hi_t + (uint32_t)g) & vm;          // c1 > c0  (node.ts:65-66)
-    const uint64_t p0 = ODD ? (vm & ~p1)                                   // c0 > c1  (node.ts:63-64)
-                            : (vcmp_lt(a1[g], lo_t + (uint32_t)g) & vm);   // else "?"
-    st = stage4<g>(st, p0, p1);
-  });
-  return st;
-}
-
-template <int G, bool STATE>
-__global__ void __launch_bounds__(256) benor_lockstep_blocked_kernel(KParams p) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // scalar trial loop
-  // Round-loop scalars in registers; the rest re-read where used (as the W kernel).
-  uint32_t m = p.m, F = p.F, W = p.W, NB = p.nblocks, k_max = p.k_max, hist_len = p.hist_len;
-  uint32_t trial_count = (uint32_t)p.trial_count;     // launches are split at 2^31 trials
-  asm volatile("" : "+s"(m), "+s"(F), "+s"(W), "+s"(NB));
-  asm volatile("" : "+s"(k_max), "+s"(hist_len), "+s"(trial_count));
-  const uint32_t nph = (W + 1u) >> 1, tb = 64u / nph, WP = 2u * nph;
-  const uint32_t XW = ((NB * G > WP ? NB * G : WP) + 1u) & ~1u;   // x1 words of the staged plane (even, padding zero)
-  const uint32_t tail_n = m - (W - 1u) * 64u;          // live receivers in the last group
-
-  uint32_t *lhist = reinterpret_cast<uint32_t *>(smem);
-  uint32_t *keys = reinterpret_cast<uint32_t *>(smem + p.hist_bytes - kParamBytes);   // see the W kernel
-  uint2 *ring = reinterpret_cast<uint2 *>(smem + p.hist_bytes + wv * p.wave_bytes);   // [tb][WP] x1 words
-  uint2 *X = ring + tb * WP;                                                            // [XW]
-  uint4 *P = reinterpret_cast<uint4 *>(X + XW);                                        // [NB*G]
-  uint32_t *D = reinterpret_cast<uint32_t *>(P + NB * G);                               // [NB][64] decided bits
-
-  for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) lhist[i] = 0u;
-  if (threadIdx.x == 0) {
-    keys[0] = (uint32_t)p.seed;
-    keys[1] = (uint32_t)(p.seed >> 32);
-    keys[2] = (uint32_t)p.trial_begin;
-    keys[3] = (uint32_t)(p.trial_begin >> 32);
-    keys[4] = (uint32_t)(uintptr_t)p.live_ids;
-    keys[5] = (uint32_t)((uintptr_t)p.live_ids >> 32);
-  }
-  if (p.init_mode != BO_INIT_RANDOM)
-    for (uint32_t w = lane; w < WP; w += 64u) {
-      const uint4 q = w < W ? p.init_plane[w] : make_uint4(0, 0, 0, 0);
-      ring[w] = make_uint2(q.z, q.w);
-    }
-  for (uint32_t w = lane; w < XW; w += 64u) X[w] = make_uint2(0u, 0u);
-  __syncthreads();
-
-  const uint32_t waves_total = gridDim.x * kWavesPerBlock;
-  const bool random_init = p.init_mode == BO_INIT_RANDOM;
-  const uint32_t m_first = m - p.init_q;
-
-  uint32_t hc = 0;                            // this wave's outcome counts of bins 0..63, lane = bin
-  for (uint32_t base = blockIdx.x * kWavesPerBlock + wv; base < trial_count; base += waves_total * tb) {
-    if (random_init) {                       // /start (node.ts:167-188), tb trials per Philox pass
-      const uint32_t s = lane / nph, bk = lane - s * nph;
-      const uint32_t t = base + s * waves_total;
-      if (s < tb && t < trial_count) {
-        const uint64_t trial = lds_u64(keys + 2) + t;
-        const uint2 kk = lds_keys(keys);
-        const uint4 r = philox4x32_10(kk.x, kk.y, make_uint4((uint32_t)trial, (uint32_t)(trial >> 32), bk, kStreamInit << 24));
-        const uint64_t v0 = group_mask(2u * bk, m), v1 = group_mask(2u * bk + 1u, m);
-        const uint64_t x1a = ((uint64_t)r.y << 32 | r.x) & v0, x1b = ((uint64_t)r.w << 32 | r.z) & v1;
-        reinterpret_cast<uint4 *>(ring + s * WP)[bk] =
-            make_uint4((uint32_t)x1a, (uint32_t)(x1a >> 32), (uint32_t)x1b, (uint32_t)(x1b >> 32));
-      }
-    }
-    for (uint32_t s = 0; s < tb; ++s) {
-      const uint32_t t = base + s * waves_total;
-      if (t >= trial_count) break;
-      const uint2 *Xr = random_init ? ring + s * WP : ring;
-      for (uint32_t b = 0; b < NB; ++b) D[b * 64u + lane] = 0u;
-      uint32_t R = 0, M = m_first;
-      bool all_dec = false;
-      uint64_t any0 = 0, any1 = 0;            // final round's x: some live node 0 / some 1
-      for (uint32_t r = 1; r <= k_max; ++r) {
-        bool done = true;
-        // One round; ODD (M odd): no R-phase tie, so no "?" proposal and a
-        // receiver's P-phase c0 = m - c1 -- only the p1 plane is staged and
-        // counted (see p_phase_k).
-        auto round = [&](auto odd_c) {
-          constexpr bool ODD = decltype(odd_c)::value;
-          uint2 *P1 = reinterpret_cast<uint2 *>(P);   // ODD: x1-style p1 plane [XW] in P's space
-          // ---- R-phase ("proposal phase", node.ts:46-82): c1 per receiver, c0 = M - c1
-#pragma nounroll
-          for (uint32_t b = 0; b < NB; ++b) {
-            uint32_t a1[G];
-            tally_groups_x1<G>(Xr, W, a1);
-            if constexpr (ODD) {
-              const uint32_t hi_t = M >> 1;
-              uint32_t st = 0;
-              Unroll<G>::run([&](auto gi) {
-                constexpr int g = decltype(gi)::value;
-                const uint64_t p1 = vcmp_gt(a1[g], hi_t + (uint32_t)g) & group_mask(b * G + g, m);   // node.ts:63-69
-                st = writelane<2 * g>(st, (uint32_t)p1);
-                st = writelane<2 * g + 1>(st, (uint32_t)(p1 >> 32));
-              });
-              if (lane < 2u * G) reinterpret_cast<uint32_t *>(P1 + b * G)[lane] = st;
-            } else {
-              const uint32_t st = stage_proposals<false, G>(a1, b, m, M);
-              if (lane < 4u * G) reinterpret_cast<uint32_t *>(P + b * G)[lane] = st;
-            }
-          }
-          if constexpr (ODD) {                         // padding group read by the pairwise tally
-            if (lane < XW - NB * G) P1[NB * G + lane] = make_uint2(0u, 0u);
-          }
-          // ---- P-phase ("voting phase", node.ts:83-158)
-          const uint32_t mF = m > F ? m - F : 0u;
-          any0 = 0;
-          any1 = 0;
-#pragma nounroll
-          for (uint32_t b = 0; b < NB; ++b) {
-            uint32_t a0[G], a1[G];
-            if constexpr (ODD) tally_groups_x1<G>(P1, W, a1);
-            else tally_groups<G>(P, W, a0, a1);
-            uint32_t st = 0, dbb = D[b * 64u + lane];
-            Unroll<G>::run([&](auto gi) {
-              constexpr int g = decltype(gi)::value;
-              const uint64_t vm = group_mask(b * G + g, m);
-              const uint32_t Fg = F + (uint32_t)g;
-              const uint64_t d0 = (ODD ? vcmp_lt(a1[g], mF + (uint32_t)g)   // c0 = m - c1 > F
-                                       : vcmp_gt(a0[g], Fg)) & vm;          // node.ts:99
-              const uint64_t d1 = vcmp_gt(a1[g], Fg) & vm & ~d0;           // node.ts:102
-              const uint64_t rest = vm & ~(d0 | d1);
-              uint64_t x1 = d1;
-              if (rest) {
-                const uint32_t a0g = ODD ? (m + 2u * (uint32_t)g) - a1[g] : a0[g];   // bias g
-                const uint64_t ad1 = ballot_s(a1[g] > a0g) & rest;         // node.ts:108-109
-                const uint64_t tie = ballot_s(a1[g] == a0g) & rest;        // node.ts:110-111
-                x1 |= ad1;
-                if (tie) {                                                // node.ts:111
-                  const uint64_t trial = lds_u64(keys + 2) + t;
-                  const uint32_t *ids = reinterpret_cast<const uint32_t *>((uintptr_t)lds_u64(keys + 4));
-                  x1 |= coin_ballot(keys, (uint32_t)trial, (uint32_t)(trial >> 32), ids, b * G + g, r, tie);
-                }
-              }
-              st = writelane<2 * g>(st, (uint32_t)x1);
-              st = writelane<2 * g + 1>(st, (uint32_t)(x1 >> 32));
-              dbb = select_lanes(dbb, dbb | (1u << g), d0 | d1);           // sticky decided bit (node.ts:100-105)
-              any1 |= x1;
-              any0 |= vm & ~x1;
-              asm volatile("" : "+s"(any0), "+s"(any1));                   // fold per group
-            });
-            D[b * 64u + lane] = dbb;
-            if (lane < 2u * G) reinterpret_cast<uint32_t *>(X + b * G)[lane] = st;
-            // groups of this block that hold live receivers for this lane
-            const uint32_t j0 = b * G;
-            uint32_t expect = 0u;
-            if (j0 + 1u < W) {
-              const uint32_t nfull = (W - 1u - j0) < (uint32_t)G ? (W - 1u - j0) : (uint32_t)G;
-              expect = nfull >= 32u ? ~0u : ((1u << nfull) - 1u);
-            }
-            if (W - 1u >= j0 && W - 1u < j0 + G && lane < tail_n) expect |= 1u << (W - 1u - j0);
-            done = done && __all((dbb & expect) == expect);
-          }
-        };
-        if (M & 1u) round(std::true_type{});
-        else round(std::false_type{});
-        Xr = X;
-        M = m;
-        R = r;
-        all_dec = done;
-        if (all_dec) break;
-      }
-      // ---- outcome
-      const uint32_t v = (any0 && any1) ? 2u : (any1 ? 1u : 0u);
-      const uint32_t bin = all_dec ? (R * 3u + v) : v;
-      if (bin < 64u) hc += (lane == bin) ? 1u : 0u;
-      else if (lane == 0) atomicAdd(&lhist[bin], 1u);
-      if (all_dec && v == 2u && lane == 0) atomicAdd(&lhist[hist_len - 1u], 1u);
-      if constexpr (STATE) {
-        if (lane == 0 && p.rounds_out) *p.rounds_out = all_dec ? R : 0u;
-        if (p.node_out) {
-          for (uint32_t c = lane; c < m; c += 64u) {
-            const uint32_t j = c >> 6;
-            const uint2 q = Xr[j];
-            const uint64_t x1 = (uint64_t)q.y << 32 | q.x;
-            bo_node_state ns;
-            ns.killed = 0;
-            ns.x = (int8_t)((x1 >> lane) & 1ull);
-            ns.decided = (int8_t)((D[(j / G) * 64u + lane] >> (j % G)) & 1u);
-            ns.pad = 0;
-            ns.k = (int32_t)R + 1;
-            p.node_out[p.live_ids[c]] = ns;
-          }
-        }
-      }
-    }
-  }
-
-  if (hc) atomicAdd(&lhist[lane], hc);
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) {
-    const uint32_t c = lhist[i];
-    if (c) atomicAdd(&p.hist[i], (unsigned long long)c);
-  }
-}
-
 
 // ------------------------------------------------ packed kernel (m <= 32)
 // Small networks (BASELINE configs C1 N=5, C2 N=10, and the C5 sweep's small
@@ -1570,24 +701,6 @@ void plan_geometry(KParams &p) {
   p.lds_bytes = p.hist_bytes + kWavesPerBlock * p.wave_bytes;
 }
 
-template <int W>
-static hipError_t launch_w(const KParams &p, int grid, hipStream_t s) {
-  if (p.node_out || p.rounds_out)
-    hipLaunchKernelGGL((benor_lockstep_w_kernel<W, true>), dim3(grid), dim3(64 * kWavesPerBlock), p.lds_bytes, s, p);
-  else
-    hipLaunchKernelGGL((benor_lockstep_w_kernel<W, false>), dim3(grid), dim3(64 * kWavesPerBlock), p.lds_bytes, s, p);
-  return hipGetLastError();
-}
-
-template <int G>
-static hipError_t launch_b(const KParams &p, int grid, hipStream_t s) {
-  if (p.node_out || p.rounds_out)
-    hipLaunchKernelGGL((benor_lockstep_blocked_kernel<G, true>), dim3(grid), dim3(64 * kWavesPerBlock), p.lds_bytes, s, p);
-  else
-    hipLaunchKernelGGL((benor_lockstep_blocked_kernel<G, false>), dim3(grid), dim3(64 * kWavesPerBlock), p.lds_bytes, s, p);
-  return hipGetLastError();
-}
-
 template <int... Is>
 static hipError_t dispatch_w(const KParams &p, int grid, hipStream_t s, std::integer_sequence<int, Is...>) {
   hipError_t e = hipErrorInvalidValue;
@@ -1595,11 +708,11 @@ static hipError_t dispatch_w(const KParams &p, int grid, hipStream_t s, std::int
   return e;
 }
 
-// W in 17..64: G = ceil(W / ceil(W/16)) in 9..16
+// W in 33..64: G = ceil(W / ceil(W/16)) in 11..16
 template <int... Is>
 static hipError_t dispatch_b(const KParams &p, int grid, hipStream_t s, std::integer_sequence<int, Is...>) {
   hipError_t e = hipErrorInvalidValue;
-  (void)((p.G == (uint32_t)(Is + 9) ? (e = launch_b<Is + 9>(p, grid, s), true) : false) || ...);
+  (void)((p.G == (uint32_t)(Is + 11) ? (e = launch_b<Is + 11>(p, grid, s), true) : false) || ...);
   return e;
 }
 
@@ -1622,7 +735,7 @@ hipError_t launch_lockstep(const KParams &p, int grid, hipStream_t s) {
     return hipGetLastError();
   }
   if (p.variant == 1) return dispatch_w(p, grid, s, std::make_integer_sequence<int, kMaxWSpecialised>{});
-  return dispatch_b(p, grid, s, std::make_integer_sequence<int, 8>{});
+  return dispatch_b(p, grid, s, std::make_integer_sequence<int, 6>{});
 }
 
 int lockstep_grid(const KParams &p, int device) {

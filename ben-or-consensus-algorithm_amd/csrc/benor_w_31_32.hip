@@ -1,0 +1,8 @@
+// W kernel instantiations W = 31..32 (see benor_w_kernel.h); split so the
+// unrolled instantiations (compile time ~ W^2) build in parallel.
+#include "benor_w_kernel.h"
+
+namespace benor {
+template hipError_t launch_w<31>(const KParams &, int, hipStream_t);
+template hipError_t launch_w<32>(const KParams &, int, hipStream_t);
+}  // namespace benor
