@@ -64,15 +64,21 @@ def test_random_batches_match_oracle(N, F, trials, k_max):
     np.testing.assert_array_equal(got, ref.hist)
 
 
-@pytest.mark.parametrize("N,F", [(12, 4), (16, 6), (9, 3), (64, 2)])
-def test_random_fault_placement_states(N, F):
+@pytest.mark.parametrize("N,F,reps", [(12, 4, 30), (16, 6, 30), (9, 3, 30), (64, 2, 30),
+                                      # per-node state from the W kernel at W = 17, 32 and the blocked kernel
+                                      (1090, 2, 4), (2047, 1, 3), (2600, 300, 3), (4096, 0, 2)])
+def test_random_fault_placement_states(N, F, reps):
     """Fault placement is arbitrary (faultyList); per-node states must match."""
     rng = np.random.default_rng(N + 31 * F)
-    for t in range(30):
+    for t in range(reps):
         fl = [False] * N
         for i in rng.choice(N, F, replace=False):
             fl[i] = True
         init = [int(v) for v in rng.integers(0, 2, N)]
+        if N > 1000 and t % 2 == 1:        # tied start (m even): round 1 proposes "?", coins decide
+            live = [i for i in range(N) if not fl[i]]
+            ones = set(int(i) for i in rng.choice(live, len(live) // 2, replace=False))
+            init = [1 if i in ones else 0 for i in range(N)]
         seed = int(rng.integers(0, 2**63))
         ref = oracle.run_trials(N, F, fl, seed=seed, trial_begin=t, trial_count=1, k_max=20,
                                 initial_values=init, want_states=True).states
