@@ -12,11 +12,13 @@ of the GPU count.
 value  = live node-rounds simulated by all ranks / timed seconds (max over ranks)
          (a live node-round = one live node executing one R-phase and one
          P-phase: SURVEY §8d primary count)
-roofline: per-receiver tally popcount words (3 * ceil(m/32) per live
-         node-round, m = N - F live nodes: c1 in the R-phase, c0 and c1 in the
-         P-phase) / average kernel duration from HIP events on the
-         launch stream, against the gfx950 v_bcnt_u32_b32 issue peak
-         (256 CU x 4 SIMD x 16 lanes x 2.4 GHz = 39.3 T words/s).
+roofline: per-receiver tally popcount words per live node-round (m = N - F
+         live nodes: c1 in the R-phase; c1 in the P-phase when the binary vote
+         count is odd -- no "?" proposal, c0 = m - c1 -- else c0 and c1: 2 or
+         3 * ceil(m/32), 44 at the bench shape) / average kernel
+         duration from HIP events on the launch stream, against the gfx950
+         v_bcnt_u32_b32 issue peak (256 CU x 4 SIMD x 16 lanes x 2.4 GHz =
+         39.3 T words/s).
 cpu_baseline: the oracle's bit-plane restatement (oracle/benor_oracle.c,
          OpenMP over trials) on a bounded sample, rank 0 at N = 1 only.
 

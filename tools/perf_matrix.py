@@ -3,7 +3,8 @@
 For each (N, F, f, mode) -- mode 0 lockstep, 1 random delivery, 2 event level -- runs `trials` trials once for warm-up and once timed
 with HIP events on the launch stream, and prints live node-rounds/s and the
 popcount-roofline fraction (the plan's algorithmic popcount words per live
-node-round -- 3*ceil(m/32) lockstep, 4*ceil(m/32) random delivery -- vs the
+node-round -- 2 or 3 * ceil(m/32) lockstep (odd / even vote count), 4 * ceil(m/32)
+random delivery -- vs the
 v_bcnt issue peak, 39.3 T/s).  One JSON line per shape.
 
     python tools/perf_matrix.py [--quick]
