@@ -173,8 +173,9 @@ __global__ void __launch_bounds__(256) benor_lockstep_blocked_kernel(KParams p) 
         // One round; ODD (M odd): no R-phase tie, so no "?" proposal and a
         // receiver's P-phase c0 = m - c1 -- only the p1 plane is staged and
         // counted (see p_phase_k).
-        auto round = [&](auto odd_c) {
+        auto round = [&](auto odd_c, auto sure_c) {
           constexpr bool ODD = decltype(odd_c)::value;
+          constexpr bool SURE = decltype(sure_c)::value;   // ODD and m > 2F: every receiver decides (decide_k)
           uint2 *P1 = reinterpret_cast<uint2 *>(P);   // ODD: x1-style p1 plane [XW] in P's space
           // ---- R-phase ("proposal phase", node.ts:46-82): c1 per receiver, c0 = M - c1
 #pragma nounroll
@@ -215,7 +216,7 @@ __global__ void __launch_bounds__(256) benor_lockstep_blocked_kernel(KParams p) 
               const uint32_t Fg = F + (uint32_t)g;
               const uint64_t d0 = (ODD ? vcmp_lt(a1[g], mF + (uint32_t)g)   // c0 = m - c1 > F
                                        : vcmp_gt(a0[g], Fg)) & vm;          // node.ts:99
-              const uint64_t d1 = vcmp_gt(a1[g], Fg) & vm & ~d0;           // node.ts:102
+              const uint64_t d1 = (SURE ? vm : vcmp_gt(a1[g], Fg) & vm) & ~d0;   // node.ts:102
               const uint64_t rest = vm & ~(d0 | d1);
               uint64_t x1 = d1;
               if (rest) {
@@ -249,8 +250,9 @@ __global__ void __launch_bounds__(256) benor_lockstep_blocked_kernel(KParams p) 
             done = done && __all((dbb & expect) == expect);
           }
         };
-        if (M & 1u) round(std::true_type{});
-        else round(std::false_type{});
+        if (!(M & 1u)) round(std::false_type{}, std::false_type{});
+        else if (m > 2u * F) round(std::true_type{}, std::true_type{});
+        else round(std::true_type{}, std::false_type{});
         Xr = X;
         M = m;
         R = r;

@@ -317,11 +317,15 @@ __device__ __forceinline__ void p_phase_k(const uint32_t (&c1r)[K][W], uint32_t 
 
 // Decisions (node.ts:99-105) of K trials: whether some live receiver stays
 // undecided, and which values were decided.  ODD: c0 = m - c1, so
-// "c0 > F" is "c1 < m - F" (no c0 tally exists).  Chain bias g throughout.
-template <bool ODD, int W, int K>
+// "c0 > F" is "c1 < m - F" (no c0 tally exists).  SURE (ODD and m > 2F):
+// c1 < m - F or c1 >= m - F > F, so every receiver decides -- 0 if
+// c1 < m - F, else 1 -- and one compare per group gives both masks.
+// Chain bias g throughout.
+template <bool ODD, bool SURE, int W, int K>
 __device__ __forceinline__ void decide_k(const uint32_t (&a0)[K][W], const uint32_t (&a1)[K][W], uint32_t m,
                                          uint32_t F, uint64_t tailm, uint64_t (&rest_any)[K], uint64_t (&any0)[K],
                                          uint64_t (&any1)[K]) {
+  static_assert(ODD || !SURE, "SURE needs binary votes");
   const uint32_t mF = m > F ? m - F : 0u;
 #pragma unroll
   for (int k = 0; k < K; ++k) rest_any[k] = any0[k] = any1[k] = 0;
@@ -332,12 +336,18 @@ __device__ __forceinline__ void decide_k(const uint32_t (&a0)[K][W], const uint3
       constexpr int k = decltype(ki)::value;
       const uint64_t d0 = (ODD ? vcmp_lt(a1[k][g], mF + (uint32_t)g)           // node.ts:99
                                : vcmp_gt(a0[k][g], F + (uint32_t)g)) & vm;
-      const uint64_t d1 = vcmp_gt(a1[k][g], F + (uint32_t)g) & vm & ~d0;      // node.ts:102
-      rest_any[k] |= vm & ~(d0 | d1);
-      any0[k] |= d0;
-      any1[k] |= d1;
-      // fold now: otherwise the ORs sink to the loop exit and all 2W masks stay live
-      asm volatile("" : "+s"(rest_any[k]), "+s"(any0[k]), "+s"(any1[k]));
+      if constexpr (SURE) {
+        any0[k] |= d0;
+        any1[k] |= vm & ~d0;                                                  // node.ts:102
+        asm volatile("" : "+s"(any0[k]), "+s"(any1[k]));
+      } else {
+        const uint64_t d1 = vcmp_gt(a1[k][g], F + (uint32_t)g) & vm & ~d0;    // node.ts:102
+        rest_any[k] |= vm & ~(d0 | d1);
+        any0[k] |= d0;
+        any1[k] |= d1;
+        // fold now: otherwise the ORs sink to the loop exit and all 2W masks stay live
+        asm volatile("" : "+s"(rest_any[k]), "+s"(any0[k]), "+s"(any1[k]));
+      }
     });
   });
 }

@@ -103,10 +103,11 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
         const bool odd = M & 1u;
         if (odd) {
           p_phase_k<true, W, 1>(c1v, M, tailm, a0, a1);
-          decide_k<true, W, 1>(a0, a1, m, F, tailm, rest_any, any0_, any1_);
+          if (m > 2u * F) decide_k<true, true, W, 1>(a0, a1, m, F, tailm, rest_any, any0_, any1_);
+          else decide_k<true, false, W, 1>(a0, a1, m, F, tailm, rest_any, any0_, any1_);
         } else {
           p_phase_k<false, W, 1>(c1v, M, tailm, a0, a1);
-          decide_k<false, W, 1>(a0, a1, m, F, tailm, rest_any, any0_, any1_);
+          decide_k<false, false, W, 1>(a0, a1, m, F, tailm, rest_any, any0_, any1_);
         }
         R = r;                                                        // node.ts:147  k = r + 1
         any0 = any0_[0];
@@ -226,10 +227,11 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
           uint64_t rest_any[K], any0[K], any1[K];
           if (m_first & 1u) {
             p_phase_k<true, W, K>(c1, m_first, tailm, a0, a1);
-            decide_k<true, W, K>(a0, a1, m, F, tailm, rest_any, any0, any1);
+            if (m > 2u * F) decide_k<true, true, W, K>(a0, a1, m, F, tailm, rest_any, any0, any1);
+            else decide_k<true, false, W, K>(a0, a1, m, F, tailm, rest_any, any0, any1);
           } else {
             p_phase_k<false, W, K>(c1, m_first, tailm, a0, a1);
-            decide_k<false, W, K>(a0, a1, m, F, tailm, rest_any, any0, any1);
+            decide_k<false, false, W, K>(a0, a1, m, F, tailm, rest_any, any0, any1);
           }
           slow = 0u;
           nk = K;
