@@ -17,7 +17,7 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
   constexpr int NPH = (W + 1) / 2;          // Philox blocks per trial (2 plane words each)
   constexpr int TB = 64 / NPH;              // trials per init batch
   constexpr int WP = 2 * NPH;               // x1 words per plane row, padded to 16 bytes
-  constexpr int K = W <= 2 ? 4 : (W <= kPairMaxW ? 2 : 1);   // trials whose round 1 runs interleaved
+  constexpr int K = W <= 2 ? 4 : (W <= 6 ? 3 : (W <= kPairMaxW ? 2 : 1));   // trials whose round 1 runs interleaved
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // uniform: scalar trial loop
