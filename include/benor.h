@@ -152,9 +152,12 @@ int bo_plan_launch(bo_plan *plan, uint64_t trial_begin, uint64_t trial_count,
 /* Same, blocking, host histogram (added into hist_host). */
 int bo_plan_run(bo_plan *plan, uint64_t trial_begin, uint64_t trial_count, uint64_t *hist_host);
 
-/* Work of one launch in the roofline's algorithmic unit: VALU popcount words
- * that the per-receiver tallies of one live node-round need (2 phases x
- * 2 counts x ceil(m/32) words, m = live nodes). */
+/* The roofline's algorithmic unit: VALU popcount words that the per-receiver
+ * tallies of one live node-round need, m = live nodes, M = m - (number of "?"
+ * initial values) binary votes.  LOCKSTEP / EVENT: the R-phase counts c1
+ * (c0 = M - c1); the P-phase counts c1 when M is odd (no tie, so no "?"
+ * proposal: c0 = m - c1) and c0, c1 otherwise -- 2 or 3 x ceil(m/32).
+ * RANDOM_DELIVERY: both values in both phases, 4 x ceil(m/32). */
 uint64_t bo_plan_popc_words_per_node_round(const bo_plan *plan);
 uint32_t bo_plan_live_nodes(const bo_plan *plan);
 
