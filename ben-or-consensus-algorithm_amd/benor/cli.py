@@ -28,13 +28,14 @@ import time
 import numpy as np
 
 
+def _int(text: str) -> int:
+    """A decimal integer, or a power written a**b (e.g. 2**30)."""
+    base, sep, exp = text.strip().partition("**")
+    return int(base) ** int(exp) if sep else int(base)
+
+
 def _ints(s: str) -> list[int]:
-    out = []
-    for part in s.split(","):
-        part = part.strip()
-        if part:
-            out.append(int(eval(part, {"__builtins__": {}})))   # allows 2**30 style
-    return out
+    return [_int(part) for part in s.split(",") if part.strip()]
 
 
 def summarize(hist: np.ndarray, N: int, F: int, k_max: int) -> dict:
@@ -105,7 +106,7 @@ def cmd_sweep(a) -> int:
     Ns = _ints(a.N)
     phis = [i * 0.5 / a.steps for i in range(a.steps)]
     cells = [(N, int(phi * N)) for N in Ns for phi in phis]
-    per_cell = max(1, int(eval(str(a.trials), {"__builtins__": {}})) // len(cells))
+    per_cell = max(1, _int(str(a.trials)) // len(cells))
     rows = []
     t0 = time.perf_counter()
     stream = torch.cuda.current_stream()
