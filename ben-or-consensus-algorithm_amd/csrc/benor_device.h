@@ -101,14 +101,6 @@ __device__ __forceinline__ uint64_t coin_ballot(const uint32_t *keys, uint32_t t
   return coin_ballot(k.x, k.y, tlo, thi, live_ids, group, round, tie);
 }
 
-// A call's result comes back in VGPRs; the ballot is wave-uniform, so move it
-// to SGPRs for the mask arithmetic that follows.
-__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
-  return (uint64_t)hi << 32 | lo;
-}
-
 // ------------------------------------------- W-specialised kernel (m <= 1024)
 // For networks of at most 1024 live nodes (W <= 16 receiver groups) the whole
 // round is unrolled at compile time: every receiver group's tally chain is a

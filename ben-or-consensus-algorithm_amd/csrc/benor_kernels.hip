@@ -9,16 +9,17 @@
 //     no barriers, no inter-wave traffic and no HBM traffic in the round loop;
 //   * lane l of receiver group j is live node c = 64 j + l (compact order of
 //     live node ids); crashed nodes (node.ts:45,171) own no lane and no bit;
-//   * a phase's messages are two bit planes over the m live senders,
-//     {is0, is1}, produced by wave ballots and kept in the wave's LDS slice as
-//     16-byte records {is0.lo, is0.hi, is1.lo, is1.hi} per 64 senders;
+//   * a phase's messages are bit planes over the m live senders produced by
+//     wave ballots (v_cmp -> SGPR lane mask): x planes carry is1 only (every
+//     x is 0 or 1 after /start), proposal planes is0 and is1 ("?" is
+//     neither) -- or is1 only when the vote count is odd and no "?" exists;
 //   * every live receiver tallies its own inbox with v_bcnt_u32_b32
-//     (popcount + accumulate, one VALU op per 32 senders per count), reading
-//     each record once per wave with a broadcast ds_read_b128 and applying it
-//     to G receiver groups per lane;
+//     (popcount + accumulate, one VALU op per 32 senders per count), taking
+//     each plane word as an SGPR straight from the ballot (W kernel) or from
+//     a broadcast LDS read, and applying it to every receiver group of the lane;
 //   * per-node coins (node.ts:111) and random initial values come from
 //     Philox4x32-10 keyed by (seed, global trial id, node id, round);
-//   * each trial's outcome is one increment of an LDS histogram, flushed to
+//   * each trial's outcome is one increment of a per-wave counter, flushed to
 //     HBM with one atomic per non-zero bin per workgroup.
 //
 // Per-receiver tallies are the simulated unit (SURVEY §7 "symmetry trap"):

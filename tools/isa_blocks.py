@@ -12,7 +12,9 @@ from collections import Counter
 
 def blocks(path, sym):
     lines = open(path).read().split("\n")
-    start = next(i for i, l in enumerate(lines) if l.startswith("_Z") and sym in l and l.rstrip().endswith(":") or (sym in l and l.split(":")[0].startswith("_Z") and ":" in l and not l.startswith("\t")))
+    # the function's label line: "<mangled name>:" (optionally followed by a comment)
+    start = next(i for i, l in enumerate(lines)
+                 if l.startswith("_Z") and sym in l.split(":", 1)[0] and ":" in l)
     cur, out = "entry", []
     cnt = Counter()
     for l in lines[start + 1:]:
