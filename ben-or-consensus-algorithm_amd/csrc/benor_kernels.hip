@@ -224,12 +224,25 @@ struct DStream {
 };
 
 // One Floyd step: sender t, else (t already in the subset) sender jj, joins
-// the lane's bitset ([word][lane] in LDS).  ds_or: LDS ops of a wave retire
-// in order, so the next step's read sees this one.
-__device__ __forceinline__ void floyd_insert(uint32_t *__restrict__ B, uint32_t lane, uint32_t t, uint32_t jj) {
-  const uint32_t cur = B[(t >> 5) * 64u + lane];
-  const uint32_t idx = ((cur >> (t & 31u)) & 1u) ? jj : t;
-  atomicOr(&B[(idx >> 5) * 64u + lane], 1u << (idx & 31u));
+// the lane's bitset ([word][lane] in LDS, `lb` = this lane's byte offset).
+// ds_or: LDS ops of a wave retire in order, so the next step's read sees this
+// one.  Branch-free: idx = t + set * (jj - t) (t <= jj), and the shifts use the
+// hardware's low-5-bit shift amounts.
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+// LDS byte address of the bitset word holding `bit` for this lane:
+// (bit >> 5) * 256 + lbase, lbase = the bitset's LDS address + lane * 4.
+__device__ __forceinline__ lds_u32 *bitset_word(uint32_t bit, uint32_t lbase) {
+  uint32_t a;                                          // v_lshrrev + v_lshl_add
+  asm("v_lshl_add_u32 %0, %1, 8, %2" : "=v"(a) : "v"(bit >> 5), "v"(lbase));
+  return (lds_u32 *)(uintptr_t)a;
+}
+
+__device__ __forceinline__ void floyd_insert(uint32_t lbase, uint32_t t, uint32_t jj) {
+  const uint32_t cur = *bitset_word(t, lbase);
+  const uint32_t set = __builtin_amdgcn_ubfe(cur, t, 1u);     // v_bfe_u32 reads offset bits [4:0]
+  const uint32_t idx = t + __umul24(set, jj - t);
+  __hip_atomic_fetch_or(bitset_word(idx, lbase), 1u << (idx & 31u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 
 __device__ __forceinline__ void random_tally(const uint4 *__restrict__ plane, uint32_t *__restrict__ B,
@@ -247,6 +260,7 @@ __device__ __forceinline__ void random_tally(const uint4 *__restrict__ plane, ui
   // Lemire's exact rejection test; otherwise one exact DStream step (same
   // words, same result -- the oracle's definition).
   const uint32_t c2 = node & 0xFFFu, c3 = (r & 0xFFFFFu) | ((phase & 1u) << 20) | (kStreamDelivery << 24);
+  const uint32_t lb = (uint32_t)(uintptr_t)(lds_u32 *)B + lane * 4u;   // LDS address of this lane's word 0
   uint32_t jj = m - k, widx = 0;
   for (;;) {
     const bool go = active && jj < m;
@@ -254,16 +268,24 @@ __device__ __forceinline__ void random_tally(const uint4 *__restrict__ plane, ui
     bool fast = go && (widx & 3u) == 0u;
     if (fast) {
       const uint4 b = philox4x32_10(k0, k1, make_uint4(tlo, thi, c2 | ((widx >> 2) << 12), c3));
-      const uint32_t n = m - jj < 4u ? m - jj : 4u;            // draws left in this subset
       const uint64_t q0 = (uint64_t)b.x * (jj + 1u), q1 = (uint64_t)b.y * (jj + 2u);
       const uint64_t q2 = (uint64_t)b.z * (jj + 3u), q3 = (uint64_t)b.w * (jj + 4u);
-      const bool rej = (uint32_t)q0 < jj + 1u || (n > 1u && (uint32_t)q1 < jj + 2u) ||
-                       (n > 2u && (uint32_t)q2 < jj + 3u) || (n > 3u && (uint32_t)q3 < jj + 4u);
-      if (!rej) {
-        floyd_insert(B, lane, (uint32_t)(q0 >> 32), jj);
-        if (n > 1u) floyd_insert(B, lane, (uint32_t)(q1 >> 32), jj + 1u);
-        if (n > 2u) floyd_insert(B, lane, (uint32_t)(q2 >> 32), jj + 2u);
-        if (n > 3u) floyd_insert(B, lane, (uint32_t)(q3 >> 32), jj + 3u);
+      // Lemire's exact test is needed only when a low word is below its range;
+      // ranges grow with i, so one compare of the smallest low word against the
+      // largest range is a safe screen (it may send a block to the exact path
+      // needlessly, never the other way).
+      const uint32_t lmin = min(min((uint32_t)q0, (uint32_t)q1), min((uint32_t)q2, (uint32_t)q3));
+      if (lmin >= jj + 4u) {
+        const uint32_t n = m - jj < 4u ? m - jj : 4u;          // draws left in this subset
+        floyd_insert(lb, (uint32_t)(q0 >> 32), jj);
+        if (n == 4u) {                                          // the common case: no per-step branch
+          floyd_insert(lb, (uint32_t)(q1 >> 32), jj + 1u);
+          floyd_insert(lb, (uint32_t)(q2 >> 32), jj + 2u);
+          floyd_insert(lb, (uint32_t)(q3 >> 32), jj + 3u);
+        } else {                                                // the subset's last block
+          if (n > 1u) floyd_insert(lb, (uint32_t)(q1 >> 32), jj + 1u);
+          if (n > 2u) floyd_insert(lb, (uint32_t)(q2 >> 32), jj + 2u);
+        }
         jj += n;
         widx += n;
       } else {
@@ -276,7 +298,7 @@ __device__ __forceinline__ void random_tally(const uint4 *__restrict__ plane, ui
       ds.widx = widx & ~3u;                                      // refill the current block, then skip to widx
       for (uint32_t i = ds.widx; i < widx; ++i) (void)ds.next();
       const uint32_t t = ds.uniform(jj + 1u);
-      floyd_insert(B, lane, t, jj);
+      floyd_insert(lb, t, jj);
       widx = ds.widx;
       ++jj;
     }
