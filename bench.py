@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--trials", type=int, default=100_000_000, help="trials per GPU per step")
     ap.add_argument("--k-max", type=int, default=16)
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x243F6A8885A308D3)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget (0 = skip)")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample budget (0 = skip)")
     ap.add_argument("--no-peak-probe", action="store_true")
     return ap.parse_args()
 
