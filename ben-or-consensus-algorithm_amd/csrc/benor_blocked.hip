@@ -10,6 +10,16 @@ namespace benor {
 // ceil(W/NB), padding < NB groups); the record loop over the W plane words is
 // a runtime loop.  Per-lane `decided` bits live in registers (one word per
 // block).  Otherwise as the W-specialised kernel.
+// Word-major tallies: each plane word is applied to all G receiver groups
+// before the next word, so consecutive v_bcnt are independent (tally_ordered
+// keeps that order; see benor_device.h).
+template <int G>
+__device__ __forceinline__ void add_word(uint32_t word, uint32_t (&a)[G]) {
+#pragma unroll
+  for (int g = 0; g < G; ++g) a[g] = tally_ordered(word, a[g]);
+}
+
+// P-phase tally over W {p0.lo, p0.hi, p1.lo, p1.hi} records (runtime W).
 template <int G>
 __device__ __forceinline__ void tally_groups(const uint4 *__restrict__ plane, uint32_t W, uint32_t (&a0)[G],
                                              uint32_t (&a1)[G]) {
@@ -17,45 +27,23 @@ __device__ __forceinline__ void tally_groups(const uint4 *__restrict__ plane, ui
   Unroll<G>::run([&](auto gi) {
     constexpr int g = decltype(gi)::value;
     a0[g] = tally_first<g>(q.x);
+  });
+  Unroll<G>::run([&](auto gi) {
+    constexpr int g = decltype(gi)::value;
     a1[g] = tally_first<g>(q.z);
   });
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    a0[g] = tally(q.y, a0[g]);
-    a1[g] = tally(q.w, a1[g]);
-  }
-  uint32_t w = 1;
-  for (; w + 1 < W; w += 2) {
+  add_word<G>(q.y, a0);
+  add_word<G>(q.w, a1);
+  for (uint32_t w = 1; w < W; ++w) {
     const uint4 u = plane[w];
-    const uint4 v = plane[w + 1];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      a0[g] = tally(u.x, a0[g]);
-      a1[g] = tally(u.z, a1[g]);
-      a0[g] = tally(u.y, a0[g]);
-      a1[g] = tally(u.w, a1[g]);
-    }
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      a0[g] = tally(v.x, a0[g]);
-      a1[g] = tally(v.z, a1[g]);
-      a0[g] = tally(v.y, a0[g]);
-      a1[g] = tally(v.w, a1[g]);
-    }
-  }
-  if (w < W) {
-    const uint4 u = plane[w];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      a0[g] = tally(u.x, a0[g]);
-      a1[g] = tally(u.z, a1[g]);
-      a0[g] = tally(u.y, a0[g]);
-      a1[g] = tally(u.w, a1[g]);
-    }
+    add_word<G>(u.x, a0);
+    add_word<G>(u.z, a1);
+    add_word<G>(u.y, a0);
+    add_word<G>(u.w, a1);
   }
 }
 
-// R-phase x1-only tally over the W words of a plane (runtime W, pairs of
+// c1-only tally over the W words of an x1-style plane (runtime W, pairs of
 // groups per 16-byte read; WP = W rounded up to even, padding words zero).
 template <int G>
 __device__ __forceinline__ void tally_groups_x1(const uint2 *__restrict__ plane, uint32_t W, uint32_t (&a1)[G]) {
@@ -65,22 +53,16 @@ __device__ __forceinline__ void tally_groups_x1(const uint2 *__restrict__ plane,
     constexpr int g = decltype(gi)::value;
     a1[g] = tally_first<g>(q.x);
   });
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    a1[g] = tally(q.y, a1[g]);
-    a1[g] = tally(q.z, a1[g]);
-    a1[g] = tally(q.w, a1[g]);
-  }
+  add_word<G>(q.y, a1);
+  add_word<G>(q.z, a1);
+  add_word<G>(q.w, a1);
   const uint32_t np = (W + 1u) >> 1;
   for (uint32_t w = 1; w < np; ++w) {
-    const uint4 s = q4[w];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      a1[g] = tally(s.x, a1[g]);
-      a1[g] = tally(s.y, a1[g]);
-      a1[g] = tally(s.z, a1[g]);
-      a1[g] = tally(s.w, a1[g]);
-    }
+    const uint4 u = q4[w];
+    add_word<G>(u.x, a1);
+    add_word<G>(u.y, a1);
+    add_word<G>(u.z, a1);
+    add_word<G>(u.w, a1);
   }
 }
 

@@ -37,6 +37,16 @@ __device__ __forceinline__ uint32_t tally(uint32_t word, uint32_t acc) {
   return r;
 }
 
+// Same, kept in source order (asm volatile).  For the runtime-W tally loops:
+// left free, the scheduler turns the word-major order (G independent ops per
+// word) into dependent per-group chains, and the hazard recognizer then puts
+// an s_nop between each dependent pair of inline asms it cannot see into.
+__device__ __forceinline__ uint32_t tally_ordered(uint32_t word, uint32_t acc) {
+  uint32_t r;
+  asm volatile("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(word), "v"(acc));
+  return r;
+}
+
 __device__ __forceinline__ uint64_t group_mask(uint32_t j, uint32_t m) {
   const uint32_t lo = j * 64u;
   if (lo >= m) return 0ull;
