@@ -13,8 +13,8 @@ and prints every node's state.
 `sweep` runs the decision-round phase diagram: every N in the list crossed
 with F = floor(phi * N), phi on a `--steps` grid in [0, 0.5); the total trial
 budget is split evenly over cells, each cell's trials split across ranks
-(torch.distributed, one process per GPU) and merged with one all-reduce per
-cell.  Rows: N, F, m, trials, decided fraction, E[R], P(R = 1..4), P(v = 1),
+(torch.distributed, one process per GPU).  All cells are launched back to back
+into one [cells, H] histogram buffer, merged with a single all-reduce.  Rows: N, F, m, trials, decided fraction, E[R], P(R = 1..4), P(v = 1),
 undecided, agreement violations.
 """
 from __future__ import annotations
@@ -107,19 +107,21 @@ def cmd_sweep(a) -> int:
     phis = [i * 0.5 / a.steps for i in range(a.steps)]
     cells = [(N, int(phi * N)) for N in Ns for phi in phis]
     per_cell = max(1, _int(str(a.trials)) // len(cells))
-    rows = []
     t0 = time.perf_counter()
     stream = torch.cuda.current_stream()
-    for ci, (N, F) in enumerate(cells):
-        plan = benor.TrialsPlan(N, F, seed=a.seed ^ (N << 20) ^ F, k_max=a.k_max)
-        h = torch.zeros(plan.hist_len, dtype=torch.int64, device="cuda")
-        b, n = strong_range(0, per_cell, rank, world)
-        plan.launch(b, n, h.data_ptr(), stream.cuda_stream)
-        merge_histogram(h)
-        hist = h.cpu().numpy().astype(np.uint64)
-        rows.append(summarize(hist, N, F, a.k_max))
+    # Every cell's plan first, then all launches back to back into one [cells, H]
+    # histogram buffer, then ONE all-reduce over ranks and one read-back.
+    plans = [benor.TrialsPlan(N, F, seed=a.seed ^ (N << 20) ^ F, k_max=a.k_max) for (N, F) in cells]
+    H = plans[0].hist_len
+    hists = torch.zeros((len(cells), H), dtype=torch.int64, device="cuda")
+    b, n = strong_range(0, per_cell, rank, world)
+    for ci, plan in enumerate(plans):
+        plan.launch(b, n, hists[ci].data_ptr(), stream.cuda_stream)
         if rank == 0 and a.progress:
-            print(f"[{ci + 1}/{len(cells)}] N={N} F={F} {time.perf_counter() - t0:.1f}s", file=sys.stderr, flush=True)
+            print(f"[{ci + 1}/{len(cells)}] N={cells[ci][0]} F={cells[ci][1]} queued", file=sys.stderr, flush=True)
+    merge_histogram(hists)
+    allh = hists.cpu().numpy().astype(np.uint64)
+    rows = [summarize(allh[ci], N, F, a.k_max) for ci, (N, F) in enumerate(cells)]
     elapsed = time.perf_counter() - t0
     if rank == 0:
         keys = list(rows[0].keys())
