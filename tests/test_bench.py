@@ -57,13 +57,16 @@ def test_bench_single_gpu_line():
 
 
 @pytest.mark.gpu
-def test_bench_two_ranks_gloo_one_gpu():
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_bench_ranks_gloo_one_gpu(ranks):
     env = dict(os.environ, BENOR_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
-           "--steps", "2", "--warmup", "1", "--trials", "2000000", "--no-peak-probe"]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(ranks),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", str(ranks),
+           "--steps", "2", "--warmup", "1", "--trials", "1000000", "--no-peak-probe"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     d = _json_line(r.stdout)
-    assert d["n_gpus"] == 2 and d["scaling"] == "weak"
-    assert d["trials_per_s"] > 0 and "cpu_baseline" not in d
+    assert d["n_gpus"] == ranks and d["scaling"] == "weak"
+    # every rank ran its own 10^6 trials per step; rank 0's merged histogram saw them all
+    assert d["trials_per_s"] * d["ms_per_step"] * 1e-3 == pytest.approx(ranks * 1_000_000, rel=1e-6)
+    assert "cpu_baseline" not in d
