@@ -12,12 +12,15 @@ namespace benor {
 // without that code, which keeps its register allocation free of it.
 constexpr int kPairMaxW = 8;               // W kernel: pair trials' round 1 up to this W
 
-template <int W, bool STATE>
+// ODD_ONLY: every round's binary vote count is odd (m odd, and an even number
+// of "?" initial values) -- the even-M code is not compiled, which frees the
+// registers it would hold (batch path only).
+template <int W, bool STATE, bool ODD_ONLY = false>
 __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
   constexpr int NPH = (W + 1) / 2;          // Philox blocks per trial (2 plane words each)
   constexpr int TB = 64 / NPH;              // trials per init batch
   constexpr int WP = 2 * NPH;               // x1 words per plane row, padded to 16 bytes
-  constexpr int K = W <= 2 ? 4 : (W <= 6 ? 3 : (W <= kPairMaxW ? 2 : 1));   // trials whose round 1 runs interleaved
+  constexpr int K = W <= 2 ? 4 : (W <= 6 ? 3 : (W <= kPairMaxW || (ODD_ONLY && W <= 16) ? 2 : 1));   // trials whose round 1 runs interleaved
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // uniform: scalar trial loop
@@ -100,12 +103,12 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
         uint32_t a0[1][W], a1[1][W];
         uint64_t rest_any[1], any0_[1], any1_[1];
         auto& c1v = reinterpret_cast<uint32_t(&)[1][W]>(c1r);
-        const bool odd = M & 1u;
+        const bool odd = ODD_ONLY || (M & 1u);
         if (odd) {
           p_phase_k<true, W, 1>(c1v, M, tailm, a0, a1);
           if (m > 2u * F) decide_k<true, true, W, 1>(a0, a1, m, F, tailm, rest_any, any0_, any1_);
           else decide_k<true, false, W, 1>(a0, a1, m, F, tailm, rest_any, any0_, any1_);
-        } else {
+        } else if constexpr (!ODD_ONLY) {
           p_phase_k<false, W, 1>(c1v, M, tailm, a0, a1);
           decide_k<false, false, W, 1>(a0, a1, m, F, tailm, rest_any, any0_, any1_);
         }
@@ -132,7 +135,8 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
           const uint64_t vm = (g == W - 1) ? tailm : ~0ull;
           const uint32_t Fg = F + (uint32_t)g;
           // ODD round: no c0 tally was made; c0 = m - c1 (all votes binary), bias g
-          const uint32_t a0g = odd ? (m + 2u * (uint32_t)g) - a1[0][g] : a0[0][g];
+          uint32_t a0g = (m + 2u * (uint32_t)g) - a1[0][g];
+          if constexpr (!ODD_ONLY) a0g = odd ? a0g : a0[0][g];
           const uint32_t a1g = a1[0][g];
           const uint64_t d0 = vcmp_gt(a0g, Fg) & vm;
           const uint64_t d1 = vcmp_gt(a1g, Fg) & vm & ~d0;
@@ -225,11 +229,11 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
             tally_x1<W>(random_init ? ring + (s + k) * WP : ring, c1[k]);
           });
           uint64_t rest_any[K], any0[K], any1[K];
-          if (m_first & 1u) {
+          if (ODD_ONLY || (m_first & 1u)) {
             p_phase_k<true, W, K>(c1, m_first, tailm, a0, a1);
             if (m > 2u * F) decide_k<true, true, W, K>(a0, a1, m, F, tailm, rest_any, any0, any1);
             else decide_k<true, false, W, K>(a0, a1, m, F, tailm, rest_any, any0, any1);
-          } else {
+          } else if constexpr (!ODD_ONLY) {
             p_phase_k<false, W, K>(c1, m_first, tailm, a0, a1);
             decide_k<false, false, W, K>(a0, a1, m, F, tailm, rest_any, any0, any1);
           }
@@ -264,8 +268,11 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
 template <int W>
 hipError_t launch_w(const KParams &p, int grid, hipStream_t s) {
   const bool state = p.node_out || p.rounds_out;
+  const bool odd_only = (p.m & 1u) && !(p.init_q & 1u);   // M = m - init_q in round 1, m after
   if (state)
     hipLaunchKernelGGL((benor_lockstep_w_kernel<W, true>), dim3(grid), dim3(64 * kWavesPerBlock), p.lds_bytes, s, p);
+  else if (odd_only)
+    hipLaunchKernelGGL((benor_lockstep_w_kernel<W, false, true>), dim3(grid), dim3(64 * kWavesPerBlock), p.lds_bytes, s, p);
   else
     hipLaunchKernelGGL((benor_lockstep_w_kernel<W, false>), dim3(grid), dim3(64 * kWavesPerBlock), p.lds_bytes, s, p);
   return hipGetLastError();
