@@ -15,6 +15,30 @@ constexpr int kPairMaxW = 8;               // W kernel: pair trials' round 1 up 
 // ODD_ONLY: every round's binary vote count is odd (m odd, and an even number
 // of "?" initial values) -- the even-M code is not compiled, which frees the
 // registers it would hold (batch path only).
+// One interleaved trial's round-1 outcome in SALU only (the compiler turns
+// the equivalent selects into VALU lane masks): a trial with some undecided
+// receiver (rest != 0) is flagged in `slow` for a re-run; otherwise it counts
+// in f1 if some x = 1 and in f2 if both values occur.
+__device__ __forceinline__ void count_halt(uint64_t rest, uint64_t any0, uint64_t any1, uint32_t bit,
+                                           uint32_t &f1, uint32_t &f2, uint32_t &slow) {
+  uint64_t t;
+  uint32_t b;
+  asm volatile(
+      "s_cmp_eq_u64 %[rest], 0\n\t"
+      "s_cselect_b64 %[t], %[a1], 0\n\t"      // t = halted ? any1 : 0
+      "s_cselect_b32 %[b], 0, %[bit]\n\t"     // b = halted ? 0 : bit
+      "s_or_b32 %[slow], %[slow], %[b]\n\t"
+      "s_cmp_lg_u64 %[t], 0\n\t"
+      "s_addc_u32 %[f1], %[f1], 0\n\t"
+      "s_cmp_lg_u64 %[a0], 0\n\t"
+      "s_cselect_b64 %[t], %[t], 0\n\t"
+      "s_cmp_lg_u64 %[t], 0\n\t"
+      "s_addc_u32 %[f2], %[f2], 0"
+      : [f1] "+s"(f1), [f2] "+s"(f2), [slow] "+s"(slow), [t] "=&s"(t), [b] "=&s"(b)
+      : [rest] "s"(rest), [a0] "s"(any0), [a1] "s"(any1), [bit] "s"(bit)
+      : "scc");
+}
+
 template <int W, bool STATE, bool ODD_ONLY = false>
 __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
   constexpr int NPH = (W + 1) / 2;          // Philox blocks per trial (2 plane words each)
@@ -62,6 +86,10 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
   const uint32_t m_first = m - p.init_q;      // binary-valued senders in round 1 ("?" excluded)
 
   uint32_t hc = 0;                            // this wave's outcome counts of bins 0..63, lane = bin
+  // Interleaved round-1 halts (R = 1, every receiver decided; bins 3 + v) are
+  // counted in three scalars -- halts, halts with some x = 1, halts with both
+  // values -- and folded into `hc` once at the end: no per-trial VALU, no branch.
+  uint32_t f_all = 0, f_1 = 0, f_2 = 0;
   for (uint32_t base = blockIdx.x * kWavesPerBlock + wv; base < trial_count; base += waves_total * TB) {
     // ---- /start (node.ts:167-188): round-1 x planes of TB trials at once.
     if (random_init) {
@@ -239,11 +267,12 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
           }
           slow = 0u;
           nk = K;
+          f_all += K;                         // minus the re-run trials, below
           Unroll<K>::run([&](auto ki) {
             constexpr int k = decltype(ki)::value;
-            if (!rest_any[k]) record(any0[k], any1[k], 1u, true);
-            else slow |= 1u << k;
+            count_halt(rest_any[k], any0[k], any1[k], 1u << k, f_1, f_2, slow);
           });
+          f_all -= (uint32_t)__builtin_popcount(slow);
         }
       }
       for (; slow; slow &= slow - 1u) {         // one call site: the whole-trial loop is inlined once
@@ -254,7 +283,9 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
     }
   }
 
+  hc += lane == 3u ? f_all - f_1 : (lane == 4u ? f_1 - f_2 : (lane == 5u ? f_2 : 0u));   // R = 1: v = 0, 1, 2
   if (hc) atomicAdd(&lhist[lane], hc);
+  if (lane == 0 && f_2) atomicAdd(&lhist[hist_len - 1u], f_2);                     // disagreement counter
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) {
     const uint32_t c = lhist[i];
