@@ -15,14 +15,27 @@
 namespace benor {
 
 // ------------------------------------------------------------------ Philox
+// hi ^ c ^ key in one gfx950 v_bitop3_b32 (LUT 0x96 = three-way xor; the key is
+// wave-uniform: an SGPR operand).
+// Left to itself the compiler emits two v_xor_b32 per output word.
+__device__ __forceinline__ uint32_t xor3_key(uint32_t hi, uint32_t c, uint32_t key) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(hi), "v"(c), "s"(key));
+  return r;
+}
+
+// Philox4x32-10 (Salmon et al., SC'11; Random123).  Callers pass a
+// wave-uniform key (the seed); the counter may vary per lane.
 __device__ __forceinline__ uint4 philox4x32_10(uint32_t k0, uint32_t k1, uint4 c) {
+  k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)k0);    // no-op on an SGPR key
+  k1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)k1);
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
     const uint32_t lo0 = 0xD2511F53u * c.x;
     const uint32_t hi0 = __umulhi(0xD2511F53u, c.x);
     const uint32_t lo1 = 0xCD9E8D57u * c.z;
     const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z);
-    c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+    c = make_uint4(xor3_key(hi1, c.y, k0), lo1, xor3_key(hi0, c.w, k1), lo0);
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
   }
