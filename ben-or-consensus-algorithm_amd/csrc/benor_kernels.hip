@@ -492,7 +492,7 @@ __global__ void __launch_bounds__(256) benor_event_kernel(KParams p) {
     uint64_t killed = p.faulty_mask, decided = 0;
     // ---- node.ts:21-26 and initial values (compact live order)
     uint4 ir = make_uint4(0, 0, 0, 0);
-    if (p.init_mode == BO_INIT_RANDOM) ir = philox4x32_10(k0, k1, make_uint4(tlo, thi, 0u, kStreamInit << 24));
+    if (p.init_mode == BO_INIT_RANDOM) ir = philox4x32_10<false>(k0, k1, make_uint4(tlo, thi, 0u, kStreamInit << 24));
     for (uint32_t c = 0; c < m; ++c) {
       const uint32_t i = p.live_ids[c];
       int8_t v;
@@ -538,7 +538,7 @@ __global__ void __launch_bounds__(256) benor_event_kernel(KParams p) {
     // ---- delivery order
     uint64_t rng;
     {
-      const uint4 o = philox4x32_10(k0, k1, make_uint4(tlo, thi, 0u, kStreamOrder << 24));
+      const uint4 o = philox4x32_10<false>(k0, k1, make_uint4(tlo, thi, 0u, kStreamOrder << 24));
       rng = (((uint64_t)o.x << 32) | o.y) ^ 0xD1B54A32D192ED03ull;
     }
     // ---- /start (node.ts:167-188)
@@ -596,7 +596,7 @@ __global__ void __launch_bounds__(256) benor_event_kernel(KParams p) {
         else if (c0 + c1 > 0 && c0 > c1) nx = 0;
         else if (c0 + c1 > 0 && c0 < c1) nx = 1;
         else {
-          const uint4 rr = philox4x32_10(k0, k1, make_uint4(tlo, thi, to, (k & 0x00FFFFFFu) | (kStreamCoin << 24)));
+          const uint4 rr = philox4x32_10<false>(k0, k1, make_uint4(tlo, thi, to, (k & 0x00FFFFFFu) | (kStreamCoin << 24)));
           nx = (rr.x > 0x80000000u) ? 0 : 1;           // node.ts:111
         }
         L.xs[to] = nx;

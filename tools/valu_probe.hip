@@ -9,9 +9,12 @@
 template <int OP>
 __global__ void __launch_bounds__(256) probe(unsigned *sink, int iters, unsigned seed) {
   unsigned a[8];
+  unsigned long long c[8];
   const unsigned x = threadIdx.x * 2654435761u + blockIdx.x + seed;
 #pragma unroll
   for (int i = 0; i < 8; ++i) a[i] = x + (unsigned)i;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) c[i] = x ^ (unsigned)i;
   for (int it = 0; it < iters; ++it) {
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -33,12 +36,15 @@ __global__ void __launch_bounds__(256) probe(unsigned *sink, int iters, unsigned
         }
         if (OP == 10) asm volatile("v_not_b32 %0, %0" : "+v"(a[i]));
         if (OP == 11) asm volatile("v_xor_b32 %0, %1, %0" : "+v"(a[i]) : "s"(seed));
+        if (OP == 12) asm volatile("v_mul_lo_u32 %0, %1, %0" : "+v"(a[i]) : "v"(x));
+        if (OP == 13) asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(c[i]) : "v"(x), "v"(a[i]) : "vcc");
+        if (OP == 14) asm volatile("v_bitop3_b32 %0, %1, %0, %2 bitop3:0x96" : "+v"(a[i]) : "v"(x), "s"(seed));
       }
     }
   }
   unsigned s = 0;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) s ^= a[i];
+  for (int i = 0; i < 8; ++i) s ^= a[i] ^ (unsigned)c[i] ^ (unsigned)(c[i] >> 32);
   if (s == 0x12345678u) sink[blockIdx.x] = s;
 }
 
@@ -85,6 +91,9 @@ int main() {
     run<9>("v_mov_b64 (s) + v_xor", cus, bpc);
     run<10>("v_not_b32", cus, bpc);
     run<11>("v_xor_b32 (s,v)", cus, bpc);
+    run<12>("v_mul_lo_u32", cus, bpc);
+    run<13>("v_mad_u64_u32", cus, bpc);
+    run<14>("v_bitop3_b32 (xor3)", cus, bpc);
   }
   return 0;
 }
