@@ -52,3 +52,30 @@ def test_small_sweep_against_law(tmp_path):
         exp = 1 - analytic.tie_prob(N - F)
         sd = (exp * (1 - exp) / 200_000) ** 0.5
         assert abs(float(r["P_R1"]) - exp) < 6 * sd + 1e-9, r
+
+
+@pytest.mark.gpu
+def test_sweep_two_ranks_equals_one(tmp_path):
+    """C5's multi-GPU path: each cell's trials split over ranks,
+    one all-reduce of the [cells, H] histogram buffer.  Two ranks over gloo on
+    one GPU must write the byte-identical CSV of one rank, since Philox is keyed
+    by the global trial id."""
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    args = ["sweep", "--N", "64,1024,2112", "--steps", "3", "--trials", str(9 * 30_001), "--k-max", "12"]
+    env = dict(os.environ, PYTHONPATH=PKG)
+    one = tmp_path / "one.csv"
+    subprocess.run([sys.executable, "-m", "benor.cli", *args, "--out", str(one)], check=True, env=env, cwd=PKG,
+                   timeout=120)
+    two = tmp_path / "two.csv"
+    env2 = dict(env, BENOR_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                    "--master-addr", "127.0.0.1", "--master-port", str(port), "-m", "benor.cli", *args,
+                    "--out", str(two)], check=True, env=env2, cwd=PKG, timeout=180)
+    assert one.read_bytes() == two.read_bytes()
+    rows = list(csv.DictReader(open(one)))
+    assert len(rows) == 9 and all(int(r["trials"]) == 30_001 for r in rows)
