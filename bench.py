@@ -55,6 +55,7 @@ def parse():
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x243F6A8885A308D3)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample budget (0 = skip)")
     ap.add_argument("--no-peak-probe", action="store_true")
+    ap.add_argument("--no-other-configs", action="store_true", help="skip the configs[1]/[2] side measurements")
     return ap.parse_args()
 
 
@@ -66,6 +67,37 @@ def node_rounds(hist, m, k_max):
         total_rounds += R * int(hist[R * 3] + hist[R * 3 + 1] + hist[R * 3 + 2])
     total_rounds += k_max * int(hist[0] + hist[1] + hist[2])
     return total_rounds * m, total_rounds
+
+
+# BASELINE configs[1] and [2] (one GPU): measured after the timed region and
+# reported beside the headline, not part of `value`.
+OTHER_CONFIGS = [("C2 N=10,F=4", 10, 4, 1_000_000), ("C2 N=10,F=5 (F>N/2, no decision)", 10, 5, 1_000_000),
+                 ("C3 N=256,F=85", 256, 85, 10_000_000)]
+
+
+def other_configs(benor, torch, k_max, seed):
+    import numpy as np
+
+    stream = torch.cuda.current_stream()
+    out = {}
+    for name, N, F, T in OTHER_CONFIGS:
+        plan = benor.TrialsPlan(N, F, [i < F for i in range(N)], seed=seed, k_max=k_max)
+        h = torch.zeros(plan.hist_len, dtype=torch.int64, device="cuda")
+        plan.launch(0, T, h.data_ptr(), stream.cuda_stream)          # warm-up launch
+        torch.cuda.synchronize()
+        h.zero_()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        plan.launch(T, T, h.data_ptr(), stream.cuda_stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1)
+        hist = h.cpu().numpy().astype(np.uint64)
+        nr, rounds = node_rounds(hist, plan.live_nodes, k_max)
+        undecided = int(hist[0] + hist[1] + hist[2])
+        out[name] = {"trials": T, "kernel_ms": ms, "node_rounds_per_s": nr / (ms * 1e-3),
+                     "trials_per_s": T / (ms * 1e-3), "mean_rounds": rounds / T, "undecided_trials": undecided}
+    return out
 
 
 def cpu_baseline(N, F, k_max, seed, budget_s):
@@ -189,6 +221,8 @@ def main():
         "all_node_rounds_per_s": rounds * N / elapsed,
         "trials_per_s": T * world * args.steps / elapsed,
     }
+    if world == 1 and not args.no_other_configs:
+        out["other_configs"] = other_configs(benor, torch, k_max, args.seed)
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(N, F, k_max, args.seed, args.cpu_seconds)
     if rank == 0:

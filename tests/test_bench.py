@@ -54,6 +54,11 @@ def test_bench_single_gpu_line():
     assert d["n_gpus"] == 1 and d["value"] > 0 and d["unit"] == "node-rounds/s"
     assert 0 < d["roofline"]["frac"] < 1.0
     assert d["cpu_baseline"]["value"] > 0 and d["cpu_baseline"]["kind"] == "port"
+    # BASELINE configs[1] and [2] beside the headline
+    oc = d["other_configs"]
+    assert oc["C2 N=10,F=4"]["undecided_trials"] == 0 and oc["C2 N=10,F=4"]["mean_rounds"] > 1.3
+    assert oc["C2 N=10,F=5 (F>N/2, no decision)"]["undecided_trials"] == 1_000_000
+    assert oc["C3 N=256,F=85"]["mean_rounds"] == 1.0 and oc["C3 N=256,F=85"]["node_rounds_per_s"] > 0
 
 
 @pytest.mark.gpu
@@ -70,3 +75,4 @@ def test_bench_ranks_gloo_one_gpu(ranks):
     # every rank ran its own 10^6 trials per step; rank 0's merged histogram saw them all
     assert d["trials_per_s"] * d["ms_per_step"] * 1e-3 == pytest.approx(ranks * 1_000_000, rel=1e-6)
     assert "cpu_baseline" not in d
+    assert "other_configs" not in d

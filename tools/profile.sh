@@ -7,8 +7,8 @@ TAG=${TAG:-r01}
 OUT="$R/gpurun_out/prof_$TAG"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-BENCH_ARGS=${BENCH_ARGS:---steps 3 --warmup 1 --cpu-seconds 0 --no-peak-probe}
-PMC_ARGS=${PMC_ARGS:---trials 100000000 --steps 1 --warmup 0 --cpu-seconds 0 --no-peak-probe}
+BENCH_ARGS=${BENCH_ARGS:---steps 3 --warmup 1 --cpu-seconds 0 --no-peak-probe --no-other-configs}
+PMC_ARGS=${PMC_ARGS:---trials 100000000 --steps 1 --warmup 0 --cpu-seconds 0 --no-peak-probe --no-other-configs}
 chk() { local rc=$1 name=$2; echo "== $name rc=$rc"; if [ "$rc" -ne 0 ]; then echo "stop after $name"; exit "$rc"; fi; }
 if [ -z "$SKIP_PROBE" ]; then
   timeout -k 10 120 "$R/tools/valu_probe" > "$OUT/valu_probe.txt" 2>&1; chk $? probe
