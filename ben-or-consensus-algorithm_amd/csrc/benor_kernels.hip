@@ -60,11 +60,20 @@ __device__ __forceinline__ uint32_t seg_tally(uint64_t plane, uint32_t half_shif
   return (uint32_t)__builtin_popcount((uint32_t)(plane >> half_shift) & segmask);
 }
 
+// Per-lane flag from a wave mask (one v_cndmask).  The mask must come from a
+// SALU op (not straight from a v_cmp): no VALU-write -> VALU-read hazard.
+__device__ __forceinline__ bool lane_in(uint64_t mask) { return select_lanes(0u, 1u, mask) != 0u; }
+
+// Segment state lives in wave masks (SGPR pairs) -- active, needs a trial,
+// decided, x = 1, x = 0 -- updated by SALU ops, so a phase's ballots are plain
+// v_cmp results combined with `act` in SALU (per-lane booleans would be
+// materialised as v_cndmask + v_cmp pairs around every ballot).  Per lane
+// only the round counter and the trial id remain in VGPRs.
 __global__ void __launch_bounds__(256) benor_packed_kernel(KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wv = threadIdx.x >> 6;
-  const uint32_t m = p.m, F = p.F;
+  const uint32_t m = p.m, F = p.F, k_max = p.k_max;
   const uint32_t P = 32u / m;                       // segments per half
   uint32_t *lhist = reinterpret_cast<uint32_t *>(smem);
   uint32_t *ring = reinterpret_cast<uint32_t *>(smem + p.hist_bytes + wv * p.wave_bytes);   // [128]
@@ -80,23 +89,29 @@ __global__ void __launch_bounds__(256) benor_packed_kernel(KParams p) {
   const uint32_t mbits = m == 32u ? ~0u : ((1u << m) - 1u);
   const uint32_t segmask = valid ? (mbits << (si * m)) : 0u;
   const uint32_t node = valid ? p.live_ids[c] : 0u;
+  const uint32_t not_leader = c ? 1u : 0u;
   const bool random_init = p.init_mode == BO_INIT_RANDOM;
+  const uint32_t M1 = m - p.init_q;                 // binary-valued senders in round 1
   // fixed init (BO_INIT_FIXED): word 0 of the plane holds every live node (m <= 32)
   const uint4 fixed = random_init ? make_uint4(0, 0, 0, 0) : p.init_plane[0];
-  const uint32_t fixed_x = ((fixed.z >> c) & 1u) ? 1u : (((fixed.x >> c) & 1u) ? 0u : 2u);
+  const uint64_t validm = ballot(valid);
+  const uint64_t leaderm = ballot(valid && c == 0u) & validm;
+  const uint64_t fx1m = ballot(valid && ((fixed.z >> c) & 1u)) & validm;
+  const uint64_t fx0m = ballot(valid && ((fixed.x >> c) & 1u)) & validm;
 
   const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
   const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
   const uint64_t waves_total = (uint64_t)gridDim.x * kWavesPerBlock;
 
   uint64_t next_j = 0, filled = 0;                  // wave queue: j-th trial of the wave = gw + j * waves_total
-  bool need = valid, act = false, dec = false;
-  uint32_t x = 2u, r = 0u;
-  uint64_t trial = 0;
+  uint64_t needm = validm, actm = 0, decm = 0, x1m = 0, x0m = 0;
+  uint32_t r = 0u;
+  uint32_t tlo = 0u, thi = 0u;
 
   for (;;) {
     // ---- pull: segments that need a trial take the next queue entries (node.ts:167-188 /start)
-    const uint64_t Lb = ballot(need && c == 0u);
+    const uint64_t Lb = needm & leaderm;
+    uint64_t firstm = 0;                            // segments in their first round
     if (Lb) {
       const uint32_t nf = (uint32_t)__builtin_popcountll(Lb);
       if (random_init && next_j + nf > filled) {   // refill 64 ring slots, one trial per lane
@@ -110,74 +125,84 @@ __global__ void __launch_bounds__(256) benor_packed_kernel(KParams p) {
         }
         filled += 64u;
       }
-      if (need) {
-        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(Lb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)Lb, 0u));
-        const uint64_t j = next_j + below - (c ? 1u : 0u);
-        const uint64_t t = gw + j * waves_total;
-        need = false;
-        act = t < p.trial_count;
-        if (act) {
-          trial = p.trial_begin + t;
-          x = random_init ? ((ring[j & 127u] >> c) & 1u) : fixed_x;
-          dec = false;
-          r = 0u;
-        }
+      // every lane computes its segment's queue entry; only needing lanes keep it
+      const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(Lb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)Lb, 0u));
+      const uint64_t j = next_j + below - not_leader;
+      const uint64_t t = gw + j * waves_total;
+      const uint64_t okm = ballot(t < p.trial_count) & needm;
+      const uint64_t tr = p.trial_begin + t;
+      tlo = select_lanes(tlo, (uint32_t)tr, needm);
+      thi = select_lanes(thi, (uint32_t)(tr >> 32), needm);
+      r = select_lanes(r, 0u, needm);
+      uint64_t n1 = fx1m, n0 = fx0m;
+      if (random_init) {
+        n1 = ballot((ring[(uint32_t)j & 127u] >> c) & 1u) & validm;
+        n0 = validm & ~n1;
       }
+      x1m = (x1m & ~needm) | (n1 & okm);
+      x0m = (x0m & ~needm) | (n0 & okm);
+      decm &= ~needm;
+      actm = (actm & ~needm) | okm;
+      firstm = okm;
+      needm = 0;
       next_j += nf;
     }
-    if (!__any(act)) break;
+    if (!actm) break;
 
     // ---- R-phase ("proposal phase", node.ts:46-82): c1 per receiver, c0 = M - c1
     //      (M = m binary-valued senders; minus the "?" ones in round 1 of a fixed init)
-    const uint64_t is1 = ballot(act && x == 1u);
-    const uint32_t c1 = seg_tally(is1, half_shift, segmask);
-    const uint32_t c0 = (r == 0u ? m - p.init_q : m) - c1;
+    const uint32_t c1 = seg_tally(x1m & actm, half_shift, segmask);
+    const uint32_t c0 = (p.init_q ? select_lanes(m, M1, firstm) : m) - c1;
     // ---- P-phase ("voting phase", node.ts:83-158)
-    const uint64_t p0 = ballot(act && c0 > c1), p1 = ballot(act && c1 > c0);   // node.ts:63-69 (else "?")
+    const uint64_t p0 = ballot(c0 > c1) & actm, p1 = ballot(c1 > c0) & actm;       // node.ts:63-69 (else "?")
     const uint32_t v0 = seg_tally(p0, half_shift, segmask), v1 = seg_tally(p1, half_shift, segmask);
     ++r;
-    const bool d0 = v0 > F, d1 = !d0 && v1 > F;                                    // node.ts:99, :102
-    const bool tie = act && !d0 && !d1 && v0 == v1;                                // node.ts:110-111
-    uint32_t nx = d0 ? 0u : (d1 ? 1u : (v1 > v0 ? 1u : 0u));                        // node.ts:106-109
-    if (__any(tie)) {
-      uint32_t kk0 = k0, kk1 = k1;
-      asm volatile("" : "+s"(kk0), "+s"(kk1));
+    const uint64_t d0 = ballot(v0 > F) & actm;                                       // node.ts:99
+    const uint64_t d1 = ballot(v1 > F) & actm & ~d0;                                 // node.ts:102
+    const uint64_t und = actm & ~(d0 | d1);
+    uint64_t nx1 = d1;
+    if (und) {
+      nx1 |= ballot(v1 > v0) & und;                                                 // node.ts:106-109
+      const uint64_t tie = ballot(v0 == v1) & und;                                  // node.ts:110-111
       if (tie) {
-        const uint4 rr = philox4x32_10(kk0, kk1, make_uint4((uint32_t)trial, (uint32_t)(trial >> 32), node,
-                                                            (r & 0x00FFFFFFu) | (kStreamCoin << 24)));
-        nx = (rr.x > 0x80000000u) ? 0u : 1u;                                       // Math.random() > 0.5 ? 0 : 1
+        uint32_t kk0 = k0, kk1 = k1;
+        asm volatile("" : "+s"(kk0), "+s"(kk1));
+        bool coin1 = false;
+        if (lane_in(tie)) {
+          const uint4 rr = philox4x32_10(kk0, kk1, make_uint4(tlo, thi, node, (r & 0x00FFFFFFu) | (kStreamCoin << 24)));
+          coin1 = !(rr.x > 0x80000000u);                                            // Math.random() > 0.5 ? 0 : 1
+        }
+        nx1 |= ballot(coin1) & tie;
       }
     }
-    if (act) {
-      x = nx;
-      dec = dec || d0 || d1;                                                        // sticky (node.ts:100-105)
-    }
+    x1m = (x1m & ~actm) | nx1;
+    x0m = (x0m & ~actm) | (actm & ~nx1);
+    decm |= d0 | d1;                                                                // sticky (node.ts:100-105)
     // ---- halt: every live node of the segment decided (auto-stop, node.ts:116-145) or k_max
-    const uint64_t db = ballot(act && dec);
-    const bool seg_done = seg_tally(db, half_shift, segmask) == m;
-    const bool fin = act && (seg_done || r >= p.k_max);
-    if (__any(fin)) {
-      const uint64_t n0 = ballot(act && x == 0u), n1 = ballot(act && x == 1u);
-      if (fin) {
-        const bool any0 = seg_tally(n0, half_shift, segmask) != 0u, any1 = seg_tally(n1, half_shift, segmask) != 0u;
+    const uint64_t done = ballot(seg_tally(decm & actm, half_shift, segmask) == m) & actm;
+    const uint64_t fin = (done | ballot(r >= k_max)) & actm;
+    if (fin) {
+      const bool any0 = seg_tally(x0m & fin, half_shift, segmask) != 0u;
+      const bool any1 = seg_tally(x1m & fin, half_shift, segmask) != 0u;
+      const uint64_t lead = fin & leaderm;
+      if (lane_in(lead)) {
+        const bool seg_done = lane_in(done & lead);
         const uint32_t v = (any0 && any1) ? 2u : (any1 ? 1u : 0u);
-        if (c == 0u) {
-          atomicAdd(&lhist[seg_done ? (r * 3u + v) : v], 1u);
-          if (seg_done && v == 2u) atomicAdd(&lhist[p.hist_len - 1u], 1u);
-          if (p.rounds_out) *p.rounds_out = seg_done ? r : 0u;
-        }
-        if (p.node_out) {                                                           // GET /getState (node.ts:197-199)
-          bo_node_state ns;
-          ns.killed = 0;
-          ns.x = (int8_t)x;
-          ns.decided = (int8_t)(dec ? 1 : 0);
-          ns.pad = 0;
-          ns.k = (int32_t)r + 1;                                                    // node.ts:147
-          p.node_out[node] = ns;
-        }
-        act = false;
-        need = true;
+        atomicAdd(&lhist[seg_done ? (r * 3u + v) : v], 1u);
+        if (seg_done && v == 2u) atomicAdd(&lhist[p.hist_len - 1u], 1u);
+        if (p.rounds_out) *p.rounds_out = seg_done ? r : 0u;
       }
+      if (p.node_out && lane_in(fin)) {                                             // GET /getState (node.ts:197-199)
+        bo_node_state ns;
+        ns.killed = 0;
+        ns.x = (int8_t)(lane_in(x1m & fin) ? 1 : (lane_in(x0m & fin) ? 0 : 2));
+        ns.decided = (int8_t)(lane_in(decm & fin) ? 1 : 0);
+        ns.pad = 0;
+        ns.k = (int32_t)r + 1;                                                      // node.ts:147
+        p.node_out[node] = ns;
+      }
+      actm &= ~fin;
+      needm |= fin;
     }
   }
 
