@@ -39,6 +39,23 @@ __device__ __forceinline__ void count_halt(uint64_t rest, uint64_t any0, uint64_
       : "scc");
 }
 
+// The same for a trial where every receiver decided (odd vote count and
+// m > 2F, decide_k's SURE case): it halts, and every live node holds a value,
+// so some x = 0 or some x = 1.  f1 += [some 1]; f2 += [some 0] + [some 1],
+// and the caller takes 1 off f2 per trial: [both] = [some 0] + [some 1] - 1.
+__device__ __forceinline__ void count_sure(uint64_t any0, uint64_t any1, uint32_t &f1, uint32_t &f2) {
+  asm volatile(
+      "s_cmp_lg_u64 %[a1], 0\n\t"
+      "s_addc_u32 %[f1], %[f1], 0\n\t"
+      "s_cmp_lg_u64 %[a1], 0\n\t"
+      "s_addc_u32 %[f2], %[f2], 0\n\t"
+      "s_cmp_lg_u64 %[a0], 0\n\t"
+      "s_addc_u32 %[f2], %[f2], 0"
+      : [f1] "+s"(f1), [f2] "+s"(f2)
+      : [a0] "s"(any0), [a1] "s"(any1)
+      : "scc");
+}
+
 template <int W, bool STATE, bool ODD_ONLY = false>
 __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
   constexpr int NPH = (W + 1) / 2;          // Philox blocks per trial (2 plane words each)
@@ -257,22 +274,35 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
             tally_x1<W>(random_init ? ring + (s + k) * WP : ring, c1[k]);
           });
           uint64_t rest_any[K], any0[K], any1[K];
+          slow = 0u;
+          nk = K;
+          auto count_all = [&]() {
+            f_all += K;                         // minus the re-run trials, below
+            Unroll<K>::run([&](auto ki) {
+              constexpr int k = decltype(ki)::value;
+              count_halt(rest_any[k], any0[k], any1[k], 1u << k, f_1, f_2, slow);
+            });
+            f_all -= (uint32_t)__builtin_popcount(slow);
+          };
           if (ODD_ONLY || (m_first & 1u)) {
             p_phase_k<true, W, K>(c1, m_first, tailm, a0, a1);
-            if (m > 2u * F) decide_k<true, true, W, K>(a0, a1, m, F, tailm, rest_any, any0, any1);
-            else decide_k<true, false, W, K>(a0, a1, m, F, tailm, rest_any, any0, any1);
+            if (m > 2u * F) {                   // every receiver decides: all K trials halt
+              decide_k<true, true, W, K>(a0, a1, m, F, tailm, rest_any, any0, any1);
+              f_all += K;
+              f_2 -= K;
+              Unroll<K>::run([&](auto ki) {
+                constexpr int k = decltype(ki)::value;
+                count_sure(any0[k], any1[k], f_1, f_2);
+              });
+            } else {
+              decide_k<true, false, W, K>(a0, a1, m, F, tailm, rest_any, any0, any1);
+              count_all();
+            }
           } else if constexpr (!ODD_ONLY) {
             p_phase_k<false, W, K>(c1, m_first, tailm, a0, a1);
             decide_k<false, false, W, K>(a0, a1, m, F, tailm, rest_any, any0, any1);
+            count_all();
           }
-          slow = 0u;
-          nk = K;
-          f_all += K;                         // minus the re-run trials, below
-          Unroll<K>::run([&](auto ki) {
-            constexpr int k = decltype(ki)::value;
-            count_halt(rest_any[k], any0[k], any1[k], 1u << k, f_1, f_2, slow);
-          });
-          f_all -= (uint32_t)__builtin_popcount(slow);
         }
       }
       for (; slow; slow &= slow - 1u) {         // one call site: the whole-trial loop is inlined once
