@@ -13,6 +13,7 @@
 #include <cstring>
 #include <string>
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "benor.h"
@@ -270,7 +271,14 @@ int bo_plan_create(const bo_trials_cfg *cfg, bo_plan **out) {
       const uint64_t stride_bytes = (uint64_t)kp.ev_stride * 4u;
       int cus = 256;
       (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      uint64_t lanes = (uint64_t)cus * 8u * 256u;
+      // Lanes per CU: the mode is bound by the latency of per-lane scratch
+      // accesses, so fewer lanes whose slices stay cache-resident beat full
+      // occupancy: 512 per CU for slices up to 4 KiB (N <= 12), else 256
+      // (tools/ev_sweep.sh, BENOR_EVENT_LANES_PER_CU overrides).
+      uint64_t per_cu = stride_bytes <= 4096u ? 512u : 256u;
+      if (const char *ev = getenv("BENOR_EVENT_LANES_PER_CU")) per_cu = strtoull(ev, nullptr, 10);
+      if (per_cu < 256u) per_cu = 256u;
+      uint64_t lanes = (uint64_t)cus * per_cu;
       const uint64_t fit = (4ull << 30) / stride_bytes;
       if (fit < lanes) lanes = fit;
       lanes = lanes / 256u * 256u;
