@@ -191,6 +191,19 @@ __global__ void __launch_bounds__(256) benor_lockstep_blocked_kernel(KParams p) 
             uint32_t a0[G], a1[G];
             if constexpr (ODD) tally_groups_x1<G>(P1, W, a1);
             else tally_groups<G>(P, W, a0, a1);
+            if constexpr (SURE && !STATE) {
+              // Every live receiver decides this round, so the trial halts: no
+              // x plane or decided bits are staged, only the outcome masks.
+              Unroll<G>::run([&](auto gi) {
+                constexpr int g = decltype(gi)::value;
+                const uint64_t vm = group_mask(b * G + g, m);
+                const uint64_t d0 = vcmp_lt(a1[g], mF + (uint32_t)g) & vm;   // node.ts:99
+                any0 |= d0;
+                any1 |= vm & ~d0;                                            // node.ts:102
+                asm volatile("" : "+s"(any0), "+s"(any1));
+              });
+              continue;
+            }
             uint32_t st = 0, dbb = D[b * 64u + lane];
             Unroll<G>::run([&](auto gi) {
               constexpr int g = decltype(gi)::value;
