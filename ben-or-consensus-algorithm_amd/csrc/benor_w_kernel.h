@@ -12,6 +12,17 @@ namespace benor {
 // without that code, which keeps its register allocation free of it.
 constexpr int kPairMaxW = 8;               // W kernel: pair trials' round 1 up to this W
 
+// Trials whose round 1 runs interleaved (K).  A small-W round is a handful of
+// words, so more independent trials hide the ballot -> s_nop -> v_bcnt and LDS
+// latencies.  Odd-only kernels carry no even-M code and take the larger K.
+// K divides the init batch TB = 64 / ceil(W/2) where it can.  v19 A/B
+// (profiles/r01-v19_ab_interleave_k.jsonl): odd W=1 +27 %, W=2 +10 %, W=3 +7 %,
+// W=4 +2 %; even W=1 +8 %, W=2 +4 %, W=3 +2 %, W=4 +1.5 %; larger K spills.
+constexpr int interleave_k(int W, bool odd_only) {
+  if (odd_only) return W <= 1 ? 16 : (W <= 4 ? 8 : (W <= 6 ? 3 : (W <= 16 ? 2 : 1)));
+  return W <= 2 ? 8 : (W <= 4 ? 4 : (W <= 6 ? 3 : (W <= kPairMaxW ? 2 : 1)));
+}
+
 // ODD_ONLY: every round's binary vote count is odd (m odd, and an even number
 // of "?" initial values) -- the even-M code is not compiled, which frees the
 // registers it would hold (batch path only).
@@ -61,7 +72,7 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
   constexpr int NPH = (W + 1) / 2;          // Philox blocks per trial (2 plane words each)
   constexpr int TB = 64 / NPH;              // trials per init batch
   constexpr int WP = 2 * NPH;               // x1 words per plane row, padded to 16 bytes
-  constexpr int K = W <= 2 ? 4 : (W <= 6 ? 3 : (W <= kPairMaxW || (ODD_ONLY && W <= 16) ? 2 : 1));   // trials whose round 1 runs interleaved
+  constexpr int K = interleave_k(W, ODD_ONLY);   // trials whose round 1 runs interleaved
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // uniform: scalar trial loop
