@@ -3,8 +3,10 @@ C ABI: seeded random network shapes (N up to 4096, F including F >= N/2),
 arbitrary fault placements, random or fixed initial values (with "?"
 entries, so the first round's binary vote count M differs from m), and
 small / large round caps.  Covers every lockstep kernel variant (packed,
-W kernel with K = 1..4 interleaving, odd / even / "every receiver decides"
-decision paths, blocked) and the random-delivery and event-level modes.
+W kernel, odd / even / "every receiver decides" decision paths, blocked) and
+the random-delivery and event-level modes.  At these trial counts a wave
+holds about one trial, so the W kernel's interleaved round 1 is covered by
+test_gpu_parity.py::test_interleaved_round1_matches_oracle instead.
 Histograms must be bit-identical."""
 import numpy as np
 import pytest

@@ -134,6 +134,28 @@ def test_restart_runs_from_current_values():
     assert [s["x"] for s in a] == [s["x"] for s in b]
 
 
+@pytest.mark.parametrize("N,F", [
+    # odd m (odd-only kernel, K = 16 / 8 / 8 / 8 / 3 / 2): every receiver decides ...
+    (64, 21), (128, 41), (256, 85), (300, 71), (400, 100), (600, 151),
+    # ... or not (m <= 2F: undecided trials re-run alone after the interleaved round 1)
+    (100, 49), (200, 99),
+    # even m (K = 8 / 8 / 4 / 4 / 3): ties, coins and re-runs
+    (64, 20), (128, 42), (256, 86), (300, 72), (512, 170),
+])
+def test_interleaved_round1_matches_oracle(N, F):
+    """The W kernel runs round 1 of K trials interleaved only when a wave holds
+    K trials of the launch, i.e. at trial counts of about K x the grid's wave
+    count (8 per CU x 4 waves x 256 CUs): 200 000 trials engage every K here
+    (`interleave_k`).  Bit-identical to the oracle."""
+    seed = 0xB5AD4ECEDA1CE2A9 ^ (N * 131 + F)
+    plan = benor.TrialsPlan(N, F, first_f(N, F), seed=seed, k_max=16)
+    T = 200_000
+    got = plan.run(31, T)
+    ref = oracle.run_trials(N, F, first_f(N, F), seed=seed, trial_begin=31, trial_count=T, k_max=16)
+    np.testing.assert_array_equal(got, ref.hist)
+    np.testing.assert_array_equal(got, plan.run(31, 70_001) + plan.run(70_032, T - 70_001))
+
+
 # ------------------------------------------------- full-size properties
 def test_full_size_sharding_invariance_and_law():
     """N=1024, F=341 (BASELINE metric config): m = 683 is odd, so no round can
