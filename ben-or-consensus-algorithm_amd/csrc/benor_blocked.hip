@@ -71,18 +71,19 @@ __device__ __forceinline__ void tally_groups_x1(const uint2 *__restrict__ plane,
 // tallies of every block.  ODD: an odd number of binary votes cannot tie,
 // so p0 is the complement of p1 (one compare per group).
 template <bool ODD, int G>
-__device__ __forceinline__ uint32_t stage_proposals(const uint32_t (&a1)[G], uint32_t b, uint32_t m, uint32_t M) {
+__device__ __forceinline__ uint2 stage_proposals(const uint32_t (&a1)[G], uint32_t b, uint32_t m, uint32_t M) {
   const uint32_t hi_t = M >> 1, lo_t = (M + 1u) >> 1;
-  uint32_t st = 0;
+  uint32_t st = 0, st2 = 0;                     // records of groups 0..15 and 16..G-1 (4 lanes each)
   Unroll<G>::run([&](auto gi) {
     constexpr int g = decltype(gi)::value;
     const uint64_t vm = group_mask(b * G + g, m);
     const uint64_t p1 = vcmp_gt(a1[g], hi_t + (uint32_t)g) & vm;          // c1 > c0  (node.ts:65-66)
     const uint64_t p0 = ODD ? (vm & ~p1)                                   // c0 > c1  (node.ts:63-64)
                             : (vcmp_lt(a1[g], lo_t + (uint32_t)g) & vm);   // else "?"
-    st = stage4<g>(st, p0, p1);
+    if constexpr (g < 16) st = stage4<g>(st, p0, p1);
+    else st2 = stage4<g - 16>(st2, p0, p1);
   });
-  return st;
+  return make_uint2(st, st2);
 }
 
 template <int G, bool STATE>
@@ -175,8 +176,11 @@ __global__ void __launch_bounds__(256) benor_lockstep_blocked_kernel(KParams p) 
               });
               if (lane < 2u * G) reinterpret_cast<uint32_t *>(P1 + b * G)[lane] = st;
             } else {
-              const uint32_t st = stage_proposals<false, G>(a1, b, m, M);
-              if (lane < 4u * G) reinterpret_cast<uint32_t *>(P + b * G)[lane] = st;
+              const uint2 st = stage_proposals<false, G>(a1, b, m, M);
+              if (lane < 4u * G) reinterpret_cast<uint32_t *>(P + b * G)[lane] = st.x;
+              if constexpr (G > 16) {
+                if (lane < 4u * G - 64u) reinterpret_cast<uint32_t *>(P + b * G)[64u + lane] = st.y;
+              }
             }
           }
           if constexpr (ODD) {                         // padding group read by the pairwise tally
@@ -303,5 +307,11 @@ template hipError_t launch_b<13>(const KParams &, int, hipStream_t);
 template hipError_t launch_b<14>(const KParams &, int, hipStream_t);
 template hipError_t launch_b<15>(const KParams &, int, hipStream_t);
 template hipError_t launch_b<16>(const KParams &, int, hipStream_t);
+template hipError_t launch_b<17>(const KParams &, int, hipStream_t);
+template hipError_t launch_b<18>(const KParams &, int, hipStream_t);
+template hipError_t launch_b<19>(const KParams &, int, hipStream_t);
+template hipError_t launch_b<20>(const KParams &, int, hipStream_t);
+template hipError_t launch_b<21>(const KParams &, int, hipStream_t);
+template hipError_t launch_b<22>(const KParams &, int, hipStream_t);
 
 }  // namespace benor

@@ -738,8 +738,20 @@ void plan_geometry(KParams &p) {
     p.variant = 1;
     p.wave_bytes = (tb * WP + 2u * WP) * 8u;            // init ring, final x1 plane, decided bits
   } else {
-    const uint32_t nb = (W + 15u) / 16u;           // blocks of at most 16 groups
-    const uint32_t G = (W + nb - 1u) / nb;         // balanced: padding < nb groups
+    // Blocks of G = ceil(W / nb) in 11..22 groups: the fewest padded groups nb * G,
+    // ties to G <= 16 (5-7 waves/SIMD; G > 16 runs at 4-5), then to fewer blocks.
+    // v19 A/B (profiles/r01-v19_ab_blocked_g.txt): one padded group fewer at G = 19..22
+    // is +3-6 %; the same padding at G > 16 is 1-2 % slower.
+    uint32_t nb = (W + 15u) / 16u, G = (W + nb - 1u) / nb;
+    for (uint32_t n = (W + 21u) / 22u; n <= (W + 10u) / 11u; ++n) {
+      const uint32_t g = (W + n - 1u) / n;
+      if (g < 11u || g > 22u) continue;
+      const bool better = n * g < nb * G || (n * g == nb * G && g <= 16u && (G > 16u || n < nb));
+      if (better) {
+        nb = n;
+        G = g;
+      }
+    }
     const uint32_t XW = ((G * nb > WP ? G * nb : WP) + 1u) & ~1u;
     p.G = G;
     p.nblocks = nb;
@@ -783,7 +795,7 @@ hipError_t launch_lockstep(const KParams &p, int grid, hipStream_t s) {
     return hipGetLastError();
   }
   if (p.variant == 1) return dispatch_w(p, grid, s, std::make_integer_sequence<int, kMaxWSpecialised>{});
-  return dispatch_b(p, grid, s, std::make_integer_sequence<int, 6>{});
+  return dispatch_b(p, grid, s, std::make_integer_sequence<int, 12>{});
 }
 
 int lockstep_grid(const KParams &p, int device) {
