@@ -1,13 +1,13 @@
 // benor_blocked.hip -- the blocked lockstep kernel (32 < W <= 64 receiver
-// groups, processed in NB = ceil(W/16) runtime blocks of G = ceil(W/NB) in
-// 11..16 groups) and its launcher.
+// groups, processed in NB runtime blocks of G = ceil(W/NB) in 11..22 groups,
+// NB chosen by plan_geometry for the fewest padded groups) and its launcher.
 #include "benor_device.h"
 
 namespace benor {
 
 // --------------------------------------------- blocked kernel (1024 < m <= 4096)
-// Receiver groups are processed in NB blocks of G (NB = ceil(W/16), G =
-// ceil(W/NB), padding < NB groups); the record loop over the W plane words is
+// Receiver groups are processed in NB blocks of G (see plan_geometry); the
+// record loop over the W plane words is
 // a runtime loop.  Per-lane `decided` bits live in registers (one word per
 // block).  Otherwise as the W-specialised kernel.
 // Word-major tallies: each plane word is applied to all G receiver groups

@@ -768,7 +768,7 @@ static hipError_t dispatch_w(const KParams &p, int grid, hipStream_t s, std::int
   return e;
 }
 
-// W in 33..64: G = ceil(W / ceil(W/16)) in 11..16
+// W in 33..64: G in 11..22 (plan_geometry)
 template <int... Is>
 static hipError_t dispatch_b(const KParams &p, int grid, hipStream_t s, std::integer_sequence<int, Is...>) {
   hipError_t e = hipErrorInvalidValue;
