@@ -7,9 +7,9 @@ namespace benor {
 
 // --------------------------------------------- blocked kernel (1024 < m <= 4096)
 // Receiver groups are processed in NB blocks of G (see plan_geometry); the
-// record loop over the W plane words is
-// a runtime loop.  Per-lane `decided` bits live in registers (one word per
-// block).  Otherwise as the W-specialised kernel.
+// record loop over the W plane words is a runtime loop.  Per-lane `decided`
+// bits live in the wave's LDS slice (one word per block).  Otherwise as the
+// W-specialised kernel.
 // Word-major tallies: each plane word is applied to all G receiver groups
 // before the next word, so consecutive v_bcnt are independent (tally_ordered
 // keeps that order; see benor_device.h).

@@ -65,7 +65,7 @@ void plan_geometry(KParams &p);
 hipError_t launch_lockstep(const KParams &p, int grid_blocks, hipStream_t stream);
 
 // Per-shape launchers, explicitly instantiated in benor_w_*.hip (W = 1..32)
-// and benor_blocked.hip (G = 11..16).
+// and benor_blocked.hip (G = 11..22).
 template <int W>
 hipError_t launch_w(const KParams &p, int grid_blocks, hipStream_t stream);
 template <int G>
