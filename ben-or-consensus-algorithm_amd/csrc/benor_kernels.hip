@@ -739,14 +739,15 @@ void plan_geometry(KParams &p) {
     p.wave_bytes = (tb * WP + 2u * WP) * 8u;            // init ring, final x1 plane, decided bits
   } else {
     // Blocks of G = ceil(W / nb) in 11..22 groups: the fewest padded groups nb * G,
-    // ties to G <= 16 (5-7 waves/SIMD; G > 16 runs at 4-5), then to fewer blocks.
-    // v19 A/B (profiles/r01-v19_ab_blocked_g.txt): one padded group fewer at G = 19..22
-    // is +3-6 %; the same padding at G > 16 is 1-2 % slower.
+    // ties to fewer blocks (larger G: more v_bcnt per LDS read and loop step, which
+    // outweighs 4-5 waves/SIMD at G > 16 against 5-7 at G <= 16).  v19 A/B
+    // (profiles/r01-v19_ab_blocked_g.txt): one padded group fewer is +3-7 %; on ties
+    // the larger G is -0.3..+1.9 %.
     uint32_t nb = (W + 15u) / 16u, G = (W + nb - 1u) / nb;
     for (uint32_t n = (W + 21u) / 22u; n <= (W + 10u) / 11u; ++n) {
       const uint32_t g = (W + n - 1u) / n;
       if (g < 11u || g > 22u) continue;
-      const bool better = n * g < nb * G || (n * g == nb * G && g <= 16u && (G > 16u || n < nb));
+      const bool better = n * g < nb * G || (n * g == nb * G && n < nb);
       if (better) {
         nb = n;
         G = g;
