@@ -32,6 +32,7 @@ BO_ERR_NO_DEVICE = 4
 BO_ERR_HIP = 5
 BO_ERR_OUT_OF_RANGE = 6
 BO_ERR_UNSUPPORTED = 7
+BO_ERR_ALREADY_STARTED = 8
 BO_MODE_LOCKSTEP = 0
 BO_MODE_RANDOM_DELIVERY = 1
 BO_MODE_EVENT = 2
@@ -50,7 +51,7 @@ EXPORTED_SYMBOLS = (
     "bo_get_state", "bo_status", "bo_network_size", "bo_network_destroy", "bo_hist_len",
     "bo_plan_create", "bo_plan_launch", "bo_plan_run", "bo_plan_popc_words_per_node_round",
     "bo_plan_live_nodes", "bo_plan_destroy", "bo_run_trials", "bo_run_trial_states",
-    "bo_popc_peak", "bo_last_error", "bo_abi_version",
+    "bo_popc_peak", "bo_last_error", "bo_abi_version", "bo_kernel_version",
 )
 
 
@@ -118,6 +119,7 @@ def lib() -> ctypes.CDLL:
     L.bo_popc_peak.restype = ctypes.c_double
     L.bo_last_error.restype = ctypes.c_char_p
     L.bo_abi_version.restype = ctypes.c_int
+    L.bo_kernel_version.restype = ctypes.c_char_p
     _lib = L
     return L
 
@@ -355,6 +357,11 @@ def run_trial_states(N: int, F: int, faulty: Sequence[bool], *, seed: int = 0, t
     rounds = ctypes.c_uint32(0)
     _check(lib().bo_run_trial_states(ctypes.byref(cfg), trial, st, ctypes.byref(rounds)))
     return int(rounds.value), [_state_dict(st[i]) for i in range(N)]
+
+
+def kernel_version() -> str:
+    """Digest of the kernel sources libbenor.so was built from."""
+    return lib().bo_kernel_version().decode()
 
 
 def popc_peak(iters: int = 20) -> float:

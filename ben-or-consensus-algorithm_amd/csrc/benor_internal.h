@@ -30,7 +30,7 @@ struct KParams {
   uint32_t W;               // u64 words per plane = ceil(m / 64) = receiver groups
   uint32_t G;               // receiver groups per tally block (template parameter)
   uint32_t nblocks;         // ceil(W / G)
-  uint32_t variant;         // 5: packed lockstep (m <= 32), 1: W-specialised lockstep (W <= 16),
+  uint32_t variant;         // 5: packed lockstep (m <= 32), 1: W-specialised lockstep (W <= kMaxWSpecialised = 32),
                             // 0: blocked lockstep, 2: random delivery, 4: event level
   uint32_t mode;            // BO_MODE_LOCKSTEP / BO_MODE_RANDOM_DELIVERY
   uint32_t q;               // quorum N - F (messages each receiver tallies per phase)

@@ -14,6 +14,7 @@
 #include <string>
 #include <algorithm>
 #include <cstdlib>
+#include <mutex>
 #include <vector>
 
 #include "benor.h"
@@ -60,11 +61,17 @@ __global__ void add_bin_kernel(unsigned long long *hist, uint32_t bin, unsigned 
 
 }  // namespace
 
+// One simulated network.  `mu` guards the node states: bo_consensus_start may
+// run on a worker thread (the N-API addon's napi_async_work) while the caller's
+// thread serves /stop, /getState and /status.  The kernel runs without the
+// lock; its results are merged under it.
 struct bo_network {
   uint32_t N = 0, F = 0;
   std::vector<bo_node_state> st;
   std::vector<uint8_t> faulty;
-  uint64_t starts = 0;
+  bool started = false;     // GET /start was served (node.ts:167-188); inboxes persist after it
+  bool in_flight = false;   // a start's kernel is running
+  mutable std::mutex mu;
 };
 
 struct bo_plan {
@@ -83,6 +90,10 @@ extern "C" {
 
 const char *bo_last_error(void) { return g_err.c_str(); }
 int bo_abi_version(void) { return BENOR_ABI_VERSION; }
+#ifndef BENOR_KERNEL_SHA
+#define BENOR_KERNEL_SHA "unknown"
+#endif
+const char *bo_kernel_version(void) { return BENOR_KERNEL_SHA; }
 uint32_t bo_hist_len(uint32_t k_max) { return (k_max + 1u) * 3u + 1u; }
 
 // ------------------------------------------------------------ network API
@@ -92,6 +103,7 @@ int bo_network_create(uint32_t N, uint32_t F, const int8_t *init, uint32_t n_ini
   *out = nullptr;
   // launchNodes.ts:10-11
   if (n_init != n_faulty || N != n_init) return fail(BO_ERR_ARRAYS_DONT_MATCH, "Arrays don't match");
+  if (N > 0 && (!init || !faulty)) return fail(BO_ERR_INVALID_ARGUMENT, "initial_values / faulty_list is NULL");
   uint32_t cnt = 0;
   for (uint32_t i = 0; i < n_faulty; ++i) cnt += faulty[i] ? 1u : 0u;
   // launchNodes.ts:12-13
@@ -123,12 +135,14 @@ void bo_network_destroy(bo_network *net) { delete net; }
 int bo_status(const bo_network *net, uint32_t i) {   // node.ts:33-39
   if (!net) return -fail(BO_ERR_INVALID_ARGUMENT, "net is NULL");
   if (i >= net->N) return -fail(BO_ERR_OUT_OF_RANGE, "node index out of range");
+  std::lock_guard<std::mutex> g(net->mu);
   return net->st[i].killed ? 500 : 200;
 }
 
 int bo_get_state(const bo_network *net, uint32_t i, bo_node_state *out) {   // node.ts:197-199
   if (!net || !out) return fail(BO_ERR_INVALID_ARGUMENT, "NULL argument");
   if (i >= net->N) return fail(BO_ERR_OUT_OF_RANGE, "node index out of range");
+  std::lock_guard<std::mutex> g(net->mu);
   *out = net->st[i];
   return BO_OK;
 }
@@ -136,12 +150,14 @@ int bo_get_state(const bo_network *net, uint32_t i, bo_node_state *out) {   // n
 int bo_node_stop(bo_network *net, uint32_t i) {   // node.ts:191-194
   if (!net) return fail(BO_ERR_INVALID_ARGUMENT, "net is NULL");
   if (i >= net->N) return fail(BO_ERR_OUT_OF_RANGE, "node index out of range");
+  std::lock_guard<std::mutex> g(net->mu);
   net->st[i].killed = 1;
   return BO_OK;
 }
 
 int bo_consensus_stop(bo_network *net) {   // consensus.ts:10-15
   if (!net) return fail(BO_ERR_INVALID_ARGUMENT, "net is NULL");
+  std::lock_guard<std::mutex> g(net->mu);
   for (auto &s : net->st) s.killed = 1;
   return BO_OK;
 }
@@ -150,24 +166,42 @@ int bo_consensus_start(bo_network *net, uint64_t seed, uint32_t k_max) {   // co
   if (!net) return fail(BO_ERR_INVALID_ARGUMENT, "net is NULL");
   if (k_max < 1 || k_max > BO_MAX_K) return fail(BO_ERR_INVALID_ARGUMENT, "k_max out of range");
   const uint32_t N = net->N;
-  // Nodes that run: not killed (faulty from launch, or stopped).  They send
-  // and receive; killed nodes do neither (node.ts:45, :171).
+  std::vector<uint8_t> crashed(N);
+  std::vector<int8_t> x(N);
   std::vector<uint32_t> active;
-  for (uint32_t i = 0; i < N; ++i)
-    if (!net->st[i].killed) active.push_back(i);
-  if (active.empty()) return BO_OK;
-  const int64_t quorum = (int64_t)N - (int64_t)net->F;
-  // Fewer running senders than the quorum: no R-phase ever triggers
-  // (node.ts:52), every running node stays at k = 1, undecided.
-  if ((int64_t)active.size() < quorum) {
-    for (uint32_t i : active) net->st[i].k = 1;   // node.ts:172
-    ++net->starts;
-    return BO_OK;
+  {
+    std::lock_guard<std::mutex> g(net->mu);
+    // The reference's per-node inboxes (node.ts:29-30) live as long as the
+    // server: a second GET /start pushes round-1 messages onto inboxes that
+    // already hold them, and every push past N-F re-triggers the tally
+    // (node.ts:47-52).  That is not a fresh consensus, so it is refused.
+    if (net->started)
+      return fail(BO_ERR_ALREADY_STARTED, net->in_flight
+                  ? "consensus is already running on this network"
+                  : "consensus already started on this network: node inboxes persist across /start "
+                    "(node.ts:29-30), launch a new network to run again");
+    // Nodes that run: not killed (faulty from launch, or stopped).  They send
+    // and receive; killed nodes do neither (node.ts:45, :171).
+    for (uint32_t i = 0; i < N; ++i) {
+      crashed[i] = net->st[i].killed ? 1 : 0;
+      x[i] = net->st[i].killed ? 0 : net->st[i].x;
+      if (!net->st[i].killed) active.push_back(i);
+    }
+    if (active.empty()) { net->started = true; return BO_OK; }
+    const int64_t quorum = (int64_t)N - (int64_t)net->F;
+    // Fewer running senders than the quorum: no R-phase ever triggers
+    // (node.ts:52), every running node stays at k = 1, undecided.
+    if ((int64_t)active.size() < quorum) {
+      for (uint32_t i : active) net->st[i].k = 1;   // node.ts:172
+      net->started = true;
+      return BO_OK;
+    }
+    int dev = 0;
+    const int rc = check_device(&dev);
+    if (rc) return rc;
+    net->started = true;
+    net->in_flight = true;
   }
-  int dev = 0;
-  int rc = check_device(&dev);
-  if (rc) return rc;
-  const uint64_t trial = net->starts++;
 
   bo_trials_cfg cfg{};
   cfg.N = N;
@@ -176,21 +210,23 @@ int bo_consensus_start(bo_network *net, uint64_t seed, uint32_t k_max) {   // co
   cfg.init_mode = BO_INIT_FIXED;
   cfg.mode = BO_MODE_LOCKSTEP;
   cfg.seed = seed;
-  std::vector<uint8_t> crashed(N);
-  std::vector<int8_t> x(N);
-  for (uint32_t i = 0; i < N; ++i) {
-    crashed[i] = net->st[i].killed ? 1 : 0;
-    x[i] = net->st[i].killed ? 0 : net->st[i].x;
-  }
   cfg.faulty = crashed.data();
   cfg.init = x.data();
   // Launch-time validation is already done; here the crashed set is the
   // killed set, which has exactly N - quorum = F members at this point.
   std::vector<bo_node_state> states(N);
   uint32_t rounds = 0;
-  rc = bo_run_trial_states(&cfg, trial, states.data(), &rounds);
+  const int rc = bo_run_trial_states(&cfg, 0, states.data(), &rounds);
+  std::lock_guard<std::mutex> g(net->mu);
+  net->in_flight = false;
   if (rc) return rc;
-  for (uint32_t i : active) net->st[i] = states[i];
+  // A GET /stop served while the kernel ran is ordered after the run: the
+  // node keeps its final x / decided / k and stays killed.
+  for (uint32_t i : active) {
+    const int8_t killed = net->st[i].killed;
+    net->st[i] = states[i];
+    net->st[i].killed = killed;
+  }
   return BO_OK;
 }
 

@@ -15,8 +15,12 @@
 // node has received /start -- the point at which, in the reference, all live
 // nodes have broadcast their round-1 proposals.  Until then a started node
 // reports k = 1 (node.ts:172).  Messages POSTed from outside are acknowledged
-// and not simulated.  Unlike the reference (node.ts:45,161), killed nodes
-// answer /message with 500 "faulty" instead of never answering.
+// and not simulated; as in the reference (node.ts:45,161), a killed node
+// never answers /message (the request stays open until the server closes).
+// The round loop runs once per network: the reference's round inboxes
+// (node.ts:29-30) outlive a run, so a later /start is acknowledged as the
+// reference acknowledges it but starts no second run (bo_consensus_start
+// refuses a second start on a network, include/benor.h).
 const http = require('http');
 const path = require('path');
 const addon = require(path.join(__dirname, 'benor.node'));
@@ -87,8 +91,8 @@ async function launchNetwork(N, F, initialValues, faultyList, options = {}) {
       }
       if (req.method === 'POST' && url === '/message') {
         req.resume();
-        return addon.getState(handle, i).killed ? send(res, 500, 'faulty')
-          : send(res, 200, { message: 'Message received' }, true);
+        if (addon.getState(handle, i).killed) return undefined;   // node.ts:45,161: no reply
+        return send(res, 200, { message: 'Message received' }, true);
       }
       return send(res, 404, 'not found');
     };

@@ -5,7 +5,9 @@
 // half are faulty), then launchNetwork + startConsensus, then prints the
 // nodes' states (the reference logs them from each node's handler instead).
 //
-// Optional: --faulty 0,1,2,3  --init 1,1,...,?  --seed S  --kMax K
+// Optional: --N 10  --faulty 0,1,2,3  --init 1,1,...,?  --seed S  --kMax K
+// (faultyArray has N entries, the ids listed in --faulty set; N defaults to the
+// length of --init, so the two arrays can differ as in start.ts:7-21)
 const benor = require('./index.js');
 
 function arg(name) {
@@ -16,7 +18,8 @@ function arg(name) {
 async function main() {
   const init = (arg('init') || '1,1,1,1,1,1,1,1,1,1').split(',').map((v) => (v === '?' ? '?' : Number(v)));
   const faultyIds = new Set((arg('faulty') || '0,1,2,3').split(',').filter((v) => v !== '').map(Number));
-  const faultyArray = init.map((_, i) => faultyIds.has(i));
+  const N = arg('N') !== undefined ? Number(arg('N')) : init.length;
+  const faultyArray = Array.from({ length: N }, (_, i) => faultyIds.has(i));
 
   if (init.length !== faultyArray.length) throw new Error("Lengths don't match");            // start.ts:22-23
   if (faultyArray.filter((f) => f === true).length > init.length / 2)                        // start.ts:25-29

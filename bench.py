@@ -3,11 +3,16 @@
 Workload (BASELINE configs[3], the metric's config): N = 1024 nodes, F = 341
 crash-faulty (the first F node ids, as in src/start.ts:7-18), iid
 Bernoulli(1/2) initial values from Philox, lockstep delivery (the reference's
-semantics for its admissible inputs), k_max = 16.  One step = one launch of
-`--trials` independent trials per GPU (default 10^8) + the RCCL all-reduce of
-the outcome histogram.  Weak scaling: every rank runs its own global trial-id
-range [(step * world + rank) * T, +T), so the merged histogram is independent
-of the GPU count.
+semantics for its admissible inputs), k_max = 16.  One step = one launch per
+GPU + the RCCL all-reduce of the outcome histogram.
+
+  --scaling strong (default; configs[3] as written): every step runs 10^8
+         trials in total, split into `world` contiguous shards of global
+         trial ids [step * T, +T) (benor.parallel.strong_range);
+  --scaling weak: every rank runs its own T trials per step, global ids
+         [(step * world + rank) * T, +T).
+Philox counters are keyed by the global trial id, so the merged histogram
+depends only on the set of trial ids, never on the GPU count (`hist_sha256`).
 
 value  = live node-rounds simulated by all ranks / timed seconds (max over ranks)
          (a live node-round = one live node executing one R-phase and one
@@ -20,14 +25,21 @@ roofline: per-receiver tally popcount words per live node-round (m = N - F
          v_bcnt_u32_b32 issue peak (256 CU x 4 SIMD x 16 lanes x 2.4 GHz =
          39.3 T words/s).
 cpu_baseline: the oracle's bit-plane restatement (oracle/benor_oracle.c,
-         OpenMP over trials) on a bounded sample, rank 0 at N = 1 only.
+         OpenMP over trials) on a bounded sample, rank 0 at N = 1 only, on
+         every host thread and on one core.
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
-torch.distributed.run (one process per GPU, backend nccl = RCCL).
+Launch: python bench.py [--gpus N --steps K --warmup W].  For N > 1 the
+driver starts it under torch.distributed.run (one process per GPU, backend
+nccl = RCCL); started without a launcher, bench.py starts the N ranks itself
+(before touching the GPU) and exits with their status.  A WORLD_SIZE that
+differs from --gpus is an error, never a silent single-GPU run.
 """
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -39,24 +51,32 @@ METRIC = "simulated node-rounds/sec at N=1024,F=341, 1–8 GPUs; % of INT/popcou
 # v_bcnt_u32_b32 issues one wave64 instruction per 4 cycles per SIMD (16 lanes/clk;
 # tools/valu_probe.hip, profiles/r01-v8_valu_probe.txt: 4.15-4.2 cyc at full occupancy,
 # vs 2.4-2.5 for v_and_b32 / v_add_u32), so the popcount roofline of the chip is
-# 256 CU x 4 SIMD x 16 lanes x 2.4 GHz.
+# 256 CU x 4 SIMD x 16 lanes x 2.4 GHz.  The same figure is the chip's VALU
+# lane-op issue peak for 4-cycle VALU ops (v_cmp, SGPR-operand ops, Philox's
+# v_mad_u64_u32 / v_bitop3_b32), used for the small-network kernel.
 SPEC_PEAK_POPC = 256 * 4 * 16 * 2.4e9
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
+                    help="strong: --trials in total per step, split over the ranks (configs[3]); "
+                         "weak: --trials per rank per step")
     ap.add_argument("--N", type=int, default=1024)
     ap.add_argument("--F", type=int, default=341)
-    ap.add_argument("--trials", type=int, default=100_000_000, help="trials per GPU per step")
+    ap.add_argument("--trials", type=int, default=100_000_000)
     ap.add_argument("--k-max", type=int, default=16)
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x243F6A8885A308D3)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample budget (0 = skip)")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0,
+                    help="CPU-baseline sample budget on all host threads (0 = skip); the 1-core leg gets 2/3 of it")
     ap.add_argument("--no-peak-probe", action="store_true")
     ap.add_argument("--no-other-configs", action="store_true", help="skip the configs[1]/[2] side measurements")
-    return ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="print this rank's place in the launch (world, rank, trial shards) and exit before any GPU work")
+    return ap.parse_args(argv)
 
 
 def node_rounds(hist, m, k_max):
@@ -69,6 +89,39 @@ def node_rounds(hist, m, k_max):
     return total_rounds * m, total_rounds
 
 
+def hist_digest(hist):
+    """Digest of a merged outcome histogram (uint64 little-endian bins)."""
+    import numpy as np
+
+    return hashlib.sha256(np.asarray(hist, dtype="<u8").tobytes()).hexdigest()[:16]
+
+
+def rank_range(scaling, step, rank, world, trials):
+    from benor.parallel import strong_range, weak_range
+
+    if scaling == "strong":
+        return strong_range(step * trials, trials, rank, world)
+    return weak_range(step, rank, world, trials)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n, argv):
+    """Start n ranks of this script under torch.distributed.run (one process
+    per GPU) and return their exit status.  Called before anything here
+    touches the GPU; the children are separate processes (no exec)."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    return subprocess.run(cmd, env=env).returncode
+
+
 # BASELINE configs[1] and [2] (one GPU): measured after the timed region and
 # reported beside the headline, not part of `value`.
 OTHER_CONFIGS = [("C2 N=10,F=4", 10, 4, 1_000_000), ("C2 N=10,F=5 (F>N/2, no decision)", 10, 5, 1_000_000),
@@ -76,6 +129,19 @@ OTHER_CONFIGS = [("C2 N=10,F=4", 10, 4, 1_000_000), ("C2 N=10,F=5 (F>N/2, no dec
 
 
 def other_configs(benor, torch, k_max, seed):
+    """One launch per config, HIP-event kernel time, and the roofline of the
+    kernel that runs it:
+      * m > 32 (W kernel): popcount words per live node-round
+        (bo_plan_popc_words_per_node_round) against the v_bcnt issue peak;
+      * m <= 32 (packed kernel, floor(32/m) trials per half wave): VALU issue.
+        Its algorithmic lane-ops per live node-round are the tally popcounts
+        (2 or 3 one-word counts), the proposal compare, the decision compare
+        and the all-decided check (3), plus one Philox4x32-10 word per coin
+        flip (41 lane-ops per 4-word block).  Coins are flipped
+        by every live node in every tie round; a deciding trial that halted
+        after round R had R - 1 of them (an R-phase tie is the only way not to
+        decide when N > 2F).  Undecided trials are counted with
+        none, so the figure is a lower bound when they exist."""
     import numpy as np
 
     stream = torch.cuda.current_stream()
@@ -93,10 +159,26 @@ def other_configs(benor, torch, k_max, seed):
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1)
         hist = h.cpu().numpy().astype(np.uint64)
-        nr, rounds = node_rounds(hist, plan.live_nodes, k_max)
+        m = plan.live_nodes
+        nr, rounds = node_rounds(hist, m, k_max)
         undecided = int(hist[0] + hist[1] + hist[2])
+        words = plan.popc_words_per_node_round
+        if m > 32:
+            roof = {"bound": "valu (v_bcnt_u32_b32 issue)", "kernel": "lockstep W kernel",
+                    "unit": "Tpopc/s", "popc_words_per_node_round": words,
+                    "achieved": nr * words / (ms * 1e-3) / 1e12}
+        else:
+            decided = T - undecided
+            tie_rounds = (rounds - k_max * undecided) - decided
+            ops = nr * (words + 3) + tie_rounds * m * 41 / 4
+            roof = {"bound": "valu issue (tallies, compares, Philox coins)", "kernel": "packed",
+                    "unit": "T lane-ops/s", "lane_ops_per_node_round": ops / max(nr, 1),
+                    "achieved": ops / (ms * 1e-3) / 1e12}
+        roof["peak"] = SPEC_PEAK_POPC / 1e12
+        roof["frac"] = roof["achieved"] / roof["peak"]
         out[name] = {"trials": T, "kernel_ms": ms, "node_rounds_per_s": nr / (ms * 1e-3),
-                     "trials_per_s": T / (ms * 1e-3), "mean_rounds": rounds / T, "undecided_trials": undecided}
+                     "trials_per_s": T / (ms * 1e-3), "mean_rounds": rounds / T, "undecided_trials": undecided,
+                     "roofline": roof}
     return out
 
 
@@ -107,41 +189,65 @@ def cpu_baseline(N, F, k_max, seed, budget_s):
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     faulty = [i < F for i in range(N)]
     m = N - F
-    n = 100_000                     # calibration sample (~0.1 s on 16 threads)
-    t0 = time.perf_counter()
-    oracle.run_trials(N, F, faulty, seed=seed, trial_begin=0, trial_count=n, k_max=k_max, threads=threads)
-    dt = time.perf_counter() - t0
-    n2 = max(n, int(n * budget_s / max(dt, 1e-6)))
-    t0 = time.perf_counter()
-    r = oracle.run_trials(N, F, faulty, seed=seed, trial_begin=0, trial_count=n2, k_max=k_max, threads=threads)
-    dt = time.perf_counter() - t0
-    nr, _ = node_rounds(r.hist, m, k_max)
-    return {"value": nr / dt, "unit": "node-rounds/s", "cores": threads, "kind": "port",
+
+    def timed(nthreads, budget):
+        n = 100_000 if nthreads > 1 else 10_000          # calibration sample
+        t0 = time.perf_counter()
+        oracle.run_trials(N, F, faulty, seed=seed, trial_begin=0, trial_count=n, k_max=k_max, threads=nthreads)
+        dt = time.perf_counter() - t0
+        n2 = max(n, int(n * budget / max(dt, 1e-6)))
+        t0 = time.perf_counter()
+        r = oracle.run_trials(N, F, faulty, seed=seed, trial_begin=0, trial_count=n2, k_max=k_max, threads=nthreads)
+        dt = time.perf_counter() - t0
+        nr, _ = node_rounds(r.hist, m, k_max)
+        return nr / dt, n2, dt
+
+    v, n2, dt = timed(threads, budget_s)
+    v1, n1, dt1 = timed(1, budget_s * 2 / 3)
+    return {"value": v, "unit": "node-rounds/s", "cores": threads, "kind": "port",
             "sample": f"{n2} trials of the bench workload (N={N}, F={F}, k_max={k_max}, same seed), "
-                      f"{dt:.1f} s, oracle/benor_oracle.c bit-plane restatement, OpenMP over trials"}
+                      f"{dt:.1f} s, oracle/benor_oracle.c bit-plane restatement, OpenMP over trials",
+            "single_core": {"value": v1, "unit": "node-rounds/s", "cores": 1,
+                            "sample": f"{n1} trials, {dt1:.1f} s, same restatement on one thread"}}
 
 
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a "
+              f"{world}-rank run as {args.gpus} GPUs", file=sys.stderr)
+        sys.exit(2)
+    if args.dry_run:
+        rank = int(os.environ.get("RANK", "0"))
+        print(json.dumps({"dry_run": True, "world": world, "rank": rank, "scaling": args.scaling,
+                          "shards": [rank_range(args.scaling, args.warmup + i, rank, world, args.trials)
+                                     for i in range(args.steps)]}), flush=True)
+        return
+
     import numpy as np
     import torch
     import torch.distributed as dist
 
     import benor
-    from benor.parallel import merge_histogram, weak_range
+    from benor.parallel import merge_histogram
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # one process per GPU; BENOR_DIST_BACKEND=gloo rehearses several ranks on one GPU
     backend = os.environ.get("BENOR_DIST_BACKEND", "nccl")
     dev = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(dev)
-    if world > 1:
+    distributed = env_world is not None          # under a launcher: the collective runs even at world 1
+    if distributed:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group(backend)
+        assert dist.get_world_size() == world
     N, F, k_max, T = args.N, args.F, args.k_max, args.trials
     faulty = [i < F for i in range(N)]
     plan = benor.TrialsPlan(N, F, faulty, seed=args.seed, k_max=k_max)
@@ -149,13 +255,21 @@ def main():
     words_per_nr = plan.popc_words_per_node_round
     H = plan.hist_len
     stream = torch.cuda.current_stream()
-    hist = torch.zeros(H, dtype=torch.int64, device="cuda")
-    step_hist = torch.zeros(H, dtype=torch.int64, device="cuda")
+    hist = torch.zeros(H + 1, dtype=torch.int64, device="cuda")
+    # the extra last bin carries 1 per rank: after the all-reduce it counts the
+    # ranks whose histograms were merged in that step
+    step_hist = torch.zeros(H + 1, dtype=torch.int64, device="cuda")
+    one = torch.ones(1, dtype=torch.int64, device="cuda")
 
-    def step(s):
+    def step(s, ev=None):
         step_hist.zero_()
-        begin, n = weak_range(s, rank, world, T)
+        step_hist[H:].copy_(one)
+        begin, n = rank_range(args.scaling, s, rank, world, T)
+        if ev:
+            ev[0].record(stream)
         plan.launch(begin, n, step_hist.data_ptr(), stream.cuda_stream)
+        if ev:
+            ev[1].record(stream)
         merge_histogram(step_hist)              # RCCL merge of the outcome histograms
         hist.add_(step_hist)
 
@@ -165,61 +279,65 @@ def main():
     hist.zero_()
     # kernel-only timing with HIP events on the launch stream
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        s = args.warmup + i
-        step_hist.zero_()
-        begin, n = weak_range(s, rank, world, T)
-        ev[i][0].record(stream)
-        plan.launch(begin, n, step_hist.data_ptr(), stream.cuda_stream)
-        ev[i][1].record(stream)
-        merge_histogram(step_hist)
-        hist.add_(step_hist)
+        step(args.warmup + i, ev[i])
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = [a.elapsed_time(b) for a, b in ev]
     t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    if world > 1:
+    if distributed:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
-    h = hist.cpu().numpy().astype(np.uint64)
-    assert int(h.sum()) == T * world * args.steps, "histogram lost trials"
+    hh = hist.cpu().numpy().astype(np.uint64)
+    h, merged_ranks = hh[:H], int(hh[H])
+    assert merged_ranks == world * args.steps, f"histogram merges saw {merged_ranks} rank-steps"
+    total_trials = T * args.steps * (1 if args.scaling == "strong" else world)
+    assert int(h[:-1].sum()) == total_trials, "histogram lost trials"   # last bin: violations (also counted)
     live_nr, rounds = node_rounds(h, m, k_max)
     value = live_nr / elapsed
-    # roofline of the dominant kernel (one launch = T trials on this rank)
-    per_launch_nr = live_nr / (world * args.steps)
+    # roofline of the dominant kernel: this rank's launches (rank 0's share of every step)
+    my_trials = rank_range(args.scaling, args.warmup, rank, world, T)[1]
+    per_launch_nr = live_nr * my_trials / total_trials
     avg_kernel_s = float(np.mean(kern_ms)) * 1e-3
     achieved = per_launch_nr * words_per_nr / avg_kernel_s
     peak_measured = None
     if not args.no_peak_probe:
         peak_measured = benor.popc_peak(10)
+    kver = benor.kernel_version()
     traffic = None
     tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tfile):
         try:
             tj = json.load(open(tfile))
-            if tj.get("N") == N and tj.get("F") == F and tj.get("trials") == T:
+            if (tj.get("N"), tj.get("F"), tj.get("trials_per_launch"), tj.get("kernel_version")) == \
+                    (N, F, my_trials, kver):
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
+    per_gpu = "per GPU" if args.scaling == "weak" else "in total"
     out = {
         "metric": METRIC, "value": value, "unit": "node-rounds/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic (Philox initial values)",
-        "config": {"workload": f"N={N},F={F} lockstep crash faults, {T} trials per GPU per step, k_max={k_max}",
-                   "N": N, "F": F, "live_nodes": m, "trials_per_gpu_per_step": T, "k_max": k_max,
+        "scaling": args.scaling, "vs_baseline": None, "dtype": "u32", "data": "synthetic (Philox initial values)",
+        "config": {"workload": f"N={N},F={F} lockstep crash faults, {T} trials {per_gpu} per step, k_max={k_max}",
+                   "N": N, "F": F, "live_nodes": m, "trials_per_step": total_trials // args.steps,
+                   "trials_per_gpu_per_step": my_trials, "k_max": k_max,
                    "parallelism": f"dp{world} (trial-id sharding, RCCL histogram all-reduce)"},
+        "dist": {"world": world, "backend": backend if distributed else None, "ranks_merged_per_step":
+                 merged_ranks / args.steps, "hist_sha256": hist_digest(h)},
         "roofline": {"bound": "valu (v_bcnt_u32_b32 issue)", "achieved": achieved / 1e12, "peak": SPEC_PEAK_POPC / 1e12,
                      "unit": "Tpopc/s", "frac": achieved / SPEC_PEAK_POPC, "traffic": traffic,
                      "kernel_ms": float(np.mean(kern_ms)), "popc_words_per_node_round": words_per_nr,
-                     "peak_probe": (peak_measured / 1e12) if peak_measured else None},
+                     "peak_probe": (peak_measured / 1e12) if peak_measured else None, "kernel_version": kver},
         "all_node_rounds_per_s": rounds * N / elapsed,
-        "trials_per_s": T * world * args.steps / elapsed,
+        "trials_per_s": total_trials / elapsed,
+        "agreement_violations": int(h[-1]),
     }
     if world == 1 and not args.no_other_configs:
         out["other_configs"] = other_configs(benor, torch, k_max, args.seed)
@@ -227,7 +345,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline(N, F, k_max, args.seed, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

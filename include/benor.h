@@ -12,10 +12,13 @@
  *     int8  0 -> 0,  1 -> 1,  2 -> "?",  -1 -> null (faulty node's x)
  * `decided`: -1 -> null, 0 -> false, 1 -> true;  `k`: -1 -> null.
  *
- * Threading: every function may be called from any host thread, but calls on
- * one bo_network handle must not overlap (the reference is single-threaded:
- * one Node event loop).  bo_plan_launch is asynchronous on its stream; all
- * other calls are synchronous.
+ * Threading: every function may be called from any host thread.  Calls on one
+ * bo_network handle are serialised by a lock in the handle; bo_consensus_start
+ * holds it only to read the start state and to merge the results, so /stop,
+ * /getState and /status stay served while its kernel runs (the N-API addon
+ * runs it on a worker thread).  bo_network_destroy must not overlap any other
+ * call on the handle.  bo_plan_launch is asynchronous on its stream; all other
+ * calls are synchronous.
  */
 #ifndef BENOR_H
 #define BENOR_H
@@ -26,7 +29,7 @@
 extern "C" {
 #endif
 
-#define BENOR_ABI_VERSION 2
+#define BENOR_ABI_VERSION 3
 
 /* Return codes.  The first two are the reference's two launch errors. */
 enum {
@@ -37,7 +40,8 @@ enum {
     BO_ERR_NO_DEVICE = 4,           /* no gfx950 device visible: the product never falls back to CPU */
     BO_ERR_HIP = 5,
     BO_ERR_OUT_OF_RANGE = 6,        /* node index >= N */
-    BO_ERR_UNSUPPORTED = 7          /* configuration outside what this build simulates */
+    BO_ERR_UNSUPPORTED = 7,         /* configuration outside what this build simulates */
+    BO_ERR_ALREADY_STARTED = 8      /* second start on one network: its inboxes persist (node.ts:29-30) */
 };
 
 /* Delivery model.  LOCKSTEP is the reference's semantics for its admissible
@@ -89,7 +93,11 @@ int bo_network_create(uint32_t N, uint32_t F,
  * (node.ts:167-188), then the POST /message round loop (node.ts:43-163) until
  * every live node has decided or k_max rounds ran -- one HIP kernel launch on
  * the calling thread's current device, synchronous.  `seed` keys the
- * per-node coins (node.ts:111).  Nodes already stopped act as crashed. */
+ * per-node coins (node.ts:111).  Nodes already stopped act as crashed.
+ * Runs once per network: the reference's round inboxes (node.ts:29-30) outlive
+ * a run, so a second start is not a fresh consensus and returns
+ * BO_ERR_ALREADY_STARTED.  A /stop served while the kernel runs takes effect
+ * after it: the node keeps its final state and is killed. */
 int bo_consensus_start(bo_network *net, uint64_t seed, uint32_t k_max);
 
 /* stopConsensus(N)  (consensus.ts:10-15) -> GET /stop on every node (node.ts:191-194). */
@@ -181,6 +189,10 @@ double bo_popc_peak(uint32_t iters);
 const char *bo_last_error(void);
 
 int bo_abi_version(void);
+
+/* Digest of the kernel sources this library was built from (16 hex digits).
+ * Profiles record it, so a measured figure is only quoted for the same kernels. */
+const char *bo_kernel_version(void);
 
 #ifdef __cplusplus
 }

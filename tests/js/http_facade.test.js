@@ -21,6 +21,20 @@ function get(port, route) {
     }).on('error', reject);
   });
 }
+function post(port, route, body, timeoutMs) {
+  return new Promise((resolve, reject) => {
+    const data = JSON.stringify(body);
+    const req = http.request({ host: '127.0.0.1', port, path: route, method: 'POST',
+      headers: { 'Content-Type': 'application/json', 'Content-Length': Buffer.byteLength(data) } }, (res) => {
+      let b = '';
+      res.on('data', (c) => { b += c; });
+      res.on('end', () => resolve({ status: res.statusCode, body: b }));
+    });
+    req.setTimeout(timeoutMs, () => { req.destroy(); resolve({ status: 'timeout' }); });
+    req.on('error', (e) => (e.code === 'ECONNRESET' ? resolve({ status: 'timeout' }) : reject(e)));
+    req.end(data);
+  });
+}
 const startConsensus = async (N) => { for (let i = 0; i < N; i++) await get(BASE + i, '/start'); };   // consensus.ts:3-8
 const stopConsensus = async (N) => { for (let i = 0; i < N; i++) await get(BASE + i, '/stop'); };     // consensus.ts:10-15
 const getNodesState = (N) => Promise.all(Array.from({ length: N }, (_, i) =>
@@ -55,9 +69,14 @@ it('setup: getState JSON and /stop', 'setup', async () => {
     const st = await getNodesState(3);
     assert.deepStrictEqual(st[0], { killed: true, x: null, decided: null, k: null });
     assert.deepStrictEqual(st[2], { killed: false, x: '?', decided: false, k: 0 });
+    const msg = { k: 1, x: 1, messageType: 'proposal phase' };
+    assert.strictEqual((await post(BASE + 1, '/message', msg, 2000)).status, 200);
     const r = await get(BASE + 1, '/stop');
     assert.strictEqual(r.body, 'killed');
     assert.strictEqual((await get(BASE + 1, '/status')).status, 500);
+    // node.ts:45,161: a killed node (faulty or stopped) never answers /message
+    assert.strictEqual((await post(BASE + 1, '/message', msg, 300)).status, 'timeout');
+    assert.strictEqual((await post(BASE + 0, '/message', msg, 300)).status, 'timeout');
   });
 });
 
@@ -88,6 +107,37 @@ for (const [name, fa, init, kind] of finality) {
     });
   });
 }
+
+// benorconsensus.test.ts:399-450 "Finality is reached - Randomized": random
+// 0/1 initial values on 7 nodes with nodes 2 and 4 faulty (m = 5, odd: one round)
+it('Finality over HTTP - Randomized', 'gpu', async () => {
+  const fa = [false, false, true, false, true, false, false];
+  for (let rep = 0; rep < 10; rep++) {
+    const init = new Array(7).fill(0).map(() => Math.round(Math.random()));
+    await withNet(fa, init, async () => {
+      await startConsensus(fa.length);
+      const t = Date.now();
+      let states = await getNodesState(fa.length);
+      while (Date.now() - t < 2000 && !reachedFinality(states)) { await delay(200); states = await getNodesState(fa.length); }
+      const vals = [];
+      states.forEach((s, i) => {
+        if (fa[i]) { assert.strictEqual(s.decided, null); assert.strictEqual(s.x, null); assert.strictEqual(s.k, null); return; }
+        assert.ok(s.decided); assert.notStrictEqual(s.x, null); vals.push(s.x);
+      });
+      assert.ok(vals.every((v) => v === vals[0]));
+    });
+  }
+});
+
+it('A second round of /start runs nothing new (inboxes persist, node.ts:29-30)', 'gpu', async () => {
+  await withNet([false, false, false, false, true], [1, 1, 1, 0, 0], async () => {
+    await startConsensus(5);
+    const a = await getNodesState(5);
+    await startConsensus(5);
+    assert.strictEqual((await get(BASE, '/start')).status, 200);
+    assert.deepStrictEqual(await getNodesState(5), a);
+  });
+});
 
 (async () => {
   let fail = 0, ran = 0;

@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol():
     L = benor.lib()
     for s in header_symbols():
         assert hasattr(L, s)
-    assert L.bo_abi_version() == 2
+    assert L.bo_abi_version() == 3
     assert L.bo_hist_len(64) == 65 * 3 + 1
 
 
@@ -86,6 +86,28 @@ def test_reference_accepts_what_it_accepts():
     benor.launchNetwork(4, 3, ["?", 1, 0, 1], [True, True, True, False])
     benor.launchNetwork(2, 2, [1, 1], [True, True])
     assert benor.getNodesState(2)[0]["x"] is None
+
+
+def test_second_start_refused_without_gpu_work():
+    """A start that stalls (a node stopped first: fewer than N-F senders,
+    node.ts:52) needs no device; a second start is refused either way --
+    the reference's inboxes persist across /start (node.ts:29-30)."""
+    nodes = benor.launchNetwork(5, 1, [1, 1, 1, 0, 0], [False, False, False, False, True])
+    nodes[0]._net.stop_node(0)
+    benor.startConsensus(5, seed=3)
+    assert [s["k"] for s in benor.getNodesState(5)] == [0, 1, 1, 1, None]
+    with pytest.raises(RuntimeError, match="libbenor error 8: consensus already started"):
+        benor.startConsensus(5, seed=3)
+
+
+def test_network_create_null_arrays():
+    L = benor.lib()
+    import ctypes
+
+    h = ctypes.c_void_p()
+    assert L.bo_network_create(3, 0, None, 3, None, 3, ctypes.byref(h)) == benor.BO_ERR_INVALID_ARGUMENT
+    assert L.bo_network_create(0, 0, None, 0, None, 0, ctypes.byref(h)) == benor.BO_OK
+    L.bo_network_destroy(h)
 
 
 @pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="a GPU is present: the loud-failure path is not reachable")

@@ -43,36 +43,89 @@ def test_bench_helpers():
     assert live_nr == rounds * 7
 
 
+def test_bench_self_launch_dry_run():
+    """`bench.py --gpus 2` without a launcher starts two ranks itself; every
+    rank sees WORLD_SIZE=2 and the strong-scaling shards partition each step."""
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--dry-run", "--steps", "2", "--warmup", "1",
+                        "--trials", "1001"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = sorted((json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")), key=lambda d: d["rank"])
+    assert [d["rank"] for d in lines] == [0, 1] and all(d["world"] == 2 for d in lines)
+    for i in range(2):
+        (b0, n0), (b1, n1) = lines[0]["shards"][i], lines[1]["shards"][i]
+        assert b0 == (1 + i) * 1001 and b0 + n0 == b1 and n0 + n1 == 1001
+
+
+def test_bench_refuses_world_mismatch():
+    env = dict(os.environ, WORLD_SIZE="1")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "8", "--dry-run"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2 and "WORLD_SIZE=1" in r.stderr
+
+
+def _run_bench(args, env_extra=None, launcher=None, timeout=300):
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", **(env_extra or {}))
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable] + (launcher or []) + ["bench.py"] + args
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return _json_line(r.stdout)
+
+
 @pytest.mark.gpu
 def test_bench_single_gpu_line():
-    env = dict(os.environ)
-    r = subprocess.run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--trials", "4000000",
-                        "--cpu-seconds", "1", "--no-peak-probe"], cwd=ROOT, env=env, capture_output=True,
-                       text=True, timeout=240)
-    assert r.returncode == 0, r.stderr[-2000:]
-    d = _json_line(r.stdout)
-    assert d["n_gpus"] == 1 and d["value"] > 0 and d["unit"] == "node-rounds/s"
+    d = _run_bench(["--steps", "2", "--warmup", "1", "--trials", "4000000", "--cpu-seconds", "1", "--no-peak-probe"])
+    assert d["n_gpus"] == 1 and d["value"] > 0 and d["unit"] == "node-rounds/s" and d["scaling"] == "strong"
     assert 0 < d["roofline"]["frac"] < 1.0
+    assert d["dist"]["world"] == 1 and d["dist"]["backend"] is None and d["agreement_violations"] == 0
     assert d["cpu_baseline"]["value"] > 0 and d["cpu_baseline"]["kind"] == "port"
-    # BASELINE configs[1] and [2] beside the headline
+    assert d["cpu_baseline"]["single_core"]["cores"] == 1 and d["cpu_baseline"]["single_core"]["value"] > 0
+    # BASELINE configs[1] and [2] beside the headline, each with its roofline
     oc = d["other_configs"]
     assert oc["C2 N=10,F=4"]["undecided_trials"] == 0 and oc["C2 N=10,F=4"]["mean_rounds"] > 1.3
     assert oc["C2 N=10,F=5 (F>N/2, no decision)"]["undecided_trials"] == 1_000_000
     assert oc["C3 N=256,F=85"]["mean_rounds"] == 1.0 and oc["C3 N=256,F=85"]["node_rounds_per_s"] > 0
+    for v in oc.values():
+        assert 0 < v["roofline"]["frac"] < 1.0 and v["roofline"]["bound"]
+    assert oc["C3 N=256,F=85"]["roofline"]["popc_words_per_node_round"] == 12
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("ranks", [2, 4])
-def test_bench_ranks_gloo_one_gpu(ranks):
-    env = dict(os.environ, BENOR_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(ranks),
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", str(ranks),
-           "--steps", "2", "--warmup", "1", "--trials", "1000000", "--no-peak-probe"]
-    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0, r.stderr[-2000:]
-    d = _json_line(r.stdout)
-    assert d["n_gpus"] == ranks and d["scaling"] == "weak"
-    # every rank ran its own 10^6 trials per step; rank 0's merged histogram saw them all
-    assert d["trials_per_s"] * d["ms_per_step"] * 1e-3 == pytest.approx(ranks * 1_000_000, rel=1e-6)
-    assert "cpu_baseline" not in d
-    assert "other_configs" not in d
+def test_bench_nccl_world_one_under_launcher():
+    """The RCCL branch: torch.distributed.run with one rank, backend nccl."""
+    d = _run_bench(["--gpus", "1", "--steps", "2", "--warmup", "1", "--trials", "1000000", "--no-peak-probe",
+                    "--no-other-configs", "--cpu-seconds", "0"],
+                   launcher=["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                             "--master-addr", "127.0.0.1", "--master-port", str(_free_port())])
+    assert d["n_gpus"] == 1 and d["dist"] == {**d["dist"], "world": 1, "backend": "nccl", "ranks_merged_per_step": 1}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scaling", ["strong", "weak"])
+def test_bench_self_launched_ranks_match_one_rank(scaling):
+    """`bench.py --gpus 2` (no launcher; two ranks on one GPU over gloo) reports
+    n_gpus 2 and merges a histogram bit-identical to one rank running the same
+    trial ids."""
+    common = ["--steps", "2", "--warmup", "1", "--no-peak-probe", "--no-other-configs", "--cpu-seconds", "0"]
+    T = 1_000_000
+    one = _run_bench(["--gpus", "1", "--scaling", scaling, "--trials", str(T if scaling == "strong" else 2 * T)]
+                     + common)
+    two = _run_bench(["--gpus", "2", "--scaling", scaling, "--trials", str(T)] + common,
+                     env_extra={"BENOR_DIST_BACKEND": "gloo"})
+    assert two["n_gpus"] == 2 and two["dist"]["world"] == 2 and two["dist"]["ranks_merged_per_step"] == 2
+    assert two["dist"]["backend"] == "gloo" and two["scaling"] == scaling
+    assert two["dist"]["hist_sha256"] == one["dist"]["hist_sha256"]
+    assert two["trials_per_s"] * two["ms_per_step"] * 1e-3 == pytest.approx(2 * T if scaling == "weak" else T,
+                                                                             rel=1e-6)
+
+
+@pytest.mark.gpu
+def test_bench_four_ranks_gloo_one_gpu():
+    d = _run_bench(["--gpus", "4", "--steps", "2", "--warmup", "1", "--trials", "1000000", "--no-peak-probe"],
+                   env_extra={"BENOR_DIST_BACKEND": "gloo"},
+                   launcher=["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+                             "--master-addr", "127.0.0.1", "--master-port", str(_free_port())])
+    assert d["n_gpus"] == 4 and d["dist"]["ranks_merged_per_step"] == 4
+    assert "cpu_baseline" not in d and "other_configs" not in d

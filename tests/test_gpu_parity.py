@@ -124,14 +124,38 @@ def test_stopped_nodes_stall():
     assert all(s["k"] == 1 and s["decided"] is False for s in st[1:4])
 
 
-def test_restart_runs_from_current_values():
+def test_second_start_is_refused():
+    """The reference's round inboxes (node.ts:29-30) outlive a run, so a second
+    GET /start re-triggers every round-1 tally (node.ts:47-52) instead of
+    running a fresh consensus: the network API refuses it and keeps the
+    first run's states."""
     benor.launchNetwork(6, 2, [0, 0, 1, 1, 0, 1], [True, False, False, False, False, True])
     benor.startConsensus(6, seed=1)
     a = benor.getNodesState(6)
-    benor.startConsensus(6, seed=1)   # second start: fresh run from the decided x
-    b = benor.getNodesState(6)
-    assert all(s["decided"] for s in b[1:5])
-    assert [s["x"] for s in a] == [s["x"] for s in b]
+    with pytest.raises(RuntimeError, match="already started"):
+        benor.startConsensus(6, seed=1)
+    assert benor.getNodesState(6) == a and all(s["decided"] for s in a[1:5])
+
+
+def test_stop_during_run_is_kept():
+    """A /stop served while the kernel runs (another thread) is ordered after
+    the run: the node keeps its final state and stays killed."""
+    import threading
+
+    N = 2048
+    init = [i % 2 for i in range(N)]               # m = 2048 even and tied: coins, several rounds
+    benor.launchNetwork(N, 0, init, [False] * N)
+    net = benor._current
+    t = threading.Thread(target=lambda: benor.startConsensus(N, seed=9, k_max=64))
+    t.start()
+    net.stop_node(5)
+    t.join()
+    st = benor.getNodesState(N)
+    assert st[5]["killed"] is True and all(not s["killed"] for i, s in enumerate(st) if i != 5)
+    if st[5]["k"] == 0:        # the stop was served before the start: 2047 < N - F senders, a stall
+        assert all(s["k"] == 1 and s["decided"] is False for i, s in enumerate(st) if i != 5)
+    else:                      # served during the run: node 5 keeps its final state
+        assert st[5]["k"] == st[0]["k"] >= 2 and st[5]["decided"] == st[0]["decided"]
 
 
 @pytest.mark.parametrize("N,F", [

@@ -64,6 +64,9 @@ def test_js_start_rejects_like_start_ts():
     p = subprocess.run(["node", START_JS, "--init", "1,1,1,1", "--faulty", "0,1,2"], capture_output=True,
                        text=True, timeout=60)
     assert p.returncode == 1 and "Too many faulty nodes" in p.stderr
+    p = subprocess.run(["node", START_JS, "--N", "5", "--init", "1,1,1,1", "--faulty", "0"], capture_output=True,
+                       text=True, timeout=60)
+    assert p.returncode == 1 and "Lengths don't match" in p.stderr
 
 
 @needs_node

@@ -68,8 +68,17 @@ def main(tag, trials, N=1024, F=341):
     if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
         hbm = (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0
         lines.append(f"- HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, KiB -> B): {hbm:.0f}")
+        kver = None                  # kernel-source digest printed by the profiled bench run
+        for log in sorted(glob.glob(os.path.join(src, "pmc*.log"))):
+            for line in open(log):
+                if line.startswith("{"):
+                    try:
+                        kver = json.loads(line)["roofline"]["kernel_version"]
+                    except (ValueError, KeyError):
+                        pass
         if (N, F) == (1024, 341):   # bench.py reads the bench shape's traffic only
-            json.dump({"N": N, "F": F, "trials": trials, "hbm_bytes_per_launch": hbm,
+            json.dump({"N": N, "F": F, "trials_per_launch": trials, "kernel_version": kver,
+                       "hbm_bytes_per_launch": hbm,
                        "fetch_kib": c["FETCH_SIZE"], "write_kib": c["WRITE_SIZE"],
                        "source": f"profiles/{tag}_summary.md"},
                       open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
