@@ -113,8 +113,6 @@ __global__ void __launch_bounds__(256) benor_lockstep_blocked_kernel(KParams p) 
     keys[1] = (uint32_t)(p.seed >> 32);
     keys[2] = (uint32_t)p.trial_begin;
     keys[3] = (uint32_t)(p.trial_begin >> 32);
-    keys[4] = (uint32_t)(uintptr_t)p.live_ids;
-    keys[5] = (uint32_t)((uintptr_t)p.live_ids >> 32);
   }
   if (p.init_mode != BO_INIT_RANDOM)
     for (uint32_t w = lane; w < WP; w += 64u) {
@@ -225,8 +223,7 @@ __global__ void __launch_bounds__(256) benor_lockstep_blocked_kernel(KParams p) 
                 x1 |= ad1;
                 if (tie) {                                                // node.ts:111
                   const uint64_t trial = lds_u64(keys + 2) + t;
-                  const uint32_t *ids = reinterpret_cast<const uint32_t *>((uintptr_t)lds_u64(keys + 4));
-                  x1 |= coin_ballot(keys, (uint32_t)trial, (uint32_t)(trial >> 32), ids, b * G + g, r, tie);
+                  x1 |= coin_ballot(keys, (uint32_t)trial, (uint32_t)(trial >> 32), b * G + g, r, tie);
                 }
               }
               st = writelane<2 * g>(st, (uint32_t)x1);

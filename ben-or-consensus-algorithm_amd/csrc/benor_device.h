@@ -107,19 +107,35 @@ __device__ __forceinline__ uint64_t ballot_s(bool p) {
 }
 
 
-// Coins of the tied receivers of one group (node.ts:111).  The key words are
-// laundered through an empty asm so that Philox's ten round keys are not
-// hoisted out of the round loop into permanently live SGPRs.
+// The coin of live node c (compact index) in round r (node.ts:111): bit
+// (c & 31) of word (r-1) & 3 of the Philox block
+//   ctr = {trial_lo, trial_hi, c >> 5, ((r-1) >> 2) | kStreamCoin << 24},
+// i.e. one block holds the coins of 32 nodes for 4 rounds.  coin 1 -> x = 1
+// (the reference's Math.random() > 0.5 ? 0 : 1 with P = 1/2).
+template <bool WIDE = true>
+__device__ __forceinline__ uint4 coin_block(uint32_t k0, uint32_t k1, uint32_t tlo, uint32_t thi, uint32_t c,
+                                            uint32_t round) {
+  return philox4x32_10<WIDE>(k0, k1, make_uint4(tlo, thi, c >> 5, ((round - 1u) >> 2) | (kStreamCoin << 24)));
+}
+
+__device__ __forceinline__ uint32_t coin_word(uint4 b, uint32_t round) {
+  const uint32_t j = (round - 1u) & 3u;
+  return j == 0u ? b.x : j == 1u ? b.y : j == 2u ? b.z : b.w;
+}
+
+// Coins of the tied receivers of one group (lanes = compact nodes 64 g + l).
+// The key words are laundered through an empty asm so that Philox's ten round
+// keys are not hoisted out of the round loop into permanently live SGPRs.
 __device__ __forceinline__ uint64_t coin_ballot(uint32_t k0, uint32_t k1, uint32_t tlo, uint32_t thi,
-                                             const uint32_t *__restrict__ live_ids, uint32_t group,
-                                             uint32_t round, uint64_t tie) {
+                                             uint32_t group, uint32_t round, uint64_t tie) {
   const uint32_t lane = threadIdx.x & 63u;
   asm volatile("" : "+s"(k0), "+s"(k1));
   bool c1 = false;
   if ((tie >> lane) & 1ull) {
-    const uint32_t node = live_ids[group * 64u + lane];
-    const uint4 rr = philox4x32_10(k0, k1, make_uint4(tlo, thi, node, (round & 0x00FFFFFFu) | (kStreamCoin << 24)));
-    c1 = !(rr.x > 0x80000000u);                 // Math.random() > 0.5 ? 0 : 1
+    // v_mul_lo/hi Philox here: with v_mad_u64_u32's VCC carry-outs the W = 31..32
+    // instantiations fail to allocate ("illegal VGPR to SGPR copy")
+    const uint4 b = coin_block<false>(k0, k1, tlo, thi, group * 64u + lane, round);
+    c1 = (coin_word(b, round) >> (lane & 31u)) & 1u;
   }
   return ballot(c1) & tie;
 }
@@ -136,13 +152,12 @@ __device__ __forceinline__ uint2 lds_keys(const uint32_t *keys) {
 }
 
 __device__ __forceinline__ uint64_t coin_ballot(const uint32_t *keys, uint32_t tlo, uint32_t thi,
-                                             const uint32_t *__restrict__ live_ids, uint32_t group,
-                                             uint32_t round, uint64_t tie) {
+                                             uint32_t group, uint32_t round, uint64_t tie) {
   const uint2 k = lds_keys(keys);
   tlo = (uint32_t)__builtin_amdgcn_readfirstlane((int)tlo);   // wave-uniform trial id; the asm keeps
   thi = (uint32_t)__builtin_amdgcn_readfirstlane((int)thi);   // Philox's first product on this path
   asm volatile("" : "+s"(tlo), "+s"(thi));
-  return coin_ballot(k.x, k.y, tlo, thi, live_ids, group, round, tie);
+  return coin_ballot(k.x, k.y, tlo, thi, group, round, tie);
 }
 
 // ------------------------------------------- W-specialised kernel (m <= 1024)

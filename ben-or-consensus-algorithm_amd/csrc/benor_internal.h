@@ -20,7 +20,7 @@ constexpr uint32_t kStreamCrash = 4u;
 constexpr int kWavesPerBlock = 4;          // 256-thread workgroups, one trial per wave
 constexpr uint32_t kMaxW = BO_MAX_N / 64;  // u64 words per bit plane at N = 4096
 constexpr int kMaxWSpecialised = 32;       // m <= 2048: fully unrolled W-specialised kernel
-constexpr uint32_t kMaxPackedM = 32;       // m <= 32: packed kernel, floor(32/m) trials per half-wave
+constexpr uint32_t kMaxLaneM = 64;         // m <= 64: lane kernel, one trial per lane (benor_lane.h)
 constexpr uint64_t kMaxTrialsPerLaunch = 1ull << 31;   // trial offsets within a launch fit 32 bits
 constexpr uint32_t kParamBytes = 32;       // LDS parameter block after the histogram (W kernel)
 
@@ -28,9 +28,9 @@ struct KParams {
   uint32_t N, F;            // network size, fault parameter
   uint32_t m;               // live (non-crashed) nodes = senders = receivers
   uint32_t W;               // u64 words per plane = ceil(m / 64) = receiver groups
-  uint32_t G;               // receiver groups per tally block (template parameter)
+  uint32_t G;               // receiver groups per tally block (template parameter); lane kernel: its KIND
   uint32_t nblocks;         // ceil(W / G)
-  uint32_t variant;         // 5: packed lockstep (m <= 32), 1: W-specialised lockstep (W <= kMaxWSpecialised = 32),
+  uint32_t variant;         // 6: lane lockstep (m <= 64), 1: W-specialised lockstep (W <= kMaxWSpecialised = 32),
                             // 0: blocked lockstep, 2: random delivery, 4: event level
   uint32_t mode;            // BO_MODE_LOCKSTEP / BO_MODE_RANDOM_DELIVERY
   uint32_t q;               // quorum N - F (messages each receiver tallies per phase)
@@ -70,6 +70,9 @@ template <int W>
 hipError_t launch_w(const KParams &p, int grid_blocks, hipStream_t stream);
 template <int G>
 hipError_t launch_b(const KParams &p, int grid_blocks, hipStream_t stream);
+// Lane kernel (benor_lane.h), m = 1..kMaxLaneM, instantiated in benor_lane_*.hip.
+template <int MM>
+hipError_t launch_lane_m(const KParams &p, int grid_blocks, hipStream_t stream);
 
 // Grid size that fills the current device for this configuration.
 int lockstep_grid(const KParams &p, int device);

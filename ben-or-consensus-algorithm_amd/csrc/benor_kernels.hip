@@ -29,190 +29,13 @@
 // distinct constant (subtracted afterwards) so that every live node's count is
 // executed by its own lane, as the reference executes it in its own handler.
 //
-// This file: the packed (m <= 32), random-delivery and event-level kernels,
-// the popcount probe, and the host-side planning / dispatch.  The lockstep
-// W kernel lives in benor_w_kernel.h (instantiated by benor_w_*.hip) and the
-// blocked kernel in benor_blocked.hip.
+// This file: the random-delivery and event-level kernels, the popcount probe,
+// and the host-side planning / dispatch.  The lockstep kernels live in
+// benor_lane.h (m <= 64, one trial per lane), benor_w_kernel.h (W kernel,
+// instantiated by benor_w_*.hip) and benor_blocked.hip (m > 2048).
 #include "benor_device.h"
 
 namespace benor {
-
-// ------------------------------------------------ packed kernel (m <= 32)
-// Small networks (BASELINE configs C1 N=5, C2 N=10, and the C5 sweep's small
-// cells) would leave most of a wave idle with one trial per wave.  Here every
-// 32-lane half of a wave holds P = floor(32/m) independent trials
-// ("segments") of m lanes each, so one wave runs 2P trials concurrently:
-//
-//   * lane (h*32 + i*m + c) is live node c (compact order) of segment h*P + i;
-//   * a phase's messages for all segments are ONE pair of wave ballots
-//     {is0, is1}; each receiver tallies its own segment's bits:
-//     popcount((ballot >> 32h) & segment_mask) per count;
-//   * segments advance independently: when a segment's trial halts (every
-//     live node decided, or k_max rounds), its leader lane records the
-//     outcome and the segment pulls the wave's next trial from a per-wave
-//     queue.  Random initial values for the queue come from an LDS ring of
-//     128 words filled 64 trials per Philox pass (one trial per lane);
-//   * coins (node.ts:111) are per lane, only on rounds where some receiver ties.
-// Same outcome definition as the other lockstep kernels: the histogram is
-// bit-identical to theirs (the trial -> wave assignment only changes order).
-__device__ __forceinline__ uint32_t seg_tally(uint64_t plane, uint32_t half_shift, uint32_t segmask) {
-  // one receiver's count over its segment's senders (node.ts:56-62, :92-98)
-  return (uint32_t)__builtin_popcount((uint32_t)(plane >> half_shift) & segmask);
-}
-
-// Per-lane flag from a wave mask (one v_cndmask).  The mask must come from a
-// SALU op (not straight from a v_cmp): no VALU-write -> VALU-read hazard.
-__device__ __forceinline__ bool lane_in(uint64_t mask) { return select_lanes(0u, 1u, mask) != 0u; }
-
-// Segment state lives in wave masks (SGPR pairs) -- active, needs a trial,
-// decided, x = 1, x = 0 -- updated by SALU ops, so a phase's ballots are plain
-// v_cmp results combined with `act` in SALU (per-lane booleans would be
-// materialised as v_cndmask + v_cmp pairs around every ballot).  Per lane
-// only the round counter and the trial id remain in VGPRs.
-__global__ void __launch_bounds__(256) benor_packed_kernel(KParams p) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wv = threadIdx.x >> 6;
-  const uint32_t m = p.m, F = p.F, k_max = p.k_max;
-  const uint32_t P = 32u / m;                       // segments per half
-  uint32_t *lhist = reinterpret_cast<uint32_t *>(smem);
-  uint32_t *ring = reinterpret_cast<uint32_t *>(smem + p.hist_bytes + wv * p.wave_bytes);   // [128]
-
-  for (uint32_t i = threadIdx.x; i < p.hist_len; i += blockDim.x) lhist[i] = 0u;
-  __syncthreads();
-
-  const uint32_t hl = lane & 31u;
-  const uint32_t si = hl / m;                       // segment index within the half
-  const uint32_t c = hl - si * m;                   // compact live index of this lane's node
-  const bool valid = si < P;
-  const uint32_t half_shift = lane & 32u;
-  const uint32_t mbits = m == 32u ? ~0u : ((1u << m) - 1u);
-  const uint32_t segmask = valid ? (mbits << (si * m)) : 0u;
-  const uint32_t node = valid ? p.live_ids[c] : 0u;
-  const uint32_t not_leader = c ? 1u : 0u;
-  const bool random_init = p.init_mode == BO_INIT_RANDOM;
-  const uint32_t M1 = m - p.init_q;                 // binary-valued senders in round 1
-  // fixed init (BO_INIT_FIXED): word 0 of the plane holds every live node (m <= 32)
-  const uint4 fixed = random_init ? make_uint4(0, 0, 0, 0) : p.init_plane[0];
-  const uint64_t validm = ballot(valid);
-  const uint64_t leaderm = ballot(valid && c == 0u) & validm;
-  const uint64_t fx1m = ballot(valid && ((fixed.z >> c) & 1u)) & validm;
-  const uint64_t fx0m = ballot(valid && ((fixed.x >> c) & 1u)) & validm;
-
-  const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
-  const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
-  const uint64_t waves_total = (uint64_t)gridDim.x * kWavesPerBlock;
-
-  uint64_t next_j = 0, filled = 0;                  // wave queue: j-th trial of the wave = gw + j * waves_total
-  uint64_t needm = validm, actm = 0, decm = 0, x1m = 0, x0m = 0;
-  uint32_t r = 0u;
-  uint32_t tlo = 0u, thi = 0u;
-
-  for (;;) {
-    // ---- pull: segments that need a trial take the next queue entries (node.ts:167-188 /start)
-    const uint64_t Lb = needm & leaderm;
-    uint64_t firstm = 0;                            // segments in their first round
-    if (Lb) {
-      const uint32_t nf = (uint32_t)__builtin_popcountll(Lb);
-      if (random_init && next_j + nf > filled) {   // refill 64 ring slots, one trial per lane
-        const uint64_t j = filled + lane;
-        const uint64_t t = gw + j * waves_total;
-        if (t < p.trial_count) {
-          const uint64_t tr = p.trial_begin + t;
-          uint32_t kk0 = k0, kk1 = k1;
-          asm volatile("" : "+s"(kk0), "+s"(kk1));
-          ring[j & 127u] = philox4x32_10(kk0, kk1, make_uint4((uint32_t)tr, (uint32_t)(tr >> 32), 0u, kStreamInit << 24)).x;
-        }
-        filled += 64u;
-      }
-      // every lane computes its segment's queue entry; only needing lanes keep it
-      const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(Lb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)Lb, 0u));
-      const uint64_t j = next_j + below - not_leader;
-      const uint64_t t = gw + j * waves_total;
-      const uint64_t okm = ballot(t < p.trial_count) & needm;
-      const uint64_t tr = p.trial_begin + t;
-      tlo = select_lanes(tlo, (uint32_t)tr, needm);
-      thi = select_lanes(thi, (uint32_t)(tr >> 32), needm);
-      r = select_lanes(r, 0u, needm);
-      uint64_t n1 = fx1m, n0 = fx0m;
-      if (random_init) {
-        n1 = ballot((ring[(uint32_t)j & 127u] >> c) & 1u) & validm;
-        n0 = validm & ~n1;
-      }
-      x1m = (x1m & ~needm) | (n1 & okm);
-      x0m = (x0m & ~needm) | (n0 & okm);
-      decm &= ~needm;
-      actm = (actm & ~needm) | okm;
-      firstm = okm;
-      needm = 0;
-      next_j += nf;
-    }
-    if (!actm) break;
-
-    // ---- R-phase ("proposal phase", node.ts:46-82): c1 per receiver, c0 = M - c1
-    //      (M = m binary-valued senders; minus the "?" ones in round 1 of a fixed init)
-    const uint32_t c1 = seg_tally(x1m & actm, half_shift, segmask);
-    const uint32_t c0 = (p.init_q ? select_lanes(m, M1, firstm) : m) - c1;
-    // ---- P-phase ("voting phase", node.ts:83-158)
-    const uint64_t p0 = ballot(c0 > c1) & actm, p1 = ballot(c1 > c0) & actm;       // node.ts:63-69 (else "?")
-    const uint32_t v0 = seg_tally(p0, half_shift, segmask), v1 = seg_tally(p1, half_shift, segmask);
-    ++r;
-    const uint64_t d0 = ballot(v0 > F) & actm;                                       // node.ts:99
-    const uint64_t d1 = ballot(v1 > F) & actm & ~d0;                                 // node.ts:102
-    const uint64_t und = actm & ~(d0 | d1);
-    uint64_t nx1 = d1;
-    if (und) {
-      nx1 |= ballot(v1 > v0) & und;                                                 // node.ts:106-109
-      const uint64_t tie = ballot(v0 == v1) & und;                                  // node.ts:110-111
-      if (tie) {
-        uint32_t kk0 = k0, kk1 = k1;
-        asm volatile("" : "+s"(kk0), "+s"(kk1));
-        bool coin1 = false;
-        if (lane_in(tie)) {
-          const uint4 rr = philox4x32_10(kk0, kk1, make_uint4(tlo, thi, node, (r & 0x00FFFFFFu) | (kStreamCoin << 24)));
-          coin1 = !(rr.x > 0x80000000u);                                            // Math.random() > 0.5 ? 0 : 1
-        }
-        nx1 |= ballot(coin1) & tie;
-      }
-    }
-    x1m = (x1m & ~actm) | nx1;
-    x0m = (x0m & ~actm) | (actm & ~nx1);
-    decm |= d0 | d1;                                                                // sticky (node.ts:100-105)
-    // ---- halt: every live node of the segment decided (auto-stop, node.ts:116-145) or k_max
-    const uint64_t done = ballot(seg_tally(decm & actm, half_shift, segmask) == m) & actm;
-    const uint64_t fin = (done | ballot(r >= k_max)) & actm;
-    if (fin) {
-      const bool any0 = seg_tally(x0m & fin, half_shift, segmask) != 0u;
-      const bool any1 = seg_tally(x1m & fin, half_shift, segmask) != 0u;
-      const uint64_t lead = fin & leaderm;
-      if (lane_in(lead)) {
-        const bool seg_done = lane_in(done & lead);
-        const uint32_t v = (any0 && any1) ? 2u : (any1 ? 1u : 0u);
-        atomicAdd(&lhist[seg_done ? (r * 3u + v) : v], 1u);
-        if (seg_done && v == 2u) atomicAdd(&lhist[p.hist_len - 1u], 1u);
-        if (p.rounds_out) *p.rounds_out = seg_done ? r : 0u;
-      }
-      if (p.node_out && lane_in(fin)) {                                             // GET /getState (node.ts:197-199)
-        bo_node_state ns;
-        ns.killed = 0;
-        ns.x = (int8_t)(lane_in(x1m & fin) ? 1 : (lane_in(x0m & fin) ? 0 : 2));
-        ns.decided = (int8_t)(lane_in(decm & fin) ? 1 : 0);
-        ns.pad = 0;
-        ns.k = (int32_t)r + 1;                                                      // node.ts:147
-        p.node_out[node] = ns;
-      }
-      actm &= ~fin;
-      needm |= fin;
-    }
-  }
-
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < p.hist_len; i += blockDim.x) {
-    const uint32_t cnt = lhist[i];
-    if (cnt) atomicAdd(&p.hist[i], (unsigned long long)cnt);
-  }
-}
-
 
 // ----------------------------------------- random-delivery kernel (f <= F)
 // Generalised delivery: with f <= F crashed nodes every live
@@ -417,7 +240,7 @@ __global__ void __launch_bounds__(256) benor_random_kernel(KParams p) {
         if (rest) {
           x1 |= ballot(a1 > a0) & rest;
           const uint64_t tie = ballot(a1 == a0) & rest;
-          if (tie) x1 |= coin_ballot(k0, k1, tlo, thi, p.live_ids, j, r, tie);
+          if (tie) x1 |= coin_ballot(k0, k1, tlo, thi, j, r, tie);
         }
         if (lane == 0) X[j] = rec(vm & ~x1, x1);
         if (d0l || d1l) dec |= 1ull << j;
@@ -621,8 +444,9 @@ __global__ void __launch_bounds__(256) benor_event_kernel(KParams p) {
         else if (c0 + c1 > 0 && c0 > c1) nx = 0;
         else if (c0 + c1 > 0 && c0 < c1) nx = 1;
         else {
-          const uint4 rr = philox4x32_10<false>(k0, k1, make_uint4(tlo, thi, to, (k & 0x00FFFFFFu) | (kStreamCoin << 24)));
-          nx = (rr.x > 0x80000000u) ? 0 : 1;           // node.ts:111
+          const uint32_t c = (uint32_t)__builtin_popcountll(~p.faulty_mask & ((1ull << to) - 1ull));   // compact index
+          const uint4 rr = philox4x32_10<false>(k0, k1, make_uint4(tlo, thi, c >> 5, ((k - 1u) >> 2) | (kStreamCoin << 24)));
+          nx = (int8_t)((coin_word(rr, k) >> (c & 31u)) & 1u);   // node.ts:111
         }
         L.xs[to] = nx;
         L.ks[to] = (int16_t)(k + 1u);
@@ -722,11 +546,13 @@ void plan_geometry(KParams &p) {
     p.lds_bytes = p.hist_bytes + kWavesPerBlock * p.wave_bytes;
     return;
   }
-  if (p.m <= kMaxPackedM) {                         // packed: floor(32/m) trials per half-wave
-    p.G = 1;
+  if (p.m <= kMaxLaneM) {                           // lane kernel: one trial per lane
+    const uint32_t M1 = p.m - p.init_q;
+    const bool odd = (p.m & 1u) && (M1 & 1u);        // every vote count odd: no tie, no coin
+    p.G = odd ? (p.m > 2u * p.F ? 2u : 1u) : 0u;     // KIND (benor_lane.hip)
     p.nblocks = 1;
-    p.variant = 5;
-    p.wave_bytes = 128u * 4u;                       // init-word ring
+    p.variant = 6;
+    p.wave_bytes = 128u * 8u + 128u * 16u;          // init-word ring, coin-block ring
     p.lds_bytes = p.hist_bytes + kWavesPerBlock * p.wave_bytes;
     return;
   }
@@ -765,7 +591,14 @@ void plan_geometry(KParams &p) {
 template <int... Is>
 static hipError_t dispatch_w(const KParams &p, int grid, hipStream_t s, std::integer_sequence<int, Is...>) {
   hipError_t e = hipErrorInvalidValue;
-  (void)((p.W == (uint32_t)(Is + 1) ? (e = launch_w<Is + 1>(p, grid, s), true) : false) || ...);
+  (void)((p.W == (uint32_t)(Is + 2) ? (e = launch_w<Is + 2>(p, grid, s), true) : false) || ...);
+  return e;
+}
+
+template <int... Is>
+static hipError_t dispatch_lane(const KParams &p, int grid, hipStream_t s, std::integer_sequence<int, Is...>) {
+  hipError_t e = hipErrorInvalidValue;
+  (void)((p.m == (uint32_t)(Is + 1) ? (e = launch_lane_m<Is + 1>(p, grid, s), true) : false) || ...);
   return e;
 }
 
@@ -782,10 +615,7 @@ hipError_t launch_lockstep(const KParams &p, int grid, hipStream_t s) {
     hipLaunchKernelGGL(benor_event_kernel, dim3(grid), dim3(256), p.lds_bytes, s, p);
     return hipGetLastError();
   }
-  if (p.variant == 5) {
-    hipLaunchKernelGGL(benor_packed_kernel, dim3(grid), dim3(64 * kWavesPerBlock), p.lds_bytes, s, p);
-    return hipGetLastError();
-  }
+  if (p.variant == 6) return dispatch_lane(p, grid, s, std::make_integer_sequence<int, (int)kMaxLaneM>{});
   if (p.variant == 2) {
     if (p.lds_bytes > 64u * 1024u) {
       hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&benor_random_kernel),
@@ -795,7 +625,7 @@ hipError_t launch_lockstep(const KParams &p, int grid, hipStream_t s) {
     hipLaunchKernelGGL(benor_random_kernel, dim3(grid), dim3(64 * kWavesPerBlock), p.lds_bytes, s, p);
     return hipGetLastError();
   }
-  if (p.variant == 1) return dispatch_w(p, grid, s, std::make_integer_sequence<int, kMaxWSpecialised>{});
+  if (p.variant == 1) return dispatch_w(p, grid, s, std::make_integer_sequence<int, kMaxWSpecialised - 1>{});   // W = 2..32
   return dispatch_b(p, grid, s, std::make_integer_sequence<int, 12>{});
 }
 
@@ -809,7 +639,7 @@ int lockstep_grid(const KParams &p, int device) {
     return (int)(grid < 1 ? 1 : grid);
   }
   // 8 workgroups (32 waves) per CU when registers and LDS allow it.
-  const uint64_t per_wave = p.variant == 5 ? 2u * (32u / p.m) : 1u;   // trials a wave runs at once
+  const uint64_t per_wave = p.variant == 6 ? 64u : 1u;   // trials a wave runs at once
   const uint64_t waves_needed = (p.trial_count + per_wave - 1u) / per_wave;
   const uint64_t blocks_needed = (waves_needed + kWavesPerBlock - 1) / kWavesPerBlock;
   uint64_t per_cu = 8;

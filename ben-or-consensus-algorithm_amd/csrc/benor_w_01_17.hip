@@ -1,9 +1,9 @@
-// W kernel instantiations W = 1..17 (see benor_w_kernel.h); split so the
+// W kernel instantiations W = 2..17 (see benor_w_kernel.h; m <= 64, W = 1, runs in
+// the lane kernel, benor_lane.h); split so the
 // unrolled instantiations (compile time ~ W^2) build in parallel.
 #include "benor_w_kernel.h"
 
 namespace benor {
-template hipError_t launch_w<1>(const KParams &, int, hipStream_t);
 template hipError_t launch_w<2>(const KParams &, int, hipStream_t);
 template hipError_t launch_w<3>(const KParams &, int, hipStream_t);
 template hipError_t launch_w<4>(const KParams &, int, hipStream_t);

@@ -19,7 +19,7 @@ constexpr int kPairMaxW = 8;               // W kernel: pair trials' round 1 up 
 // (profiles/r01-v19_ab_interleave_k.jsonl): odd W=1 +27 %, W=2 +10 %, W=3 +7 %,
 // W=4 +2 %; even W=1 +8 %, W=2 +4 %, W=3 +2 %, W=4 +1.5 %; larger K spills.
 constexpr int interleave_k(int W, bool odd_only) {
-  if (odd_only) return W <= 1 ? 16 : (W <= 4 ? 8 : (W <= 6 ? 3 : (W <= 16 ? 2 : 1)));
+  if (odd_only) return W <= 4 ? 8 : (W <= 6 ? 3 : (W <= 16 ? 2 : 1));   // W >= 2 (m > 64)
   return W <= 2 ? 8 : (W <= 4 ? 4 : (W <= 6 ? 3 : (W <= kPairMaxW ? 2 : 1)));
 }
 
@@ -77,7 +77,7 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // uniform: scalar trial loop
   // Only the round loop's own scalars are kept in registers.  What a rare
-  // path needs (Philox key, trial id base, live ids) sits in a small LDS
+  // path needs (Philox key, trial id base) sits in a small LDS
   // parameter block and is re-read where it is used, so the register
   // allocator never holds -- and spills -- a kernarg tuple across the
   // trial loop.
@@ -90,7 +90,7 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
   uint2 *ring = reinterpret_cast<uint2 *>(smem + p.hist_bytes + wv * p.wave_bytes);   // [TB][WP] x1 words
   uint2 *X = ring + TB * WP;       // [WP] final x1 plane (GET /getState only)
   uint2 *D = X + WP;               // [WP] sticky decided bits, kept only while some receiver is undecided
-  // parameter block: [0,1] Philox key (seed), [2,3] trial_begin, [4,5] live_ids
+  // parameter block: [0,1] Philox key (seed), [2,3] trial_begin
   uint32_t *keys = reinterpret_cast<uint32_t *>(smem + p.hist_bytes - kParamBytes);
 
   for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) lhist[i] = 0u;
@@ -99,8 +99,6 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
     keys[1] = (uint32_t)(p.seed >> 32);
     keys[2] = (uint32_t)p.trial_begin;
     keys[3] = (uint32_t)(p.trial_begin >> 32);
-    keys[4] = (uint32_t)(uintptr_t)p.live_ids;
-    keys[5] = (uint32_t)((uintptr_t)p.live_ids >> 32);
   }
   if (p.init_mode != BO_INIT_RANDOM && lane < (uint32_t)W) {
     const uint4 q = p.init_plane[lane];
@@ -204,8 +202,7 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
             x1 |= ad1;
             if (tie) {                                                  // node.ts:111
               const uint64_t trial = lds_u64(keys + 2) + t;
-              const uint32_t *ids = reinterpret_cast<const uint32_t *>((uintptr_t)lds_u64(keys + 4));
-              x1 |= coin_ballot(keys, (uint32_t)trial, (uint32_t)(trial >> 32), ids, g, r, tie);
+              x1 |= coin_ballot(keys, (uint32_t)trial, (uint32_t)(trial >> 32), g, r, tie);
             }
           }
           uint64_t dg = d0 | d1;

@@ -223,9 +223,10 @@ def main():
         sys.exit(2)
     if args.dry_run:
         rank = int(os.environ.get("RANK", "0"))
-        print(json.dumps({"dry_run": True, "world": world, "rank": rank, "scaling": args.scaling,
-                          "shards": [rank_range(args.scaling, args.warmup + i, rank, world, args.trials)
-                                     for i in range(args.steps)]}), flush=True)
+        line = json.dumps({"dry_run": True, "world": world, "rank": rank, "scaling": args.scaling,
+                           "shards": [rank_range(args.scaling, args.warmup + i, rank, world, args.trials)
+                                      for i in range(args.steps)]})
+        os.write(1, (line + "\n").encode())          # one write: ranks share the pipe
         return
 
     import numpy as np

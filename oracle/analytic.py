@@ -10,9 +10,8 @@ x-multiset is not tied makes every node propose the majority v
 that round iff m > F (node.ts:99-105), else adopts v (node.ts:106-109) and x
 freezes.  A tied round (m even, c0 == c1) makes every node propose "?"; the
 P-phase then sees c0 == c1 == 0 and every node flips its own coin
-(node.ts:111).  The coin is 1 iff w <= 0x80000000 for a uniform 32-bit w, so
-P(coin = 1) = 1/2 + 2^-32 exactly (the reference's Math.random() gives
-1/2 + 2^-53; both differ from 1/2 far below any test's resolution).
+(node.ts:111).  The coin is one uniform Philox bit, so P(coin = 1) = 1/2
+exactly (the reference's Math.random() > 0.5 ? 0 : 1 gives 1/2 + 2^-53).
 """
 from __future__ import annotations
 
@@ -20,7 +19,7 @@ from math import comb
 
 import numpy as np
 
-P_COIN1 = 0.5 + 2.0 ** -32
+P_COIN1 = 0.5
 
 
 def tie_prob(m: int, p: float = 0.5) -> float:
@@ -80,6 +79,31 @@ def expected_rounds(N: int, F: int) -> float:
     m = N - F
     q = tie_prob(m)
     return 1.0 / (1.0 - q)
+
+
+def rounds_cdf(probs: np.ndarray, k_max: int) -> np.ndarray:
+    """CDF of the rounds-to-decision R over 1..k_max+1 from bin probabilities
+    (R = k_max + 1 stands for "not decided within k_max rounds")."""
+    pr = np.asarray(probs, dtype=np.float64)[: (k_max + 1) * 3].reshape(k_max + 1, 3).sum(axis=1)
+    pmf = np.concatenate([pr[1:], pr[:1]])             # R = 1..k_max, then undecided
+    return np.cumsum(pmf)
+
+
+def ks_rounds_pvalue(counts: np.ndarray, probs: np.ndarray, k_max: int) -> float:
+    """Kolmogorov-Smirnov test of the rounds-to-decision distribution (the
+    histogram summed over decided values) against the exact law.
+
+    R is discrete, so the statistic D = max |F_n(r) - F(r)| is taken over the
+    support points and its p-value from the Kolmogorov distribution of n
+    samples (scipy.stats.kstwo) is conservative: P(D >= d) is never larger
+    under H0 than for a continuous law."""
+    from scipy import stats
+
+    c = np.asarray(counts, dtype=np.float64)[: (k_max + 1) * 3].reshape(k_max + 1, 3).sum(axis=1)
+    n = c.sum()
+    emp = np.cumsum(np.concatenate([c[1:], c[:1]])) / n
+    d = float(np.max(np.abs(emp - rounds_cdf(probs, k_max))))
+    return float(stats.kstwo.sf(d, int(n))) if d > 0 else 1.0
 
 
 def chi2_pvalue(counts: np.ndarray, probs: np.ndarray, min_expected: float = 5.0) -> float:

@@ -24,9 +24,11 @@
  *
  * Shared conventions (identical in the HIP kernel):
  *   Philox4x32-10, key = {seed_lo, seed_hi}.
- *   coin(trial, node, round) = ctr {trial_lo, trial_hi, node, round | 0<<24},
- *       word 0 = w; coin = (w > 0x80000000) ? 0 : 1, i.e. the reference's
- *       `Math.random() > 0.5 ? 0 : 1` (node.ts:111) with u = w * 2^-32.
+ *   coin of the c-th live node (ascending node id) in round r >= 1 =
+ *       bit (c & 31) of word (r-1) & 3 of philox(ctr {trial_lo, trial_hi,
+ *       c >> 5, ((r-1) >> 2) | 0<<24}): one block per 32 nodes and 4 rounds;
+ *       x = coin, the reference's `Math.random() > 0.5 ? 0 : 1` (node.ts:111)
+ *       with P(1) = 1/2.
  *   random initial value of the c-th live node (ascending node id):
  *       bit (c & 31) of word c>>5, word j = philox(ctr {trial_lo, trial_hi,
  *       j>>2, 1<<24})[j & 3].
@@ -79,10 +81,13 @@ static inline uint32_t orc_philox_word(uint64_t seed, uint64_t trial, uint32_t c
     return out[idx];
 }
 
-/* node.ts:111  `Math.random() > 0.5 ? 0 : 1` with u = w * 2^-32. */
-int oracle_coin(uint64_t seed, uint64_t trial, uint32_t node, uint32_t round) {
-    uint32_t w = orc_philox_word(seed, trial, node, (round & 0x00FFFFFFu) | (ORC_STREAM_COIN << 24), 0);
-    return (w > 0x80000000u) ? 0 : 1;
+/* node.ts:111  `Math.random() > 0.5 ? 0 : 1`: the coin of the c-th live node
+ * (compact index) in round r >= 1. */
+int oracle_coin(uint64_t seed, uint64_t trial, uint32_t c, uint32_t round) {
+    const uint32_t rr = round - 1u;
+    uint32_t w = orc_philox_word(seed, trial, c >> 5, ((rr >> 2) & 0x00FFFFFFu) | (ORC_STREAM_COIN << 24),
+                                 (int)(rr & 3u));
+    return (int)((w >> (c & 31u)) & 1u);
 }
 
 /* Random initial value (0/1) of the c-th live node. */
@@ -160,6 +165,8 @@ int oracle_message_sim(uint32_t N, uint32_t F, const int8_t *init, const uint8_t
         live += faulty[i] ? 0 : 1;
     }
     if (stalled) *stalled = 0;
+    uint32_t *cidx = (uint32_t *)malloc(sizeof(uint32_t) * (N + 1));   /* compact live index (coins) */
+    for (uint32_t i = 0, c = 0; i < N; ++i) { cidx[i] = c; c += faulty[i] ? 0 : 1; }
     const int64_t quorum = (int64_t)N - (int64_t)F;
     const uint32_t KR = k_max + 2;
     /* proposals / votes: Map<k, Value[]> per node (node.ts:29-30) */
@@ -231,7 +238,7 @@ int oracle_message_sim(uint32_t N, uint32_t F, const int8_t *init, const uint8_t
                 else {
                     if (c0 + c1 > 0 && c0 > c1) st[i].x = 0;
                     else if (c0 + c1 > 0 && c0 < c1) st[i].x = 1;
-                    else st[i].x = (int8_t)oracle_coin(seed, trial, i, (uint32_t)m.k);
+                    else st[i].x = (int8_t)oracle_coin(seed, trial, cidx[i], (uint32_t)m.k);
                 }
                 st[i].k = m.k + 1;                          /* node.ts:147 */
                 uint8_t *pd = &pdone[(size_t)i * KR + (uint32_t)m.k];
@@ -257,7 +264,7 @@ int oracle_message_sim(uint32_t N, uint32_t F, const int8_t *init, const uint8_t
 #undef BCAST
     if (!halted && stalled) *stalled = 1;
     for (size_t j = 0; j < (size_t)N * KR; ++j) { free(prop[j].v); free(vote[j].v); }
-    free(prop); free(vote); free(pdone); free(completed); free(pool);
+    free(prop); free(vote); free(pdone); free(completed); free(pool); free(cidx);
     if (halted == 2) return rounds;
     return -1;
 }
@@ -414,7 +421,7 @@ static void run_one(const orc_trials_cfg *cfg, const uint32_t *live_ids, uint32_
             else if (c1 > (int)F) { x = 1; dec[c >> 6] |= bit; }
             else if (c0 + c1 > 0 && c0 > c1) x = 0;
             else if (c0 + c1 > 0 && c0 < c1) x = 1;
-            else x = oracle_coin(cfg->seed, trial, live_ids[c], r);
+            else x = oracle_coin(cfg->seed, trial, c, r);
             if (x) nx1[c >> 6] |= bit; else nx0[c >> 6] |= bit;
         }
         for (uint32_t w = 0; w < W; ++w) { x0[w] = nx0[w]; x1[w] = nx1[w]; }
@@ -547,12 +554,13 @@ static uint32_t event_trial(const orc_event_cfg *cfg, uint64_t trial, orc_node_s
     const int64_t quorum = (int64_t)N - (int64_t)F;
     const size_t H = (size_t)(cfg->k_max + 1) * 3;
     orc_node_state st[64];
-    uint32_t live_ids[64], m = 0;
+    uint32_t live_ids[64], cidx[64], m = 0;
     uint64_t killed = 0, decided = 0, all = (N == 64) ? ~0ull : ((1ull << N) - 1);
     for (uint32_t i = 0; i < N; ++i) {
         const int f = cfg->faulty[i] != 0;
         st[i].killed = (int8_t)f; st[i].decided = f ? -1 : 0; st[i].k = f ? -1 : 0; st[i].pad = 0;
         st[i].x = -1;
+        cidx[i] = m;
         if (f) killed |= 1ull << i; else live_ids[m++] = i;
     }
     for (uint32_t c = 0; c < m; ++c) {
@@ -636,7 +644,7 @@ static uint32_t event_trial(const orc_event_cfg *cfg, uint64_t trial, orc_node_s
             else if (c1 > (int)F) { st[to].x = 1; st[to].decided = 1; decided |= 1ull << to; }
             else if (c0 + c1 > 0 && c0 > c1) st[to].x = 0;
             else if (c0 + c1 > 0 && c0 < c1) st[to].x = 1;
-            else st[to].x = (int8_t)oracle_coin(cfg->seed, trial, to, k);
+            else st[to].x = (int8_t)oracle_coin(cfg->seed, trial, cidx[to], k);
             st[to].k = (int32_t)k + 1;
             uint8_t *pd = &pdone[(size_t)to * KR + k];
             if (!*pd) {

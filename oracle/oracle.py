@@ -79,8 +79,9 @@ def philox4x32_10(key, ctr):
     return list(o)
 
 
-def coin(seed: int, trial: int, node: int, rnd: int) -> int:
-    return lib().oracle_coin(seed, trial, node, rnd)
+def coin(seed: int, trial: int, c: int, rnd: int) -> int:
+    """Coin of the c-th live node (compact index) in round rnd >= 1."""
+    return lib().oracle_coin(seed, trial, c, rnd)
 
 
 def random_init(seed: int, trial: int, c: int) -> int:

@@ -195,7 +195,7 @@ def test_full_size_sharding_invariance_and_law():
     assert whole.sum() == T
     assert whole[3] + whole[4] == T            # bins (R=1, v=0), (R=1, v=1)
     assert whole[-1] == 0
-    assert analytic.chi2_pvalue(whole[:-1], analytic.hist_probs(N, F, k)) > 1e-3
+    assert analytic.chi2_pvalue(whole[:-1], analytic.hist_probs(N, F, k)) > 0.01
     # a spot-check of the same launch range against the oracle
     ref = oracle.run_trials(N, F, first_f(N, F), seed=0x243F6A8885A308D3, trial_begin=1_999_000,
                             trial_count=1000, k_max=k)
@@ -212,18 +212,32 @@ def test_launch_split_past_2_31_trials():
     T = (1 << 31) + 3000
     h = plan.run(5, T)
     assert h.sum() == T and h[3] + h[4] == T
-    assert analytic.chi2_pvalue(h[:-1], analytic.hist_probs(N, F, k)) > 1e-3
+    assert analytic.chi2_pvalue(h[:-1], analytic.hist_probs(N, F, k)) > 0.01
     tail = plan.run(5 + (1 << 31), 3000)
     ref = oracle.run_trials(N, F, first_f(N, F), seed=77, trial_begin=5 + (1 << 31), trial_count=3000, k_max=k)
     np.testing.assert_array_equal(tail, ref.hist)
 
 
-@pytest.mark.parametrize("N,F,k_max", [(10, 4, 24), (10, 5, 11), (64, 0, 32), (100, 30, 32)])
+# north_star: in random mode the rounds-to-decide and decided-value
+# distributions pass KS / chi-square at p > 0.01 against the reference network's
+# law, including the F > N/2 no-decision case
+# (benorconsensus.test.ts:292-345).  10^6 trials each (BASELINE configs[1]).
+P_MIN = 0.01
+
+
+@pytest.mark.parametrize("N,F,k_max", [(5, 1, 24), (10, 4, 24), (10, 5, 11), (64, 0, 32), (100, 30, 32),
+                                       (12, 6, 16), (256, 86, 16)])
 def test_analytic_law_1e6(N, F, k_max):
     plan = benor.TrialsPlan(N, F, first_f(N, F), seed=0xA11CE + N, k_max=k_max)
     h = plan.run(0, 1_000_000)
     assert h.sum() == 1_000_000 and h[-1] == 0
-    assert analytic.chi2_pvalue(h[:-1], analytic.hist_probs(N, F, k_max)) > 1e-3
+    probs = analytic.hist_probs(N, F, k_max)
+    assert analytic.chi2_pvalue(h[:-1], probs) > P_MIN            # joint (rounds, decided value)
+    assert analytic.ks_rounds_pvalue(h[:-1], probs, k_max) > P_MIN  # rounds-to-decision CDF
+    decided = h[3:-1].reshape(-1, 3).sum(axis=0)                   # decided-value marginal
+    if decided[:2].sum():
+        pv = analytic.chi2_pvalue(decided[:2], np.array([0.5, 0.5]))
+        assert pv > P_MIN and decided[2] == 0
 
 
 def test_no_decision_case_f_gt_half():

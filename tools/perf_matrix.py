@@ -25,7 +25,8 @@ SHAPES = [
     (256, 85, 85, 0, 10_000_000), (512, 170, 170, 0, 10_000_000), (1024, 341, 341, 0, 20_000_000),
     (1024, 0, 0, 0, 4_000_000), (1536, 512, 512, 0, 2_000_000), (2048, 682, 682, 0, 1_000_000),
     (4096, 1365, 1365, 0, 400_000), (4096, 0, 0, 0, 100_000),
-    (10, 4, 2, 1, 2_000_000), (100, 30, 10, 1, 200_000), (1024, 341, 300, 1, 20_000), (1024, 341, 0, 1, 2_000),
+    # random delivery at full occupancy (>= 8192 resident waves: one trial per wave)
+    (10, 4, 2, 1, 2_000_000), (100, 30, 10, 1, 200_000), (1024, 341, 300, 1, 200_000), (1024, 341, 0, 1, 100_000),
     (10, 4, 4, 2, 2_000_000), (32, 10, 10, 2, 200_000), (64, 21, 21, 2, 100_000),
 ]
 
