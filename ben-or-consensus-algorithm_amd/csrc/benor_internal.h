@@ -55,6 +55,9 @@ struct KParams {
   const uint32_t *crash_at;        // [N] (device) or nullptr
   uint32_t crash_count, crash_window;
   uint32_t ev_cap, ev_stride;      // per-lane pool capacity and scratch stride (u32 words)
+  // random delivery (variant 2): Bernoulli + fix-up sampler with p = rd_a / 16 and
+  // rd_b-bit index fields; rd_a = 0 selects Floyd (oracle_delivery_bernoulli)
+  uint32_t rd_a, rd_b;
   uint64_t ev_lanes;               // lanes the scratch buffer holds
   uint32_t *scratch;               // [ev_lanes][ev_stride]
 };

@@ -93,14 +93,111 @@ __device__ __forceinline__ void floyd_insert(uint32_t lbase, uint32_t t, uint32_
   __hip_atomic_fetch_or(bitset_word(idx, lbase), 1u << (idx & 31u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 
+// Sampler (b) of oracle_delivery_mask: Bernoulli(a/16) mask, then exact
+// fix-up flips at uniform sender indices until the mask holds q senders.  The
+// mask words and the fix-up fields are taken in stream order; every lane runs
+// the same (wave-uniform) stream schedule, so Philox blocks are drawn once per
+// 4 words for the whole wave.  Writes the lane's mask into B ([word][lane]).
+//
+// The fix-up definition is sequential (each field sees the flips before it),
+// but a field's test depends on an earlier field only when both name the same
+// sender: the repeat then sees the bit already flipped (or still unwanted) and
+// is refused either way.  So fields go 4 at a time: the 4 mask words are read
+// back to back (one LDS round trip instead of 4), each field is tested against
+// them and refused when an earlier field of the batch named the same sender,
+// and the flips go out as ds_xor (LDS ops of a wave apply in issue order; a
+// refused field xors 0).  PER = floor(32/b) fields per stream word (b = 7..12).
+template <int PER, bool POW2>
+__device__ __forceinline__ void bernoulli_fixup(uint32_t *__restrict__ B, uint32_t m, uint32_t b, uint32_t rm,
+                                                uint32_t need, uint32_t blk0, uint32_t k0, uint32_t k1,
+                                                uint32_t tlo, uint32_t thi, uint32_t c2, uint32_t c3) {
+  constexpr int NF = 4 * PER;                        // fields per Philox block
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t lb = (uint32_t)(uintptr_t)(lds_u32 *)B + lane * 4u;   // LDS address of this lane's word 0
+  for (uint32_t blk = blk0;; ++blk) {
+    if (!__any(need != 0u)) break;
+    const uint4 bb = philox4x32_10(k0, k1, make_uint4(tlo, thi, c2 | (blk << 12), c3));
+    const uint32_t u4[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+    for (int g = 0; g < NF; g += 4) {
+      uint32_t fb[4], cur[4];
+      lds_u32 *wp[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int f = g + j;                         // field f: word f / PER, bits (f % PER) * b
+        fb[j] = __builtin_amdgcn_ubfe(u4[f / PER], (uint32_t)(f % PER) * b, b);
+        // an index >= m (never when m = 2^b) reads word 0 and is refused below
+        wp[j] = bitset_word(POW2 ? fb[j] : (fb[j] < m ? fb[j] : 0u), lb);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) cur[j] = *wp[j];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bool ok = need != 0u && (POW2 || fb[j] < m) && __builtin_amdgcn_ubfe(cur[j], fb[j], 1u) == rm;
+#pragma unroll
+        for (int k = 0; k < j; ++k) ok = ok && fb[k] != fb[j];
+        if (ok) {
+          __hip_atomic_fetch_xor(wp[j], 1u << (fb[j] & 31u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+          --need;
+        }
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void bernoulli_mask(uint32_t *__restrict__ B, uint32_t m, uint32_t q, bool active,
+                                               uint32_t a, uint32_t b, uint32_t k0, uint32_t k1, uint32_t tlo,
+                                               uint32_t thi, uint32_t c2, uint32_t c3) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t W32 = (m + 31u) >> 5;
+  const uint32_t tz = (uint32_t)__builtin_ctz(a), nw = 4u - tz;
+  const uint32_t total = W32 * nw;                   // stream words of the mask
+  uint32_t c = 0, r = 0, i = tz, w = 0;
+  for (uint32_t base = 0; base < total; base += 4u) {
+    const uint4 bb = philox4x32_10(k0, k1, make_uint4(tlo, thi, c2 | ((base >> 2) << 12), c3));
+    const uint32_t u4[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (base + (uint32_t)e < total) {
+        r = ((a >> i) & 1u) ? (~u4[e] | r) : (~u4[e] & r);      // bit = (u < a), u's bit i from this word
+        if (++i == 4u) {
+          const uint32_t n = m - 32u * w;
+          if (n < 32u) r &= (1u << n) - 1u;
+          B[w * 64u + lane] = r;
+          c += (uint32_t)__builtin_popcount(r);
+          r = 0u;
+          i = tz;
+          ++w;
+        }
+      }
+    }
+  }
+  const uint32_t rm = c > q ? 1u : 0u;               // 1: clear members, 0: set non-members
+  const uint32_t need = active ? (rm ? c - q : q - c) : 0u;
+  const uint32_t blk0 = (total + 3u) >> 2;           // the fix-up starts at a fresh Philox block
+  const bool pow2 = (1u << b) == m;
+  if (b <= 8u) {
+    if (pow2) bernoulli_fixup<4, true>(B, m, b, rm, need, blk0, k0, k1, tlo, thi, c2, c3);
+    else bernoulli_fixup<4, false>(B, m, b, rm, need, blk0, k0, k1, tlo, thi, c2, c3);
+  } else if (b <= 10u) {
+    if (pow2) bernoulli_fixup<3, true>(B, m, b, rm, need, blk0, k0, k1, tlo, thi, c2, c3);
+    else bernoulli_fixup<3, false>(B, m, b, rm, need, blk0, k0, k1, tlo, thi, c2, c3);
+  } else {
+    if (pow2) bernoulli_fixup<2, true>(B, m, b, rm, need, blk0, k0, k1, tlo, thi, c2, c3);
+    else bernoulli_fixup<2, false>(B, m, b, rm, need, blk0, k0, k1, tlo, thi, c2, c3);
+  }
+}
+
 __device__ __forceinline__ void random_tally(const uint4 *__restrict__ plane, uint32_t *__restrict__ B,
                                              uint32_t W, uint32_t m, uint32_t q, bool active, uint32_t k0,
                                              uint32_t k1, uint32_t tlo, uint32_t thi, uint32_t node, uint32_t r,
-                                             uint32_t phase, uint32_t &c0, uint32_t &c1) {
+                                             uint32_t phase, uint32_t rd_a, uint32_t rd_b, uint32_t &c0,
+                                             uint32_t &c1) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t e = m - q;
-  const bool deliver_T = q <= e;
-  const uint32_t k = deliver_T ? q : e;
+  const bool bern = rd_a != 0u;
+  const bool deliver_T = bern || q <= e;
+  const uint32_t k = bern ? 0u : (deliver_T ? q : e);
   // Floyd over [0, m): for jj = m-k .. m-1, t = uniform(jj + 1) (Lemire, exact).
   // Words come from Philox stream 2 in order (DStream above: word i is element
   // i & 3 of block i >> 2).  Fast path: one block = 4 draws, taken while the
@@ -108,6 +205,7 @@ __device__ __forceinline__ void random_tally(const uint4 *__restrict__ plane, ui
   // Lemire's exact rejection test; otherwise one exact DStream step (same
   // words, same result -- the oracle's definition).
   const uint32_t c2 = node & 0xFFFu, c3 = (r & 0xFFFFFu) | ((phase & 1u) << 20) | (kStreamDelivery << 24);
+  if (bern) bernoulli_mask(B, m, q, active, rd_a, rd_b, k0, k1, tlo, thi, c2, c3);
   const uint32_t lb = (uint32_t)(uintptr_t)(lds_u32 *)B + lane * 4u;   // LDS address of this lane's word 0
   uint32_t jj = m - k, widx = 0;
   for (;;) {
@@ -218,7 +316,7 @@ __global__ void __launch_bounds__(256) benor_random_kernel(KParams p) {
         const bool active = c < m;
         const uint32_t node = active ? p.live_ids[c] : 0u;
         uint32_t a0, a1;
-        random_tally(X, B, W, m, q, active, k0, k1, tlo, thi, node, r, 0u, a0, a1);
+        random_tally(X, B, W, m, q, active, k0, k1, tlo, thi, node, r, 0u, p.rd_a, p.rd_b, a0, a1);
         const uint64_t vm = group_mask(j, m);
         const uint64_t p0 = ballot(a0 > a1) & vm;
         const uint64_t p1 = ballot(a1 > a0) & vm;
@@ -230,7 +328,7 @@ __global__ void __launch_bounds__(256) benor_random_kernel(KParams p) {
         const bool active = c < m;
         const uint32_t node = active ? p.live_ids[c] : 0u;
         uint32_t a0, a1;
-        random_tally(P, B, W, m, q, active, k0, k1, tlo, thi, node, r, 1u, a0, a1);
+        random_tally(P, B, W, m, q, active, k0, k1, tlo, thi, node, r, 1u, p.rd_a, p.rd_b, a0, a1);
         const uint64_t vm = group_mask(j, m);
         const bool d0l = a0 > F, d1l = a1 > F;
         const uint64_t d0 = ballot(d0l) & vm;
@@ -542,6 +640,16 @@ void plan_geometry(KParams &p) {
     p.G = 1;
     p.nblocks = W;
     p.variant = 2;
+    // sampler choice and parameters: oracle_delivery_bernoulli
+    const uint32_t e = p.m - p.q, k = p.q <= e ? p.q : e;
+    p.rd_a = p.rd_b = 0u;
+    if (k >= 64u && (uint64_t)k * 8u > p.m) {
+      uint32_t a = (16u * p.q + p.m - 1u) / p.m;
+      p.rd_a = a < 1u ? 1u : (a > 15u ? 15u : a);
+      uint32_t b = 1u;
+      while ((1u << b) < p.m) ++b;
+      p.rd_b = b;
+    }
     p.wave_bytes = 2u * W * 16u + 2u * W * 64u * 4u;   // X, P records + per-lane bitset
     p.lds_bytes = p.hist_bytes + kWavesPerBlock * p.wave_bytes;
     return;

@@ -293,13 +293,30 @@ typedef struct {
  * independent per (receiver, round, phase).  At f == F it is every live
  * sender, i.e. lockstep.
  *
- * Subset: k = min(e, q) with e = m - q; Floyd's algorithm draws a uniform
- * k-subset T of [0, m): for j = m-k .. m-1, t = uniform[0, j] (Lemire's
- * multiply-shift with exact rejection), T += (t in T) ? j : t.  Delivered set
- * = T if q <= e, else the live senders minus T.  Random words: Philox stream 2,
- * ctr {trial_lo, trial_hi, (node & 0xFFF) | (block << 12),
- * (round & 0xFFFFF) | (phase << 20) | (2 << 24)}, consumed in order
- * (word i = block i>>2, lane i&3).  `node` is the receiver's node id. */
+ * Random words: Philox stream 2, ctr {trial_lo, trial_hi, (node & 0xFFF) |
+ * (block << 12), (round & 0xFFFFF) | (phase << 20) | (2 << 24)}, consumed in
+ * order (word i = block i>>2, lane i&3).  `node` is the receiver's node id.
+ * Two exact samplers, picked by the plan constants (m, q); k = min(e, q),
+ * e = m - q:
+ *
+ * (a) k < 64 or k * 8 <= m: Floyd's algorithm draws a uniform k-subset T of [0, m): for
+ *     j = m-k .. m-1, t = uniform[0, j] (Lemire's multiply-shift with exact
+ *     rejection), T += (t in T) ? j : t.  Delivered set = T if q <= e, else
+ *     the live senders minus T.
+ * (b) otherwise, Bernoulli mask + exact fix-up.  Every sender is included
+ *     independently with p = a/16, a = ceil(16 q / m) in [1, 15]: bit = (u < a)
+ *     for a 4-bit u whose bit i comes from stream word i of the mask word,
+ *     evaluated from bit tz(a) upward as r = a_i ? (~w | r) : (~w & r) (the
+ *     bits of u below tz(a) cannot change the comparison and are not drawn),
+ *     so each 32-sender mask word takes 4 - tz(a) stream words; bits >= m are
+ *     cleared.  Given its count c the mask is a uniform c-subset; then, while
+ *     c != q, the next b-bit field (b = ceil(log2 m); floor(32/b) fields per
+ *     stream word, low bits first, starting at the Philox block after the
+ *     mask's last word) is a sender index idx, and when
+ *     idx < m and its bit is set (c > q) or clear (c < q) the bit is flipped:
+ *     each flip removes a uniform member (adds a uniform non-member), so the
+ *     result is a uniform q-subset.  Cost ~ m/32 words + |c - q| draws instead
+ *     of k draws. */
 typedef struct {
     uint32_t key[2], ctr[4];
     uint32_t buf[4];
@@ -328,6 +345,20 @@ static inline uint32_t dstream_uniform(orc_dstream *s, uint32_t range) {
     return (uint32_t)(m >> 32);
 }
 
+/* Sampler (b) parameters: p = a/16 and the index field width b. */
+int oracle_delivery_bernoulli(uint32_t m, uint32_t q, uint32_t *a_out, uint32_t *b_out) {
+    const uint32_t e = m - q, k = q <= e ? q : e;
+    if (k < 64u || (uint64_t)k * 8u <= m) return 0;
+    uint32_t a = (16u * q + m - 1u) / m;
+    if (a < 1u) a = 1u;
+    if (a > 15u) a = 15u;
+    uint32_t b = 1;
+    while ((1u << b) < m) ++b;
+    if (a_out) *a_out = a;
+    if (b_out) *b_out = b;
+    return 1;
+}
+
 /* D[W]: delivered-sender mask (compact sender indices) of receiver `node`. */
 void oracle_delivery_mask(uint64_t seed, uint64_t trial, uint32_t node, uint32_t round, uint32_t phase,
                           uint32_t m, uint32_t q, uint64_t *D) {
@@ -338,6 +369,43 @@ void oracle_delivery_mask(uint64_t seed, uint64_t trial, uint32_t node, uint32_t
     s.ctr[2] = node & 0xFFFu;
     s.ctr[3] = (round & 0xFFFFFu) | ((phase & 1u) << 20) | (ORC_STREAM_DELIVERY << 24);
     s.widx = 0;
+    uint32_t a, b;
+    if (oracle_delivery_bernoulli(m, q, &a, &b)) {          /* sampler (b) */
+        uint32_t M32[128];
+        const uint32_t W32 = (m + 31) / 32;
+        uint32_t tz = 0;
+        while (!((a >> tz) & 1u)) ++tz;
+        int64_t c = 0;
+        for (uint32_t w = 0; w < W32; ++w) {
+            uint32_t r = 0;
+            for (uint32_t i = tz; i < 4; ++i) {
+                const uint32_t u = dstream_next(&s);
+                r = ((a >> i) & 1u) ? (~u | r) : (~u & r);
+            }
+            const uint32_t n = m - 32u * w;
+            if (n < 32u) r &= (1u << n) - 1u;
+            M32[w] = r;
+            c += __builtin_popcount(r);
+        }
+        const uint32_t per = 32u / b, fmask = (1u << b) - 1u;
+        s.widx = (s.widx + 3u) & ~3u;                       /* fix-up fields start at a fresh block */
+        uint32_t word = 0, left = 0;
+        while (c != (int64_t)q) {
+            if (left == 0) { word = dstream_next(&s); left = per; }
+            const uint32_t idx = word & fmask;
+            word >>= b;
+            --left;
+            if (idx >= m) continue;
+            const uint32_t bit = (M32[idx >> 5] >> (idx & 31u)) & 1u;
+            if (bit == (c > (int64_t)q ? 1u : 0u)) {
+                M32[idx >> 5] ^= 1u << (idx & 31u);
+                c += bit ? -1 : 1;
+            }
+        }
+        for (uint32_t w = 0; w < W; ++w)
+            D[w] = (uint64_t)M32[2 * w] | ((2 * w + 1 < W32) ? (uint64_t)M32[2 * w + 1] << 32 : 0ull);
+        return;
+    }
     const uint32_t e = m - q;
     const int deliver_T = q <= e;
     const uint32_t k = deliver_T ? q : e;

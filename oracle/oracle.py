@@ -64,6 +64,9 @@ def lib():
                                            ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                            ctypes.POINTER(ctypes.c_uint64)]
         L.oracle_delivery_mask.restype = None
+        L.oracle_delivery_bernoulli.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
+                                                ctypes.POINTER(ctypes.c_uint32)]
+        L.oracle_delivery_bernoulli.restype = ctypes.c_int
         L.oracle_event_trials.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
                                           ctypes.POINTER(NodeState), ctypes.POINTER(ctypes.c_uint64)]
         L.oracle_event_trials.restype = ctypes.c_int
@@ -125,6 +128,15 @@ def hist_len(k_max: int) -> int:
 class TrialsResult:
     hist: np.ndarray
     states: list | None
+
+
+def delivery_bernoulli(m: int, q: int):
+    """(a, b) of the Bernoulli + fix-up sampler for (m, q), or None when the
+    Floyd sampler is used."""
+    a, b = ctypes.c_uint32(), ctypes.c_uint32()
+    if lib().oracle_delivery_bernoulli(m, q, ctypes.byref(a), ctypes.byref(b)):
+        return a.value, b.value
+    return None
 
 
 def delivery_mask(seed, trial, node, rnd, phase, m, q) -> list[int]:

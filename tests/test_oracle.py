@@ -184,6 +184,56 @@ def test_delivery_mask_exact_size_and_uniform(m, q):
         assert p > 0.01, p
 
 
+@pytest.mark.parametrize("m,q", [(7, 3), (10, 6), (8, 2), (16, 2), (16, 14)])
+def test_delivery_subset_law_is_uniform(m, q):
+    """Joint law, not only the marginals: every q-subset of the m senders is
+    equally likely (chi-square over all C(m, q) subsets), Floyd sampler."""
+    from math import comb
+
+    from scipy import stats
+
+    n = comb(m, q)
+    reps = 40 * n
+    cnt = {}
+    for i in range(reps):
+        D = oracle.delivery_mask(0x5EED, i // 7, i % 7, 1 + (i & 1), (i >> 1) & 1, m, q)
+        cnt[D[0]] = cnt.get(D[0], 0) + 1
+    assert len(cnt) == n and all(bin(k).count("1") == q for k in cnt)
+    assert stats.chisquare(list(cnt.values())).pvalue > 0.01
+
+
+def test_bernoulli_sampler_law_is_uniform():
+    """Bernoulli + fix-up sampler (k >= 64): exact size, uniform marginals, and
+    pairwise inclusion P(i, j in S) = q(q-1)/(m(m-1)) for every pair (a
+    non-uniform subset law with uniform marginals would show up in the pair
+    counts), chi-square p > 0.01."""
+    from scipy import stats
+
+    m, q, reps = 200, 72, 6000                      # k = 72 >= 64, 72 * 8 > 200: Bernoulli with p = 6/16
+    assert oracle.delivery_bernoulli(m, q) == (6, 8)
+    inc = np.zeros(m)
+    pair = np.zeros(m // 2)                         # disjoint pairs (2i, 2i+1)
+    for t in range(reps):
+        D = oracle.delivery_mask(0xB0B, t, t % 13, 1 + t % 3, t & 1, m, q)
+        bits = np.array([(D[i >> 6] >> (i & 63)) & 1 for i in range(m)])
+        assert bits.sum() == q
+        inc += bits
+        pair += bits[0::2] & bits[1::2]
+    assert stats.chisquare(inc, np.full(m, reps * q / m)).pvalue > 0.01
+    p2 = q * (q - 1) / (m * (m - 1))
+    z = (pair.sum() - reps * (m // 2) * p2) / np.sqrt(reps * (m // 2) * p2 * (1 - p2))
+    assert abs(z) < 3
+
+
+def test_delivery_sampler_choice():
+    assert not oracle.delivery_bernoulli(1024, 1024 - 41)          # k = 41: Floyd
+    assert oracle.delivery_bernoulli(1024, 683) == (11, 10)        # p = 11/16, 10-bit indices
+    assert oracle.delivery_bernoulli(2100, 1400) == (11, 12)
+    assert oracle.delivery_bernoulli(300, 100) == (6, 9)          # p = 3/8: 3 stream words per mask word
+    assert not oracle.delivery_bernoulli(10, 6)                   # k = 4 < 64: Floyd
+    assert not oracle.delivery_bernoulli(16, 2) and not oracle.delivery_bernoulli(64, 64)
+
+
 def test_random_delivery_reduces_to_lockstep_at_f_equals_F():
     for N, F in [(10, 4), (64, 21), (130, 2), (5, 1)]:
         fl = [i < F for i in range(N)]
