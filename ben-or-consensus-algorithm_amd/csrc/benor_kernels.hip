@@ -145,36 +145,65 @@ __device__ __forceinline__ void bernoulli_fixup(uint32_t *__restrict__ B, uint32
   }
 }
 
+// Mask generation for p = A/16, unrolled at compile time: NW = 4 - tz(A)
+// stream words per mask word, L = lcm(NW, 4) stream words (L/4 Philox blocks)
+// per super-block, bit = (u < A) combined from bit tz(A) up.
+template <int A>
+__device__ __forceinline__ uint32_t bernoulli_words(uint32_t *__restrict__ B, uint32_t m, uint32_t k0,
+                                                    uint32_t k1, uint32_t tlo, uint32_t thi, uint32_t c2,
+                                                    uint32_t c3, uint32_t &blocks) {
+  constexpr int TZ = __builtin_ctz(A), NW = 4 - TZ;
+  constexpr int L = NW == 3 ? 12 : 4, NB = L / 4, MW = L / NW;   // words, blocks, mask words per super-block
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t W32 = (m + 31u) >> 5;
+  uint32_t c = 0;
+  uint32_t blk = 0;
+  for (uint32_t w0 = 0; w0 < W32; w0 += MW) {
+    uint32_t u[L];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      if (j == 0 || w0 + (uint32_t)((4 * j) / NW) < W32) {    // blocks a partial super-block needs
+        const uint4 bb = philox4x32_10(k0, k1, make_uint4(tlo, thi, c2 | ((blk + j) << 12), c3));
+        u[4 * j] = bb.x, u[4 * j + 1] = bb.y, u[4 * j + 2] = bb.z, u[4 * j + 3] = bb.w;
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < MW; ++t) {
+      const uint32_t w = w0 + (uint32_t)t;
+      if (w < W32) {
+        uint32_t r = ~u[t * NW];
+#pragma unroll
+        for (int i = TZ + 1; i < 4; ++i) r = ((A >> i) & 1) ? (~u[t * NW + i - TZ] | r) : (~u[t * NW + i - TZ] & r);
+        const uint32_t n = m - 32u * w;
+        if (n < 32u) r &= (1u << n) - 1u;
+        B[w * 64u + lane] = r;
+        c += (uint32_t)__builtin_popcount(r);
+      }
+    }
+    blk += NB;
+  }
+  blocks = (W32 * NW + 3u) >> 2;                     // blocks the mask used (the fix-up starts after them)
+  return c;
+}
+
+template <int... As>
+__device__ __forceinline__ uint32_t bernoulli_words_any(uint32_t a, uint32_t *__restrict__ B, uint32_t m,
+                                                        uint32_t k0, uint32_t k1, uint32_t tlo, uint32_t thi,
+                                                        uint32_t c2, uint32_t c3, uint32_t &blocks,
+                                                        std::integer_sequence<int, As...>) {
+  uint32_t c = 0;
+  (void)((a == (uint32_t)(As + 1) ? (c = bernoulli_words<As + 1>(B, m, k0, k1, tlo, thi, c2, c3, blocks), true)
+                                  : false) || ...);
+  return c;
+}
+
 __device__ __forceinline__ void bernoulli_mask(uint32_t *__restrict__ B, uint32_t m, uint32_t q, bool active,
                                                uint32_t a, uint32_t b, uint32_t k0, uint32_t k1, uint32_t tlo,
                                                uint32_t thi, uint32_t c2, uint32_t c3) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t W32 = (m + 31u) >> 5;
-  const uint32_t tz = (uint32_t)__builtin_ctz(a), nw = 4u - tz;
-  const uint32_t total = W32 * nw;                   // stream words of the mask
-  uint32_t c = 0, r = 0, i = tz, w = 0;
-  for (uint32_t base = 0; base < total; base += 4u) {
-    const uint4 bb = philox4x32_10(k0, k1, make_uint4(tlo, thi, c2 | ((base >> 2) << 12), c3));
-    const uint32_t u4[4] = {bb.x, bb.y, bb.z, bb.w};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      if (base + (uint32_t)e < total) {
-        r = ((a >> i) & 1u) ? (~u4[e] | r) : (~u4[e] & r);      // bit = (u < a), u's bit i from this word
-        if (++i == 4u) {
-          const uint32_t n = m - 32u * w;
-          if (n < 32u) r &= (1u << n) - 1u;
-          B[w * 64u + lane] = r;
-          c += (uint32_t)__builtin_popcount(r);
-          r = 0u;
-          i = tz;
-          ++w;
-        }
-      }
-    }
-  }
+  uint32_t blk0 = 0;                                 // the fix-up starts at a fresh Philox block
+  const uint32_t c = bernoulli_words_any(a, B, m, k0, k1, tlo, thi, c2, c3, blk0, std::make_integer_sequence<int, 15>{});
   const uint32_t rm = c > q ? 1u : 0u;               // 1: clear members, 0: set non-members
   const uint32_t need = active ? (rm ? c - q : q - c) : 0u;
-  const uint32_t blk0 = (total + 3u) >> 2;           // the fix-up starts at a fresh Philox block
   const bool pow2 = (1u << b) == m;
   if (b <= 8u) {
     if (pow2) bernoulli_fixup<4, true>(B, m, b, rm, need, blk0, k0, k1, tlo, thi, c2, c3);
