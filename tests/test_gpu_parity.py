@@ -86,6 +86,30 @@ def test_random_fault_placement_states(N, F, reps):
         assert got == ref
 
 
+@pytest.mark.parametrize("N,F,W,G", [(2113, 0, 34, 17), (2800, 0, 44, 22), (4000, 0, 63, 21), (2600, 300, 36, 18)])
+def test_blocked_kernel_block_sizes(N, F, W, G):
+    """The blocked kernel (m > 2048) at block sizes G > 16, where even-M
+    proposal records are staged in two VGPRs: random-init histograms and a
+    tied fixed start (round 1 proposes "?", coins follow) per node, against
+    the oracle.  W = ceil(m/64); G is the plan's block size."""
+    m = N - F
+    assert (m + 63) // 64 == W
+    seed = 0xB10C ^ N
+    plan = benor.TrialsPlan(N, F, first_f(N, F), seed=seed, k_max=24)
+    ref = oracle.run_trials(N, F, first_f(N, F), seed=seed, trial_begin=11, trial_count=300, k_max=24)
+    np.testing.assert_array_equal(plan.run(11, 300), ref.hist)
+    if m % 2 == 0:
+        live = [i for i in range(N) if i >= F]
+        init = [0] * N
+        for i in live[::2]:
+            init[i] = 1                                  # m/2 ones: tied round 1
+        for t in range(2):
+            want = oracle.run_trials(N, F, first_f(N, F), seed=seed, trial_begin=t, trial_count=1, k_max=24,
+                                     initial_values=init, want_states=True).states
+            _, got = benor.run_trial_states(N, F, first_f(N, F), seed=seed, trial=t, k_max=24, initial_values=init)
+            assert got == want
+
+
 def test_reference_known_answers_network_api(reference_cases):
     """benorconsensus.test.ts:133-486 through launchNetwork / startConsensus /
     getNodesState / stopConsensus -- the reference's call sequence."""
