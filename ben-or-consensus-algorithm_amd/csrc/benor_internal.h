@@ -21,6 +21,7 @@ constexpr int kWavesPerBlock = 4;          // 256-thread workgroups, one trial p
 constexpr uint32_t kMaxW = BO_MAX_N / 64;  // u64 words per bit plane at N = 4096
 constexpr int kMaxWSpecialised = 32;       // m <= 2048: fully unrolled W-specialised kernel
 constexpr uint32_t kMaxLaneM = 64;         // m <= 64: lane kernel, one trial per lane (benor_lane.h)
+constexpr uint32_t kMaxEventN = 256;       // event level: node ids in 8 bits of a message
 constexpr uint64_t kMaxTrialsPerLaunch = 1ull << 31;   // trial offsets within a launch fit 32 bits
 constexpr uint32_t kParamBytes = 32;       // LDS parameter block after the histogram (W kernel)
 
@@ -49,8 +50,8 @@ struct KParams {
   unsigned long long *hist;        // [hist_len] (device, accumulated)
   bo_node_state *node_out;         // [N] (device) or nullptr; only with trial_count == 1
   uint32_t *rounds_out;            // (device) or nullptr
-  // event-level mode (variant 4)
-  uint64_t faulty_mask;            // N <= 64
+  // event-level mode (variant 4), N <= kMaxEventN
+  uint64_t faulty_mask[4];         // node-id bitset, N <= 256
   const int8_t *init_x;            // [N] (device; fixed init)
   const uint32_t *crash_at;        // [N] (device) or nullptr
   uint32_t crash_count, crash_window;

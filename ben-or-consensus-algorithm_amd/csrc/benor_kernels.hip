@@ -431,15 +431,32 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t &s) {
   return z ^ (z >> 31);
 }
 
+// Node-id bitsets of NW 64-bit words (N <= 64 NW, event mode N <= 256): a
+// dynamic word index is resolved by selects over the NW registers.
+template <int NW>
+__device__ __forceinline__ bool set_has(const uint64_t (&m)[NW], uint32_t i) {
+  uint64_t w = m[0];
+#pragma unroll
+  for (int j = 1; j < NW; ++j) w = (i >> 6) == (uint32_t)j ? m[j] : w;
+  return (w >> (i & 63u)) & 1ull;
+}
+template <int NW>
+__device__ __forceinline__ void set_add(uint64_t (&m)[NW], uint32_t i) {
+  const uint64_t bit = 1ull << (i & 63u);
+#pragma unroll
+  for (int j = 0; j < NW; ++j) m[j] |= (i >> 6) == (uint32_t)j ? bit : 0ull;
+}
+
 struct EvLane {
-  uint32_t *pool;      // [cap]
-  uint32_t *ibox;      // [N][4][2] packed {c0, c1, len} bytes
+  uint32_t *pool;      // [cap] messages: to | phase << 8 | x << 9 | k << 11
+  uint32_t *ibox;      // [N][4][2] packed {c0, c1, len}, 10 bits each
+  uint64_t *comp;      // [4][NW] completion masks, round k at k & 3
+  uint64_t *crash;     // [N] sorted (event << 8 | node)
   int8_t *xs;          // [N]
   int16_t *ks;         // [N]
-  uint64_t *comp;      // [4] completion masks, round k at k & 3
-  uint32_t *crash;     // [64] sorted (event << 6 | node)
 };
 
+template <int NW>
 __global__ void __launch_bounds__(256) benor_event_kernel(KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint32_t *lhist = reinterpret_cast<uint32_t *>(smem);
@@ -447,7 +464,12 @@ __global__ void __launch_bounds__(256) benor_event_kernel(KParams p) {
   __syncthreads();
 
   const uint32_t N = p.N, F = p.F, quorum = p.N - p.F, m = p.m;
-  const uint64_t all = N == 64 ? ~0ull : ((1ull << N) - 1ull);
+  uint64_t all[NW];
+#pragma unroll
+  for (int j = 0; j < NW; ++j) {
+    const uint32_t lo = 64u * (uint32_t)j;
+    all[j] = N >= lo + 64u ? ~0ull : (N > lo ? (1ull << (N - lo)) - 1ull : 0ull);
+  }
   const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t lanes = (uint64_t)gridDim.x * blockDim.x;
   const uint32_t cap = p.ev_cap;
@@ -456,55 +478,74 @@ __global__ void __launch_bounds__(256) benor_event_kernel(KParams p) {
   L.pool = base;
   L.ibox = L.pool + cap;
   L.comp = reinterpret_cast<uint64_t *>(L.ibox + N * 8u);
-  L.crash = reinterpret_cast<uint32_t *>(L.comp + 4);
-  L.xs = reinterpret_cast<int8_t *>(L.crash + 64);
-  L.ks = reinterpret_cast<int16_t *>(L.xs + 64);
+  L.crash = L.comp + 4 * NW;
+  L.xs = reinterpret_cast<int8_t *>(L.crash + N);
+  L.ks = reinterpret_cast<int16_t *>(L.xs + ((N + 3u) & ~3u));
   const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
+
+  auto full = [&](const uint64_t *a, const uint64_t (&b)[NW]) {   // a | b == all
+    bool f = true;
+#pragma unroll
+    for (int j = 0; j < NW; ++j) f = f && (a[j] | b[j]) == all[j];
+    return f;
+  };
 
   for (uint64_t t = gid; t < p.trial_count; t += lanes) {
     const uint64_t trial = p.trial_begin + t;
     const uint32_t tlo = (uint32_t)trial, thi = (uint32_t)(trial >> 32);
-    uint64_t killed = p.faulty_mask, decided = 0;
-    // ---- node.ts:21-26 and initial values (compact live order)
+    uint64_t killed[NW], decided[NW];
+#pragma unroll
+    for (int j = 0; j < NW; ++j) {
+      killed[j] = p.faulty_mask[j];
+      decided[j] = 0ull;
+    }
+    // ---- node.ts:21-26 and initial values (compact live order): word c >> 5 of stream 1
     uint4 ir = make_uint4(0, 0, 0, 0);
-    if (p.init_mode == BO_INIT_RANDOM) ir = philox4x32_10<false>(k0, k1, make_uint4(tlo, thi, 0u, kStreamInit << 24));
     for (uint32_t c = 0; c < m; ++c) {
       const uint32_t i = p.live_ids[c];
       int8_t v;
-      if (p.init_mode == BO_INIT_RANDOM) v = (int8_t)((((c >> 5) ? ir.y : ir.x) >> (c & 31u)) & 1u);
-      else v = p.init_x[i];
+      if (p.init_mode == BO_INIT_RANDOM) {
+        if ((c & 127u) == 0u) ir = philox4x32_10<false>(k0, k1, make_uint4(tlo, thi, c >> 7, kStreamInit << 24));
+        const uint32_t j = (c >> 5) & 3u;
+        const uint32_t w = j == 0u ? ir.x : j == 1u ? ir.y : j == 2u ? ir.z : ir.w;
+        v = (int8_t)((w >> (c & 31u)) & 1u);
+      } else {
+        v = p.init_x[i];
+      }
       L.xs[i] = v;
       L.ks[i] = 0;
     }
     for (uint32_t i = 0; i < N; ++i)
-      if ((killed >> i) & 1ull) { L.xs[i] = -1; L.ks[i] = -1; }
+      if (set_has(killed, i)) { L.xs[i] = -1; L.ks[i] = -1; }
     for (uint32_t j = 0; j < N * 8u; ++j) L.ibox[j] = 0u;
-    for (int j = 0; j < 4; ++j) L.comp[j] = 0ull;
+    for (int j = 0; j < 4 * NW; ++j) L.comp[j] = 0ull;
     // ---- mid-run /stop schedule, sorted by event index
     uint32_t ncrash = 0;
     if (p.crash_at) {
       for (uint32_t i = 0; i < N; ++i)
-        if (p.crash_at[i] != 0xFFFFFFFFu && p.crash_at[i] < (1u << 26)) L.crash[ncrash++] = (p.crash_at[i] << 6) | i;
+        if (p.crash_at[i] != 0xFFFFFFFFu) L.crash[ncrash++] = ((uint64_t)p.crash_at[i] << 8) | i;
     } else if (p.crash_count > 0 && m > 0 && p.crash_window > 0) {
       DStream ds;
       ds.k0 = k0; ds.k1 = k1; ds.c0 = tlo; ds.c1 = thi; ds.c2 = 0u; ds.c3 = kStreamCrash << 24; ds.widx = 0;
       const uint32_t kk = p.crash_count < m ? p.crash_count : m;
-      uint64_t T = 0;
-      uint32_t picks[64];
-      uint32_t n = 0;
-      for (uint32_t j = m - kk; j < m; ++j, ++n) {
+      // Floyd over compact live indices; the picks go to the crash list first
+      // (node field = compact index), then get their event indices in pick order
+      uint64_t T[NW];
+#pragma unroll
+      for (int j = 0; j < NW; ++j) T[j] = 0ull;
+      for (uint32_t j = m - kk; j < m; ++j) {
         const uint32_t tt = ds.uniform(j + 1u);
-        const uint32_t idx = ((T >> tt) & 1ull) ? j : tt;
-        T |= 1ull << idx;
-        picks[n] = idx;
+        const uint32_t idx = set_has(T, tt) ? j : tt;
+        set_add(T, idx);
+        L.crash[ncrash++] = idx;
       }
       for (uint32_t q2 = 0; q2 < kk; ++q2) {
         const uint32_t when = ds.uniform(p.crash_window);
-        if (when < (1u << 26)) L.crash[ncrash++] = (when << 6) | p.live_ids[picks[q2]];
+        L.crash[q2] = ((uint64_t)when << 8) | p.live_ids[(uint32_t)L.crash[q2]];
       }
     }
-    for (uint32_t a = 1; a < ncrash; ++a) {            // insertion sort (<= 64 entries)
-      const uint32_t v = L.crash[a];
+    for (uint32_t a = 1; a < ncrash; ++a) {            // insertion sort (<= N entries)
+      const uint64_t v = L.crash[a];
       uint32_t b = a;
       while (b > 0 && L.crash[b - 1] > v) { L.crash[b] = L.crash[b - 1]; --b; }
       L.crash[b] = v;
@@ -519,28 +560,30 @@ __global__ void __launch_bounds__(256) benor_event_kernel(KParams p) {
     // ---- /start (node.ts:167-188)
     uint32_t len = 0;
     for (uint32_t i = 0; i < N; ++i) {
-      if ((killed >> i) & 1ull) continue;
+      if (set_has(killed, i)) continue;
       L.ks[i] = 1;
-      const uint32_t body = ((uint32_t)(L.xs[i] & 3) << 7) | (1u << 9);
+      const uint32_t body = ((uint32_t)(L.xs[i] & 3) << 9) | (1u << 11);
       for (uint32_t to = 0; to < N; ++to) L.pool[len++] = to | body;
     }
     uint32_t cur = 1, R = 0, halted = 0;
     bool overflow = false;
-    for (uint32_t e = 0;; ++e) {
+    for (uint64_t e = 0;; ++e) {
       // scheduled GET /stop (node.ts:191-194)
       bool crashed = false;
-      while (next < ncrash && (L.crash[next] >> 6) == e) {
-        const uint32_t i = L.crash[next] & 63u;
-        killed |= 1ull << i;
+      while (next < ncrash && (L.crash[next] >> 8) == e) {
+        set_add(killed, (uint32_t)(L.crash[next] & 255u));
         crashed = true;
         ++next;
       }
       if (crashed) {
-        if (killed == all) { halted = 3; break; }
-        while ((L.comp[cur & 3u] | killed) == all) {
-          if ((decided | killed) == all) { halted = 1; R = cur; break; }
+        bool dead = true;
+#pragma unroll
+        for (int j = 0; j < NW; ++j) dead = dead && killed[j] == all[j];
+        if (dead) { halted = 3; break; }
+        while (full(L.comp + (cur & 3u) * NW, killed)) {
+          if (full(decided, killed)) { halted = 1; R = cur; break; }
           if (cur >= p.k_max) { halted = 2; R = cur; break; }
-          L.comp[cur & 3u] = 0ull;
+          for (int j = 0; j < NW; ++j) L.comp[(cur & 3u) * NW + j] = 0ull;
           ++cur;
         }
         if (halted) break;
@@ -549,45 +592,52 @@ __global__ void __launch_bounds__(256) benor_event_kernel(KParams p) {
       const uint32_t pick = (uint32_t)(((uint64_t)(uint32_t)(splitmix64(rng) >> 32) * (uint64_t)len) >> 32);
       const uint32_t msg = L.pool[pick];
       L.pool[pick] = L.pool[--len];
-      const uint32_t to = msg & 63u, ph = (msg >> 6) & 1u, k = msg >> 9;
-      const uint32_t x = (msg >> 7) & 3u;
-      if ((killed >> to) & 1ull) continue;             // node.ts:45
+      const uint32_t to = msg & 255u, ph = (msg >> 8) & 1u, k = msg >> 11;
+      const uint32_t x = (msg >> 9) & 3u;
+      if (set_has(killed, to)) continue;               // node.ts:45
       uint32_t *bx = &L.ibox[(to * 4u + (k & 3u)) * 2u + ph];
       uint32_t b = *bx;
-      b += 1u << 16;                                   // len
+      b += 1u << 20;                                   // len
       if (x == 0u) b += 1u;                            // c0
-      else if (x == 1u) b += 1u << 8;                  // c1
+      else if (x == 1u) b += 1u << 10;                 // c1
       *bx = b;
-      if ((b >> 16) != quorum) continue;               // node.ts:52, :88 (fires once: exactly F faulty)
-      const uint32_t c0 = b & 0xFFu, c1 = (b >> 8) & 0xFFu;
+      if ((b >> 20) != quorum) continue;               // node.ts:52, :88 (fires once: exactly F faulty)
+      const uint32_t c0 = b & 1023u, c1 = (b >> 10) & 1023u;
       uint32_t body;
       if (ph == 0u) {                                  // node.ts:53-80
         const uint32_t v = c0 > c1 ? 0u : (c1 > c0 ? 1u : 2u);
-        body = (1u << 6) | (v << 7) | (k << 9);
+        body = (1u << 8) | (v << 9) | (k << 11);
       } else {                                         // node.ts:89-157
         int8_t nx;
-        if (c0 > F) { nx = 0; decided |= 1ull << to; }
-        else if (c1 > F) { nx = 1; decided |= 1ull << to; }
+        if (c0 > F) { nx = 0; set_add(decided, to); }
+        else if (c1 > F) { nx = 1; set_add(decided, to); }
         else if (c0 + c1 > 0 && c0 > c1) nx = 0;
         else if (c0 + c1 > 0 && c0 < c1) nx = 1;
         else {
-          const uint32_t c = (uint32_t)__builtin_popcountll(~p.faulty_mask & ((1ull << to) - 1ull));   // compact index
+          // compact index of `to` (coin_block, node.ts:111)
+          uint32_t c = 0;
+#pragma unroll
+          for (int j = 0; j < NW; ++j) {
+            const uint32_t lo = 64u * (uint32_t)j;
+            const uint64_t below = to >= lo + 64u ? ~0ull : (to > lo ? (1ull << (to - lo)) - 1ull : 0ull);
+            c += (uint32_t)__builtin_popcountll(~p.faulty_mask[j] & below & all[j]);
+          }
           const uint4 rr = philox4x32_10<false>(k0, k1, make_uint4(tlo, thi, c >> 5, ((k - 1u) >> 2) | (kStreamCoin << 24)));
-          nx = (int8_t)((coin_word(rr, k) >> (c & 31u)) & 1u);   // node.ts:111
+          nx = (int8_t)((coin_word(rr, k) >> (c & 31u)) & 1u);
         }
         L.xs[to] = nx;
         L.ks[to] = (int16_t)(k + 1u);
         L.ibox[(to * 4u + ((k + 2u) & 3u)) * 2u + 0u] = 0u;   // recycle round k-2's slots for k+2
         L.ibox[(to * 4u + ((k + 2u) & 3u)) * 2u + 1u] = 0u;
-        L.comp[k & 3u] |= 1ull << to;
-        while ((L.comp[cur & 3u] | killed) == all) {
-          if ((decided | killed) == all) { halted = 1; R = cur; break; }
+        L.comp[(k & 3u) * NW + (to >> 6)] |= 1ull << (to & 63u);
+        while (full(L.comp + (cur & 3u) * NW, killed)) {
+          if (full(decided, killed)) { halted = 1; R = cur; break; }
           if (cur >= p.k_max) { halted = 2; R = cur; break; }
-          L.comp[cur & 3u] = 0ull;
+          for (int j = 0; j < NW; ++j) L.comp[(cur & 3u) * NW + j] = 0ull;
           ++cur;
         }
         if (halted) break;
-        body = ((uint32_t)(nx & 3) << 7) | ((k + 1u) << 9);
+        body = ((uint32_t)(nx & 3) << 9) | ((k + 1u) << 11);
       }
       if (len + N > cap) { overflow = true; halted = 3; break; }
       for (uint32_t dst = 0; dst < N; ++dst) L.pool[len++] = dst | body;
@@ -596,7 +646,7 @@ __global__ void __launch_bounds__(256) benor_event_kernel(KParams p) {
     bool any0 = false, any1 = false, anyq = false;
     uint32_t nlive = 0;
     for (uint32_t i = 0; i < N; ++i) {
-      if ((killed >> i) & 1ull) continue;
+      if (set_has(killed, i)) continue;
       ++nlive;
       const int8_t v = L.xs[i];
       if (v == 0) any0 = true; else if (v == 1) any1 = true; else anyq = true;
@@ -607,11 +657,11 @@ __global__ void __launch_bounds__(256) benor_event_kernel(KParams p) {
     if (overflow && p.rounds_out) atomicOr(p.rounds_out, 0x80000000u);
     if (p.node_out) {
       for (uint32_t i = 0; i < N; ++i) {
-        const bool f = (p.faulty_mask >> i) & 1ull;
+        const bool f = (p.faulty_mask[i >> 6] >> (i & 63u)) & 1ull;
         bo_node_state ns;
-        ns.killed = (int8_t)((killed >> i) & 1ull);
+        ns.killed = (int8_t)(set_has(killed, i) ? 1 : 0);
         ns.x = L.xs[i];
-        ns.decided = f ? (int8_t)-1 : (int8_t)((decided >> i) & 1ull);
+        ns.decided = f ? (int8_t)-1 : (int8_t)(set_has(decided, i) ? 1 : 0);
         ns.pad = 0;
         ns.k = L.ks[i];
         p.node_out[i] = ns;
@@ -660,8 +710,10 @@ void plan_geometry(KParams &p) {
     p.wave_bytes = 0;
     p.lds_bytes = p.hist_bytes;
     // per-lane scratch (u32 words): pool, inbox window, comp[4] (u64), crash[64], xs[64] (i8), ks[64] (i16)
+    const uint32_t NW = p.N <= 64u ? 1u : 4u;
     p.ev_cap = 4u * p.N * p.N + 64u;
-    p.ev_stride = p.ev_cap + p.N * 8u + 8u + 64u + 16u + 32u;
+    // per-lane scratch (u32 words): pool, inbox window, comp[4][NW] (u64), crash[N] (u64), xs (i8), ks (i16)
+    p.ev_stride = p.ev_cap + p.N * 8u + 8u * NW + 2u * p.N + ((p.N + 3u) & ~3u) / 4u + (p.N + 1u) / 2u;
     p.ev_stride = (p.ev_stride + 31u) & ~31u;
     return;
   }
@@ -749,7 +801,8 @@ static hipError_t dispatch_b(const KParams &p, int grid, hipStream_t s, std::int
 
 hipError_t launch_lockstep(const KParams &p, int grid, hipStream_t s) {
   if (p.variant == 4) {
-    hipLaunchKernelGGL(benor_event_kernel, dim3(grid), dim3(256), p.lds_bytes, s, p);
+    if (p.N <= 64u) hipLaunchKernelGGL(benor_event_kernel<1>, dim3(grid), dim3(256), p.lds_bytes, s, p);
+    else hipLaunchKernelGGL(benor_event_kernel<4>, dim3(grid), dim3(256), p.lds_bytes, s, p);
     return hipGetLastError();
   }
   if (p.variant == 6) return dispatch_lane(p, grid, s, std::make_integer_sequence<int, (int)kMaxLaneM>{});

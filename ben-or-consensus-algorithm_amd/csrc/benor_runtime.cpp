@@ -238,7 +238,8 @@ int bo_plan_create(const bo_trials_cfg *cfg, bo_plan **out) {
   if (cfg->k_max < 1 || cfg->k_max > BO_MAX_K) return fail(BO_ERR_INVALID_ARGUMENT, "k_max must be in [1, 1024]");
   if (cfg->mode != BO_MODE_LOCKSTEP && cfg->mode != BO_MODE_RANDOM_DELIVERY && cfg->mode != BO_MODE_EVENT)
     return fail(BO_ERR_UNSUPPORTED, "unknown delivery mode");
-  if (cfg->mode == BO_MODE_EVENT && cfg->N > 64) return fail(BO_ERR_UNSUPPORTED, "event mode simulates N <= 64");
+  if (cfg->mode == BO_MODE_EVENT && cfg->N > benor::kMaxEventN)
+    return fail(BO_ERR_UNSUPPORTED, "event mode simulates N <= 256");
   if (cfg->init_mode != BO_INIT_RANDOM && cfg->init_mode != BO_INIT_FIXED)
     return fail(BO_ERR_INVALID_ARGUMENT, "unknown init_mode");
   if (!cfg->faulty) return fail(BO_ERR_INVALID_ARGUMENT, "faulty is NULL");
@@ -276,8 +277,8 @@ int bo_plan_create(const bo_trials_cfg *cfg, bo_plan **out) {
   kp.q = cfg->N - cfg->F;
   kp.crash_count = cfg->crash_count;
   kp.crash_window = cfg->crash_window;
-  for (uint32_t i = 0; i < cfg->N && i < 64; ++i)
-    if (cfg->faulty[i]) kp.faulty_mask |= 1ull << i;
+  for (uint32_t i = 0; i < cfg->N && i < 4u * 64u; ++i)
+    if (cfg->faulty[i]) kp.faulty_mask[i >> 6] |= 1ull << (i & 63u);
   if (m > 0) {
     benor::plan_geometry(kp);
     std::vector<uint4> plane(kp.W, make_uint4(0, 0, 0, 0));

@@ -55,7 +55,7 @@ enum {
 /* EVENT is message-granular: the reference's handler
  * (node.ts:45-158) delivery by delivery, in a seeded random order, with the
  * reference's mid-run GET /stop (node.ts:191-194) applied at scheduled
- * delivery counts.  Exactly F crash-faulty nodes; N <= 64. */
+ * delivery counts.  Exactly F crash-faulty nodes; N <= 256. */
 enum { BO_MODE_LOCKSTEP = 0, BO_MODE_RANDOM_DELIVERY = 1, BO_MODE_EVENT = 2 };
 
 enum { BO_INIT_RANDOM = 0, BO_INIT_FIXED = 1 };

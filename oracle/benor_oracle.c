@@ -578,7 +578,7 @@ int oracle_run_trials(const orc_trials_cfg *cfg, uint64_t *hist, orc_node_state 
 }
 
 /* ===================================================================== */
-/* (iii) event-level asynchronous mode                    */
+/* (iii) event-level asynchronous mode, N <= 256          */
 /* ===================================================================== */
 /* Message-granular restatement of node.ts:43-199 with the reference's own
  * mid-run crash: GET /stop (node.ts:191-194) may hit a live node at any
@@ -612,7 +612,18 @@ typedef struct {
 
 #define ORC_STREAM_CRASH 4u
 
-typedef struct { int8_t c0, c1, len, pad; } orc_ibox;
+typedef struct { int16_t c0, c1, len, pad; } orc_ibox;
+
+/* bitsets over node ids (N <= ORC_EV_MAX_N) */
+#define ORC_EV_MAX_N 256u
+#define ORC_EV_NW (ORC_EV_MAX_N / 64u)
+typedef struct { uint64_t w[ORC_EV_NW]; } orc_set;
+static inline int set_has(const orc_set *s, uint32_t i) { return (int)((s->w[i >> 6] >> (i & 63u)) & 1u); }
+static inline void set_add(orc_set *s, uint32_t i) { s->w[i >> 6] |= 1ull << (i & 63u); }
+static inline int set_union_full(const orc_set *a, const orc_set *b, const orc_set *all) {
+    for (uint32_t j = 0; j < ORC_EV_NW; ++j) if ((a->w[j] | b->w[j]) != all->w[j]) return 0;
+    return 1;
+}
 
 /* One trial.  Returns the outcome bin (index into the histogram) and fills
  * state_out[N] when given; *events_out = messages delivered. */
@@ -620,23 +631,27 @@ static uint32_t event_trial(const orc_event_cfg *cfg, uint64_t trial, orc_node_s
                             uint64_t *events_out) {
     const uint32_t N = cfg->N, F = cfg->F, KR = cfg->k_max + 3;
     const int64_t quorum = (int64_t)N - (int64_t)F;
-    const size_t H = (size_t)(cfg->k_max + 1) * 3;
-    orc_node_state st[64];
-    uint32_t live_ids[64], cidx[64], m = 0;
-    uint64_t killed = 0, decided = 0, all = (N == 64) ? ~0ull : ((1ull << N) - 1);
+    orc_node_state *st = (orc_node_state *)malloc(sizeof(orc_node_state) * N);
+    uint32_t *live_ids = (uint32_t *)malloc(sizeof(uint32_t) * N), *cidx = (uint32_t *)malloc(sizeof(uint32_t) * N);
+    uint32_t m = 0;
+    orc_set killed, decided, all;
+    memset(&killed, 0, sizeof killed);
+    memset(&decided, 0, sizeof decided);
+    memset(&all, 0, sizeof all);
     for (uint32_t i = 0; i < N; ++i) {
         const int f = cfg->faulty[i] != 0;
         st[i].killed = (int8_t)f; st[i].decided = f ? -1 : 0; st[i].k = f ? -1 : 0; st[i].pad = 0;
         st[i].x = -1;
         cidx[i] = m;
-        if (f) killed |= 1ull << i; else live_ids[m++] = i;
+        set_add(&all, i);
+        if (f) set_add(&killed, i); else live_ids[m++] = i;
     }
     for (uint32_t c = 0; c < m; ++c) {
         const uint32_t i = live_ids[c];
         st[i].x = (int8_t)(cfg->init_mode == 1 ? cfg->init[i] : oracle_random_init(cfg->seed, trial, c));
     }
     /* crash schedule */
-    uint32_t crash_at[64];
+    uint32_t *crash_at = (uint32_t *)malloc(sizeof(uint32_t) * N);
     for (uint32_t i = 0; i < N; ++i) crash_at[i] = cfg->crash_at ? cfg->crash_at[i] : 0xFFFFFFFFu;
     if (!cfg->crash_at && cfg->crash_count > 0 && m > 0 && cfg->crash_window > 0) {
         orc_dstream s;
@@ -644,35 +659,37 @@ static uint32_t event_trial(const orc_event_cfg *cfg, uint64_t trial, orc_node_s
         s.ctr[0] = (uint32_t)trial; s.ctr[1] = (uint32_t)(trial >> 32);
         s.ctr[2] = 0; s.ctr[3] = ORC_STREAM_CRASH << 24; s.widx = 0;
         const uint32_t k = cfg->crash_count < m ? cfg->crash_count : m;
-        uint64_t T = 0;
-        uint32_t picks[64];
+        orc_set T;
+        memset(&T, 0, sizeof T);
+        uint32_t *picks = (uint32_t *)malloc(sizeof(uint32_t) * (k + 1));
         for (uint32_t j = m - k, n = 0; j < m; ++j, ++n) {
             const uint32_t t = dstream_uniform(&s, j + 1u);
-            const uint32_t idx = ((T >> t) & 1ull) ? j : t;
-            T |= 1ull << idx;
+            const uint32_t idx = set_has(&T, t) ? j : t;
+            set_add(&T, idx);
             picks[n] = idx;
         }
         for (uint32_t n = 0; n < k; ++n) crash_at[live_ids[picks[n]]] = dstream_uniform(&s, cfg->crash_window);
+        free(picks);
     }
     /* inboxes[node][k][phase] */
     orc_ibox *ib = (orc_ibox *)calloc((size_t)N * KR * 2, sizeof(orc_ibox));
-    uint64_t *comp = (uint64_t *)calloc(KR, sizeof(uint64_t));
+    orc_set *comp = (orc_set *)calloc(KR, sizeof(orc_set));
     uint8_t *pdone = (uint8_t *)calloc((size_t)N * KR, 1);
     size_t cap = (size_t)4 * N * N + 64, len = 0;
     uint32_t *pool = (uint32_t *)malloc(cap * sizeof(uint32_t));
-    /* message: to (6) | phase << 6 | (x & 3) << 7 | k << 9 */
+    /* message: to (8) | phase << 8 | (x & 3) << 9 | k << 11 */
 #define EV_SEND(K, X, PH)                                                               \
     do {                                                                                \
         for (uint32_t to_ = 0; to_ < N; ++to_) {                                        \
             if (len == cap) { cap *= 2; pool = (uint32_t *)realloc(pool, cap * 4); }   \
-            pool[len++] = to_ | ((uint32_t)(PH) << 6) | ((uint32_t)((X) & 3) << 7) | ((uint32_t)(K) << 9); \
+            pool[len++] = to_ | ((uint32_t)(PH) << 8) | ((uint32_t)((X) & 3) << 9) | ((uint32_t)(K) << 11); \
         }                                                                               \
     } while (0)
     orc_rng rng;
     rng.s = (((uint64_t)orc_philox_word(cfg->seed, trial, 0, ORC_STREAM_ORDER << 24, 0) << 32) |
              orc_philox_word(cfg->seed, trial, 0, ORC_STREAM_ORDER << 24, 1)) ^ 0xD1B54A32D192ED03ull;
     for (uint32_t i = 0; i < N; ++i)                    /* /start, node.ts:171-185 */
-        if (!((killed >> i) & 1ull)) { st[i].k = 1; EV_SEND(1u, st[i].x, 0u); }
+        if (!set_has(&killed, i)) { st[i].k = 1; EV_SEND(1u, st[i].x, 0u); }
     uint32_t cur = 1, R = 0;
     int halted = 0;                                      /* 1 decided, 2 k_max, 3 stall */
     uint64_t e = 0;
@@ -680,11 +697,11 @@ static uint32_t event_trial(const orc_event_cfg *cfg, uint64_t trial, orc_node_s
         /* scheduled /stop (node.ts:191-194) */
         int crashed = 0;
         for (uint32_t i = 0; i < N; ++i)
-            if (crash_at[i] == e && !((killed >> i) & 1ull)) { killed |= 1ull << i; st[i].killed = 1; crashed = 1; }
-        if (crashed && killed == all) { halted = 3; break; }
+            if (crash_at[i] == e && !set_has(&killed, i)) { set_add(&killed, i); st[i].killed = 1; crashed = 1; }
+        if (crashed && set_union_full(&killed, &killed, &all)) { halted = 3; break; }
         if (crashed) {
-            while (cur < KR && (comp[cur] | killed) == all) {
-                if ((decided | killed) == all) { halted = 1; R = cur; break; }
+            while (cur < KR && set_union_full(&comp[cur], &killed, &all)) {
+                if (set_union_full(&decided, &killed, &all)) { halted = 1; R = cur; break; }
                 if (cur >= cfg->k_max) { halted = 2; R = cur; break; }
                 ++cur;
             }
@@ -695,9 +712,9 @@ static uint32_t event_trial(const orc_event_cfg *cfg, uint64_t trial, orc_node_s
         const uint32_t msg = pool[pick];
         pool[pick] = pool[--len];
         ++e;
-        const uint32_t to = msg & 63u, ph = (msg >> 6) & 1u, k = msg >> 9;
-        const int8_t x = (int8_t)((msg >> 7) & 3u);
-        if ((killed >> to) & 1ull) continue;             /* node.ts:45 */
+        const uint32_t to = msg & 255u, ph = (msg >> 8) & 1u, k = msg >> 11;
+        const int8_t x = (int8_t)((msg >> 9) & 3u);
+        if (set_has(&killed, to)) continue;              /* node.ts:45 */
         if (k >= KR) continue;
         orc_ibox *b = &ib[((size_t)to * KR + k) * 2 + ph];
         b->len++;
@@ -708,8 +725,8 @@ static uint32_t event_trial(const orc_event_cfg *cfg, uint64_t trial, orc_node_s
             const int8_t v = (c0 > c1) ? 0 : (c1 > c0) ? 1 : 2;
             EV_SEND(k, v, 1u);
         } else {                                         /* node.ts:89-157 */
-            if (c0 > (int)F) { st[to].x = 0; st[to].decided = 1; decided |= 1ull << to; }
-            else if (c1 > (int)F) { st[to].x = 1; st[to].decided = 1; decided |= 1ull << to; }
+            if (c0 > (int)F) { st[to].x = 0; st[to].decided = 1; set_add(&decided, to); }
+            else if (c1 > (int)F) { st[to].x = 1; st[to].decided = 1; set_add(&decided, to); }
             else if (c0 + c1 > 0 && c0 > c1) st[to].x = 0;
             else if (c0 + c1 > 0 && c0 < c1) st[to].x = 1;
             else st[to].x = (int8_t)oracle_coin(cfg->seed, trial, cidx[to], k);
@@ -717,9 +734,9 @@ static uint32_t event_trial(const orc_event_cfg *cfg, uint64_t trial, orc_node_s
             uint8_t *pd = &pdone[(size_t)to * KR + k];
             if (!*pd) {
                 *pd = 1;
-                comp[k] |= 1ull << to;
-                while (cur < KR && (comp[cur] | killed) == all) {
-                    if ((decided | killed) == all) { halted = 1; R = cur; break; }
+                set_add(&comp[k], to);
+                while (cur < KR && set_union_full(&comp[cur], &killed, &all)) {
+                    if (set_union_full(&decided, &killed, &all)) { halted = 1; R = cur; break; }
                     if (cur >= cfg->k_max) { halted = 2; R = cur; break; }
                     ++cur;
                 }
@@ -729,25 +746,25 @@ static uint32_t event_trial(const orc_event_cfg *cfg, uint64_t trial, orc_node_s
         }
     }
 #undef EV_SEND
-    free(ib); free(comp); free(pdone); free(pool);
+    free(ib); free(comp); free(pdone); free(pool); free(crash_at);
     if (events_out) *events_out = e;
     /* outcome over the nodes still running */
     int any0 = 0, any1 = 0, anyq = 0, nlive = 0;
     for (uint32_t i = 0; i < N; ++i) {
-        if ((killed >> i) & 1ull) continue;
+        if (set_has(&killed, i)) continue;
         ++nlive;
         if (st[i].x == 0) any0 = 1; else if (st[i].x == 1) any1 = 1; else anyq = 1;
     }
     const uint32_t v = (nlive == 0 || anyq || (any0 && any1)) ? 2u : (any1 ? 1u : 0u);
     if (st_out) for (uint32_t i = 0; i < N; ++i) st_out[i] = st[i];
+    free(st); free(live_ids); free(cidx);
     if (halted == 1) return (uint32_t)((size_t)R * 3 + v) | (v == 2 ? 0x80000000u : 0u);
-    (void)H;
     return v;
 }
 
 /* Batch: hist as oracle_run_trials; events_out (optional) = total messages delivered. */
 int oracle_event_trials(const orc_event_cfg *cfg, uint64_t *hist, orc_node_state *node_out, uint64_t *events_out) {
-    if (cfg->k_max < 1 || cfg->N < 1 || cfg->N > 64) return -1;
+    if (cfg->k_max < 1 || cfg->N < 1 || cfg->N > ORC_EV_MAX_N) return -1;
     uint32_t f = 0;
     for (uint32_t i = 0; i < cfg->N; ++i) f += cfg->faulty[i] ? 1 : 0;
     if (f != cfg->F) return -2;                          /* launchNodes.ts:12-13 */

@@ -137,6 +137,8 @@ EVENT_HIST_CASES = [
     # (N, F, trials, k_max, crash_count, crash_window): event-level mode, first F nodes faulty
     (10, 4, 3000, 16, 0, 0), (10, 4, 3000, 16, 1, 150), (5, 1, 3000, 16, 1, 40), (16, 5, 1000, 16, 2, 400),
     (33, 10, 300, 16, 1, 2000), (64, 21, 100, 16, 3, 8000), (12, 4, 2000, 16, 0, 0), (7, 3, 2000, 12, 1, 60),
+    # N > 64 (r02): node-id bitsets of 4 words
+    (100, 30, 60, 16, 2, 20000), (128, 42, 40, 16, 3, 40000), (256, 85, 8, 16, 4, 150000), (130, 0, 40, 16, 0, 0),
 ]
 
 EVENT_STATE_CASES = [
