@@ -179,6 +179,17 @@ def other_configs(benor, torch, k_max, seed):
         out[name] = {"trials": T, "kernel_ms": ms, "node_rounds_per_s": nr / (ms * 1e-3),
                      "trials_per_s": T / (ms * 1e-3), "mean_rounds": rounds / T, "undecided_trials": undecided,
                      "roofline": roof}
+        if ms < 1.0:
+            # a launch this short is mostly ramp-up: also time 20x the trials for the steady state
+            h.zero_()
+            e0.record(stream)
+            plan.launch(2 * T, 20 * T, h.data_ptr(), stream.cuda_stream)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            ms20 = e0.elapsed_time(e1)
+            nr20, _ = node_rounds(h.cpu().numpy().astype(np.uint64), m, k_max)
+            out[name]["steady_state"] = {"trials": 20 * T, "kernel_ms": ms20, "node_rounds_per_s": nr20 / (ms20 * 1e-3),
+                                         "roofline_frac": roof["frac"] * (nr20 / ms20) / (nr / ms)}
     return out
 
 
