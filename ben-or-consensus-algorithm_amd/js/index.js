@@ -49,6 +49,8 @@ function randomSeed() {
 // Resolves once the round loop has run to completion (all live nodes decided,
 // or kMax rounds).  The reference resolves before consensus finishes and the
 // callers poll getNodesState; polling here sees the final states at once.
+// A second start on the same network rejects: the reference's round inboxes
+// outlive a run (node.ts:29-30), so it would not be a fresh consensus.
 async function startConsensus(N, options = {}) {
   if (N === 0) return;
   const seed = options.seed !== undefined ? BigInt(options.seed) : randomSeed();

@@ -116,6 +116,14 @@ it('Hidden Test - Finality is reached - One node', 'gpu', async () => {   // :45
   await b.stopConsensus(servers.length); await closeAllServers(servers);
 });
 
+it('A second startConsensus on one network is refused (inboxes persist, node.ts:29-30)', 'gpu', async () => {
+  const fa = [false, false, false, false, true];
+  const { servers, states } = await runToFinality(fa, [1, 1, 1, 0, 0]);
+  await assert.rejects(b.startConsensus(fa.length, { seed: 1n }), /libbenor error 8: consensus already started/);
+  assert.deepStrictEqual(await b.getNodesState(fa.length), states);
+  await b.stopConsensus(servers.length); await closeAllServers(servers);
+});
+
 it('runTrials histogram (N=10, F=4)', 'gpu', async () => {
   const h = await b.runTrials({ N: 10, F: 4, seed: 7n, kMax: 16, trialCount: 100000 });
   let total = 0n; for (const v of h) total += v;
