@@ -413,7 +413,7 @@ __global__ void __launch_bounds__(256) benor_random_kernel(KParams p) {
 }
 
 
-// ------------------------------------------------ event-level kernel (N <= 64)
+// ------------------------------------------------ event-level kernel (N <= 256)
 // message-granular simulation with the reference's literal
 // handler (node.ts:45-158), a seeded delivery order and mid-run GET /stop
 // (node.ts:191-194).  Definition: oracle/benor_oracle.c event_trial().  One
@@ -431,7 +431,7 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t &s) {
   return z ^ (z >> 31);
 }
 
-// Node-id bitsets of NW 64-bit words (N <= 64 NW, event mode N <= 256): a
+// Node-id bitsets of NW 64-bit words (N <= 64 NW; event mode N <= 256): a
 // dynamic word index is resolved by selects over the NW registers.
 template <int NW>
 __device__ __forceinline__ bool set_has(const uint64_t (&m)[NW], uint32_t i) {

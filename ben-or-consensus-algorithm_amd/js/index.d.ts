@@ -57,7 +57,7 @@ export interface TrialsConfig {
   kMax?: number;
   trialBegin?: bigint | number;
   trialCount?: bigint | number;
-  /** 0 lockstep (default), 1 random delivery (f <= F), 2 event level (N <= 64) */
+  /** 0 lockstep (default), 1 random delivery (f <= F), 2 event level (N <= 256) */
   mode?: 0 | 1 | 2;
   /** event mode: deliveries after which node i is stopped (null = never) */
   crashAt?: (number | null)[];

@@ -133,7 +133,7 @@ def other_configs(benor, torch, k_max, seed):
     kernel that runs it:
       * m > 32 (W kernel): popcount words per live node-round
         (bo_plan_popc_words_per_node_round) against the v_bcnt issue peak;
-      * m <= 32 (packed kernel, floor(32/m) trials per half wave): VALU issue.
+      * m <= 64 (lane kernel, one trial per lane): VALU issue.
         Its algorithmic lane-ops per live node-round are the tally popcounts
         (2 or 3 one-word counts), the proposal compare, the decision compare
         and the all-decided check (3), plus one Philox4x32-10 word per coin
@@ -163,7 +163,7 @@ def other_configs(benor, torch, k_max, seed):
         nr, rounds = node_rounds(hist, m, k_max)
         undecided = int(hist[0] + hist[1] + hist[2])
         words = plan.popc_words_per_node_round
-        if m > 32:
+        if m > 64:
             roof = {"bound": "valu (v_bcnt_u32_b32 issue)", "kernel": "lockstep W kernel",
                     "unit": "Tpopc/s", "popc_words_per_node_round": words,
                     "achieved": nr * words / (ms * 1e-3) / 1e12}

@@ -316,7 +316,7 @@ def test_random_delivery_rejects_too_many_faults():
         benor.TrialsPlan(10, 2, first_f(10, 3), mode=RD)
 
 
-# ------------------------------------------------- event-level mode (N <= 64)
+# ------------------------------------------------- event-level mode (N <= 256)
 EV = benor.BO_MODE_EVENT
 
 
