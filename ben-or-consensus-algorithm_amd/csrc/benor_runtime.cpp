@@ -219,7 +219,10 @@ int bo_consensus_start(bo_network *net, uint64_t seed, uint32_t k_max) {   // co
   const int rc = bo_run_trial_states(&cfg, 0, states.data(), &rounds);
   std::lock_guard<std::mutex> g(net->mu);
   net->in_flight = false;
-  if (rc) return rc;
+  if (rc) {
+    net->started = false;          // nothing ran: the start may be retried
+    return rc;
+  }
   // A GET /stop served while the kernel ran is ordered after the run: the
   // node keeps its final x / decided / k and stays killed.
   for (uint32_t i : active) {
