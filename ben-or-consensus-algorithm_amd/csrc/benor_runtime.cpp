@@ -230,6 +230,15 @@ int bo_consensus_start(bo_network *net, uint64_t seed, uint32_t k_max) {   // co
     net->st[i] = states[i];
     net->st[i].killed = killed;
   }
+  // The reference's auto-stop (node.ts:116-145): after its P-phase a node asks
+  // every node's /getState and, when every answer has `decided` truthy, sends
+  // /stop to all of them.  A faulty node answers decided: null (node.ts:24)
+  // and a node stopped before the run answers false, so it fires only when
+  // every node of the network decided -- then every node ends killed.
+  bool all_decided = true;
+  for (uint32_t i = 0; i < N; ++i) all_decided = all_decided && net->st[i].decided == 1;
+  if (all_decided)
+    for (uint32_t i = 0; i < N; ++i) net->st[i].killed = 1;
   return BO_OK;
 }
 

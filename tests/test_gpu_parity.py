@@ -128,6 +128,8 @@ def test_reference_known_answers_network_api(reference_cases):
                 ref = oracle.run_trials(N, sum(case["faulty"]), case["faulty"], seed=0x5EED, trial_begin=0,
                                         trial_count=1, k_max=benor.DEFAULT_K_MAX, initial_values=init,
                                         want_states=True).states
+                if all(r["decided"] is True for r in ref):          # auto-stop (node.ts:116-145)
+                    ref = [dict(r, killed=True) for r in ref]
                 assert states == ref
             else:
                 check_reference_expectations(case, benor.getNodesState(N), statuses)
@@ -163,23 +165,38 @@ def test_second_start_is_refused():
 
 def test_stop_during_run_is_kept():
     """A /stop served while the kernel runs (another thread) is ordered after
-    the run: the node keeps its final state and stays killed."""
+    the run: the node keeps its final state and stays killed.  N=2048 with
+    F=1024 never decides (m <= 2F), so the run lasts k_max = 1024 rounds."""
     import threading
 
-    N = 2048
-    init = [i % 2 for i in range(N)]               # m = 2048 even and tied: coins, several rounds
-    benor.launchNetwork(N, 0, init, [False] * N)
+    N, F, K = 2048, 1024, 1024
+    init = [i % 2 for i in range(N)]
+    benor.launchNetwork(N, F, init, [i < F for i in range(N)])
     net = benor._current
-    t = threading.Thread(target=lambda: benor.startConsensus(N, seed=9, k_max=64))
+    t = threading.Thread(target=lambda: benor.startConsensus(N, seed=9, k_max=K))
     t.start()
-    net.stop_node(5)
+    net.stop_node(1500)
     t.join()
     st = benor.getNodesState(N)
-    assert st[5]["killed"] is True and all(not s["killed"] for i, s in enumerate(st) if i != 5)
-    if st[5]["k"] == 0:        # the stop was served before the start: 2047 < N - F senders, a stall
-        assert all(s["k"] == 1 and s["decided"] is False for i, s in enumerate(st) if i != 5)
-    else:                      # served during the run: node 5 keeps its final state
-        assert st[5]["k"] == st[0]["k"] >= 2 and st[5]["decided"] == st[0]["decided"]
+    assert st[1500]["killed"] is True and all(not s["killed"] for i, s in enumerate(st) if i >= F and i != 1500)
+    if st[1500]["k"] == 0:     # served before the start: 1023 < N - F senders, a stall (node.ts:52)
+        assert all(s["k"] == 1 and s["decided"] is False for i, s in enumerate(st) if i >= F and i != 1500)
+    else:                      # served during (or after) the run: node 1500 keeps its final state
+        assert st[1500]["k"] == st[F]["k"] == K + 1 and st[1500]["decided"] is False
+
+
+def test_auto_stop_kills_every_node_when_all_decided():
+    """node.ts:116-145: once every node's /getState reports decided, every node
+    gets /stop.  Faulty nodes report decided: null, so it fires only at F = 0
+    (and without nodes stopped before the run)."""
+    benor.launchNetwork(5, 0, [1, 1, 0, 1, 1], [False] * 5)
+    benor.startConsensus(5, seed=4)
+    st = benor.getNodesState(5)
+    assert all(s["killed"] and s["decided"] and s["x"] == 1 and s["k"] == 2 for s in st)
+    assert all(benor.getStatus(i) == (500, "faulty") for i in range(5))
+    benor.launchNetwork(5, 1, [1, 1, 0, 1, 1], [False] * 4 + [True])
+    benor.startConsensus(5, seed=4)
+    assert not any(s["killed"] for s in benor.getNodesState(5)[:4])
 
 
 @pytest.mark.parametrize("N,F", [
