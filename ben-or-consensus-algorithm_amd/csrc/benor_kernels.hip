@@ -447,8 +447,14 @@ __device__ __forceinline__ void set_add(uint64_t (&m)[NW], uint32_t i) {
   for (int j = 0; j < NW; ++j) m[j] |= (i >> 6) == (uint32_t)j ? bit : 0ull;
 }
 
+// Messages are 16 bits: to | phase << 8 | x << 9 | (k & 3) << 11.  A message
+// to a live receiver is for a round in [cur, cur + 2] (cur = the lowest round
+// some running node has not completed: a receiver completes round k only
+// after all m of its round-k messages arrived, and no node is more than one
+// round ahead of cur), so k = cur + ((k - cur) & 3) recovers it; messages to
+// killed receivers are dropped unread.  Half the pool bytes of a 32-bit form.
 struct EvLane {
-  uint32_t *pool;      // [cap] messages: to | phase << 8 | x << 9 | k << 11
+  uint16_t *pool;      // [cap] messages
   uint32_t *ibox;      // [N][4][2] packed {c0, c1, len}, 10 bits each
   uint64_t *comp;      // [4][NW] completion masks, round k at k & 3
   uint64_t *crash;     // [N] sorted (event << 8 | node)
@@ -475,8 +481,8 @@ __global__ void __launch_bounds__(256) benor_event_kernel(KParams p) {
   const uint32_t cap = p.ev_cap;
   uint32_t *base = p.scratch + gid * p.ev_stride;
   EvLane L;
-  L.pool = base;
-  L.ibox = L.pool + cap;
+  L.pool = reinterpret_cast<uint16_t *>(base);
+  L.ibox = base + (((cap + 1u) >> 1) + 1u & ~1u);     // pool words, even (comp is 8-byte aligned)
   L.comp = reinterpret_cast<uint64_t *>(L.ibox + N * 8u);
   L.crash = L.comp + 4 * NW;
   L.xs = reinterpret_cast<int8_t *>(L.crash + N);
@@ -563,7 +569,7 @@ __global__ void __launch_bounds__(256) benor_event_kernel(KParams p) {
       if (set_has(killed, i)) continue;
       L.ks[i] = 1;
       const uint32_t body = ((uint32_t)(L.xs[i] & 3) << 9) | (1u << 11);
-      for (uint32_t to = 0; to < N; ++to) L.pool[len++] = to | body;
+      for (uint32_t to = 0; to < N; ++to) L.pool[len++] = (uint16_t)(to | body);
     }
     uint32_t cur = 1, R = 0, halted = 0;
     bool overflow = false;
@@ -592,7 +598,7 @@ __global__ void __launch_bounds__(256) benor_event_kernel(KParams p) {
       const uint32_t pick = (uint32_t)(((uint64_t)(uint32_t)(splitmix64(rng) >> 32) * (uint64_t)len) >> 32);
       const uint32_t msg = L.pool[pick];
       L.pool[pick] = L.pool[--len];
-      const uint32_t to = msg & 255u, ph = (msg >> 8) & 1u, k = msg >> 11;
+      const uint32_t to = msg & 255u, ph = (msg >> 8) & 1u, k = cur + (((msg >> 11) - cur) & 3u);
       const uint32_t x = (msg >> 9) & 3u;
       if (set_has(killed, to)) continue;               // node.ts:45
       uint32_t *bx = &L.ibox[(to * 4u + (k & 3u)) * 2u + ph];
@@ -606,7 +612,7 @@ __global__ void __launch_bounds__(256) benor_event_kernel(KParams p) {
       uint32_t body;
       if (ph == 0u) {                                  // node.ts:53-80
         const uint32_t v = c0 > c1 ? 0u : (c1 > c0 ? 1u : 2u);
-        body = (1u << 8) | (v << 9) | (k << 11);
+        body = (1u << 8) | (v << 9) | ((k & 3u) << 11);
       } else {                                         // node.ts:89-157
         int8_t nx;
         if (c0 > F) { nx = 0; set_add(decided, to); }
@@ -637,10 +643,10 @@ __global__ void __launch_bounds__(256) benor_event_kernel(KParams p) {
           ++cur;
         }
         if (halted) break;
-        body = ((uint32_t)(nx & 3) << 9) | ((k + 1u) << 11);
+        body = ((uint32_t)(nx & 3) << 9) | (((k + 1u) & 3u) << 11);
       }
       if (len + N > cap) { overflow = true; halted = 3; break; }
-      for (uint32_t dst = 0; dst < N; ++dst) L.pool[len++] = dst | body;
+      for (uint32_t dst = 0; dst < N; ++dst) L.pool[len++] = (uint16_t)(dst | body);
     }
     // ---- outcome over the nodes still running
     bool any0 = false, any1 = false, anyq = false;
@@ -713,7 +719,8 @@ void plan_geometry(KParams &p) {
     const uint32_t NW = p.N <= 64u ? 1u : 4u;
     p.ev_cap = 4u * p.N * p.N + 64u;
     // per-lane scratch (u32 words): pool, inbox window, comp[4][NW] (u64), crash[N] (u64), xs (i8), ks (i16)
-    p.ev_stride = p.ev_cap + p.N * 8u + 8u * NW + 2u * p.N + ((p.N + 3u) & ~3u) / 4u + (p.N + 1u) / 2u;
+    p.ev_stride = (((p.ev_cap + 1u) >> 1) + 1u & ~1u) + p.N * 8u + 8u * NW + 2u * p.N + ((p.N + 3u) & ~3u) / 4u +
+                  (p.N + 1u) / 2u;
     p.ev_stride = (p.ev_stride + 31u) & ~31u;
     return;
   }
