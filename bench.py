@@ -193,6 +193,26 @@ def other_configs(benor, torch, k_max, seed):
     return out
 
 
+def network_latency(benor, reps=200):
+    """BASELINE configs[0]: one start.ts-style network (N=5, F=1, node 4 faulty,
+    initial values [1,1,1,0,0], benorconsensus.test.ts:179-223) through the
+    reference's own calls -- launchNetwork + startConsensus + getNodesState --
+    on the GPU; median and p90 wall time over `reps` networks."""
+    times = []
+    for rep in range(reps + 5):
+        t0 = time.perf_counter()
+        benor.launchNetwork(5, 1, [1, 1, 1, 0, 0], [False, False, False, False, True])
+        benor.startConsensus(5, seed=rep)
+        states = benor.getNodesState(5)
+        dt = time.perf_counter() - t0
+        if rep >= 5:
+            times.append(dt * 1e3)
+    times.sort()
+    ok = all(s["decided"] and s["x"] == 1 and s["k"] <= 2 for s in states[:4])
+    return {"networks": reps, "median_ms": times[len(times) // 2], "p90_ms": times[int(len(times) * 0.9)],
+            "reference_assertions_hold": ok}
+
+
 def cpu_baseline(N, F, k_max, seed, budget_s):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
@@ -353,6 +373,7 @@ def main():
     }
     if world == 1 and not args.no_other_configs:
         out["other_configs"] = other_configs(benor, torch, k_max, args.seed)
+        out["other_configs"]["C1 N=5,F=1 network API"] = network_latency(benor)
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(N, F, k_max, args.seed, args.cpu_seconds)
     if rank == 0:

@@ -87,8 +87,10 @@ def test_bench_single_gpu_line():
     assert oc["C2 N=10,F=4"]["undecided_trials"] == 0 and oc["C2 N=10,F=4"]["mean_rounds"] > 1.3
     assert oc["C2 N=10,F=5 (F>N/2, no decision)"]["undecided_trials"] == 1_000_000
     assert oc["C3 N=256,F=85"]["mean_rounds"] == 1.0 and oc["C3 N=256,F=85"]["node_rounds_per_s"] > 0
-    for v in oc.values():
-        assert 0 < v["roofline"]["frac"] < 1.0 and v["roofline"]["bound"]
+    c1 = oc.pop("C1 N=5,F=1 network API")                 # configs[0]: one network, reference calls
+    assert c1["reference_assertions_hold"] and 0 < c1["median_ms"] < 50
+    for k, v in oc.items():
+        assert 0 < v["roofline"]["frac"] < 1.0 and v["roofline"]["bound"], k
     assert oc["C3 N=256,F=85"]["roofline"]["popc_words_per_node_round"] == 12
 
 
