@@ -320,6 +320,26 @@ def test_random_delivery_matches_oracle(N, F, f, trials):
     np.testing.assert_array_equal(got, ref.hist)
 
 
+# Bernoulli + fix-up sampler (k >= 64, 8k > m): every comparator width (a odd,
+# a = 2 mod 4, a = 4 mod 8, a = 8: 4, 3, 2, 1 stream words per mask word), every
+# index-field width class (b = 7..12: 4, 3 or 2 fields per word) and m = 2^b
+# (no range check) against the oracle.
+@pytest.mark.parametrize("m,q", [(256, 170), (200, 120), (512, 380), (700, 315), (1024, 683), (1500, 1003),
+                                 (3000, 1790), (2048, 1229), (256, 66)])
+def test_random_delivery_bernoulli_sampler_shapes(m, q):
+    ab = oracle.delivery_bernoulli(m, q)
+    assert ab is not None
+    f = 3 if m < 1024 else 0                       # crashed nodes: N = m + f, quorum q = N - F
+    N, F = m + f, m + f - q
+    fl = first_f(N, f)
+    seed = 0xBE5 ^ m ^ (q << 13)
+    T = 40 if m >= 1500 else 200
+    got = benor.TrialsPlan(N, F, fl, seed=seed, k_max=8, mode=RD).run(17, T)
+    ref = oracle.run_trials(N, F, fl, seed=seed, trial_begin=17, trial_count=T, k_max=8,
+                            mode=oracle.MODE_RANDOM_DELIVERY)
+    np.testing.assert_array_equal(got, ref.hist)
+
+
 def test_random_delivery_equals_lockstep_at_f_equals_F():
     for N, F in [(10, 4), (100, 33), (1024, 341)]:
         fl = first_f(N, F)
