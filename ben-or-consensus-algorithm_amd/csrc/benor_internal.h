@@ -21,6 +21,7 @@ constexpr int kWavesPerBlock = 4;          // 256-thread workgroups, one trial p
 constexpr uint32_t kMaxW = BO_MAX_N / 64;  // u64 words per bit plane at N = 4096
 constexpr int kMaxWSpecialised = 32;       // m <= 2048: fully unrolled W-specialised kernel
 constexpr uint32_t kMaxLaneM = 64;         // m <= 64: lane kernel, one trial per lane (benor_lane.h)
+constexpr uint32_t kMaxMfmaM = 1024;       // matrix-core kernel (benor_mfma.h): W <= 16, operands in registers
 constexpr uint32_t kMaxEventN = 256;       // event level: node ids in 8 bits of a message
 constexpr uint64_t kMaxTrialsPerLaunch = 1ull << 31;   // trial offsets within a launch fit 32 bits
 constexpr uint32_t kParamBytes = 32;       // LDS parameter block after the histogram (W kernel)
@@ -31,7 +32,8 @@ struct KParams {
   uint32_t W;               // u64 words per plane = ceil(m / 64) = receiver groups
   uint32_t G;               // receiver groups per tally block (template parameter); lane kernel: its KIND
   uint32_t nblocks;         // ceil(W / G)
-  uint32_t variant;         // 6: lane lockstep (m <= 64), 1: W-specialised lockstep (W <= kMaxWSpecialised = 32),
+  uint32_t variant;         // 7: matrix-core lockstep (benor_mfma.h; the W kernel serves its state launches),
+                            // 6: lane lockstep (m <= 64), 1: W-specialised lockstep (W <= kMaxWSpecialised = 32),
                             // 0: blocked lockstep, 2: random delivery, 4: event level
   uint32_t mode;            // BO_MODE_LOCKSTEP / BO_MODE_RANDOM_DELIVERY
   uint32_t q;               // quorum N - F (messages each receiver tallies per phase)
@@ -77,6 +79,10 @@ hipError_t launch_b(const KParams &p, int grid_blocks, hipStream_t stream);
 // Lane kernel (benor_lane.h), m = 1..kMaxLaneM, instantiated in benor_lane_*.hip.
 template <int MM>
 hipError_t launch_lane_m(const KParams &p, int grid_blocks, hipStream_t stream);
+
+// Matrix-core kernel (benor_mfma.h), W = 2..16, instantiated in benor_mfma_*.hip.
+template <int W>
+hipError_t launch_mfma(const KParams &p, int grid_blocks, hipStream_t stream);
 
 // Grid size that fills the current device for this configuration.
 int lockstep_grid(const KParams &p, int device);

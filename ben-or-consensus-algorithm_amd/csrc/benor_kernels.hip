@@ -33,6 +33,8 @@
 // and the host-side planning / dispatch.  The lockstep kernels live in
 // benor_lane.h (m <= 64, one trial per lane), benor_w_kernel.h (W kernel,
 // instantiated by benor_w_*.hip) and benor_blocked.hip (m > 2048).
+#include <stdlib.h>
+
 #include "benor_device.h"
 
 namespace benor {
@@ -759,6 +761,12 @@ void plan_geometry(KParams &p) {
     p.nblocks = 1;
     p.variant = 1;
     p.wave_bytes = (tb * WP + 2u * WP) * 8u;            // init ring, final x1 plane, decided bits
+    // Matrix-core kernel (benor_mfma.h) where every trial halts in round 1:
+    // all vote counts odd (m odd, even number of "?") and m > 2F.  Its state
+    // launches (network API) still run here, so the W kernel's LDS plan stays.
+    const bool sure = (p.m & 1u) && !(p.init_q & 1u) && p.m > 2u * p.F;
+    const char *no_mfma = getenv("BENOR_NO_MFMA");
+    if (sure && p.m <= kMaxMfmaM && !(no_mfma && no_mfma[0] == '1')) p.variant = 7;
   } else {
     // Blocks of G = ceil(W / nb) in 11..22 groups: the fewest padded groups nb * G,
     // ties to fewer blocks (larger G: more v_bcnt per LDS read and loop step, which
@@ -798,6 +806,13 @@ static hipError_t dispatch_lane(const KParams &p, int grid, hipStream_t s, std::
   return e;
 }
 
+template <int... Is>
+static hipError_t dispatch_mfma(const KParams &p, int grid, hipStream_t s, std::integer_sequence<int, Is...>) {
+  hipError_t e = hipErrorInvalidValue;
+  (void)((p.W == (uint32_t)(Is + 2) ? (e = launch_mfma<Is + 2>(p, grid, s), true) : false) || ...);
+  return e;
+}
+
 // W in 33..64: G in 11..22 (plan_geometry)
 template <int... Is>
 static hipError_t dispatch_b(const KParams &p, int grid, hipStream_t s, std::integer_sequence<int, Is...>) {
@@ -822,7 +837,10 @@ hipError_t launch_lockstep(const KParams &p, int grid, hipStream_t s) {
     hipLaunchKernelGGL(benor_random_kernel, dim3(grid), dim3(64 * kWavesPerBlock), p.lds_bytes, s, p);
     return hipGetLastError();
   }
-  if (p.variant == 1) return dispatch_w(p, grid, s, std::make_integer_sequence<int, kMaxWSpecialised - 1>{});   // W = 2..32
+  if (p.variant == 7 && !p.node_out && !p.rounds_out)
+    return dispatch_mfma(p, grid, s, std::make_integer_sequence<int, 15>{});                                  // W = 2..16
+  if (p.variant == 1 || p.variant == 7)
+    return dispatch_w(p, grid, s, std::make_integer_sequence<int, kMaxWSpecialised - 1>{});                    // W = 2..32
   return dispatch_b(p, grid, s, std::make_integer_sequence<int, 12>{});
 }
 
@@ -836,12 +854,14 @@ int lockstep_grid(const KParams &p, int device) {
     return (int)(grid < 1 ? 1 : grid);
   }
   // 8 workgroups (32 waves) per CU when registers and LDS allow it.
-  const uint64_t per_wave = p.variant == 6 ? 64u : 1u;   // trials a wave runs at once
+  const bool mfma = p.variant == 7 && !p.node_out && !p.rounds_out;
+  const uint64_t per_wave = p.variant == 6 ? 64u : (mfma ? 32u : 1u);   // trials a wave runs at once
   const uint64_t waves_needed = (p.trial_count + per_wave - 1u) / per_wave;
   const uint64_t blocks_needed = (waves_needed + kWavesPerBlock - 1) / kWavesPerBlock;
   uint64_t per_cu = 8;
-  if (p.lds_bytes > 0) {
-    const uint64_t lds_fit = (160u * 1024u) / p.lds_bytes;
+  const uint32_t lds = mfma ? p.hist_bytes : p.lds_bytes;   // the matrix-core kernel uses no wave slices
+  if (lds > 0) {
+    const uint64_t lds_fit = (160u * 1024u) / lds;
     if (lds_fit < per_cu) per_cu = lds_fit ? lds_fit : 1;
   }
   uint64_t grid = (uint64_t)cus * per_cu;

@@ -1,0 +1,256 @@
+// benor_mfma.h -- the matrix-core lockstep kernel: every receiver's inbox
+// count as a product on the gfx950 MFMA units, for the shapes whose trials all
+// halt in round 1 (node.ts:99-105 with every receiver deciding).
+//
+// Formulation.  In one phase, receiver r of trial t counts the votes of the
+// senders it hears: c[r][t] = sum_s D[r][s] * v[s][t], D the delivery matrix
+// (lockstep: every live sender reaches every live receiver, node.ts:45,171),
+// v the 0/1 vote plane.  With the trials of a wave as the N dimension this is
+// a (receivers x senders) . (senders x 32 trials) product, which
+// v_mfma_scale_f32_32x32x64_f8f6f4 computes on e2m1 (fp4) operands: 0 and 1
+// are exact e2m1 values, and the f32 accumulation of at most 4096 unit
+// products is exact, so every count -- and every decision -- is bit-identical
+// to the popcount kernels and the oracle.  One instruction does 32 x 32 x 64 =
+// 65536 receiver-sender terms; tools/mfma_probe.hip measured it at 16.1 ns per
+// SIMD under full load, 3.5x the v_bcnt_u32_b32 rate in terms per second.
+//
+// Eligible shapes (plan_geometry, variant 7): lockstep, 64 < m <= 1024, every
+// vote count odd (m odd, an even number of "?" initial values) and m > 2F.
+// Then no R-phase count ties (no "?" proposal, p0 = not p1) and every receiver
+// decides in the P-phase (decide_k's SURE case), so the trial halts in round 1
+// with x = the decided value: the whole round loop is R-phase, P-phase,
+// outcome.  That covers the headline N=1024/F=341 and configs[2] N=256/F=85.
+// The network API's single-trial launch (per-node state) stays on the W kernel.
+//
+// Layout (one wave = one tile of 32 trials, trial t0 + (lane & 31)):
+//  * B operand, R-phase: K chunk c holds senders 64c .. 64c+63; lane half
+//    h = lane >> 5 brings 32 of them (x-plane word 2c + h) as 32 e2m1 nibbles
+//    in 4 VGPRs (nibble i of VGPR v = sender bit 4i + v, value 1.0 = 0b0010).
+//  * A operand: all ones (e2m1 1.0): D restricted to live nodes.  The 32-row
+//    receiver tiles are identical products; an empty asm on A per tile keeps
+//    the compiler from merging them -- each receiver's count is executed.
+//  * C/D: accumulator register j of lane l is receiver row
+//    (j & 3) + 8 (j >> 2) + 4 (l >> 5) of the tile, trial column l & 31
+//    (cdna_hip_programming.md section 3) -- the same column as the B operand,
+//    so a tile's 16 results per lane become the next phase's B operand in
+//    place: no LDS, no lane exchange.
+//  * Thresholds ride in the accumulator's initial value: C = -(hi + 0.5) makes
+//    the sign bit of the result the proposal p0 = (c1 <= hi) (node.ts:63-69,
+//    c1 > c0 <=> c1 > M/2 for odd M), and C = -(F + 0.5) in the P-phase makes
+//    the sign bit "not d0" = (c0 <= F) (node.ts:99).  v_perm_b32 gathers four
+//    sign bits as bytes; two such words mask-merge into 8 e2m1 nibbles.
+//  * Padding: senders >= m are zero bits in the x words; receiver rows >= m in
+//    the last tile are masked out of the P-phase operand and the outcome.
+#pragma once
+
+#include "benor_device.h"
+
+namespace benor {
+
+typedef int mf_v4i __attribute__((ext_vector_type(4)));
+typedef int mf_v8i __attribute__((ext_vector_type(8)));
+typedef float mf_v16f __attribute__((ext_vector_type(16)));
+
+// 32 receivers x 32 trials x 64 senders, e2m1 operands, unit scales (E8M0 127 = 2^0).
+__device__ __forceinline__ mf_v16f mfma_count(mf_v4i a, mf_v4i b, mf_v16f c) {
+  const mf_v8i a8 = __builtin_shufflevector(a, a, 0, 1, 2, 3, -1, -1, -1, -1);   // fp4 reads the low 4 VGPRs
+  const mf_v8i b8 = __builtin_shufflevector(b, b, 0, 1, 2, 3, -1, -1, -1, -1);
+  return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, c, 4, 4, 0, 127, 0, 127);
+}
+
+// Sign bits of four f32 results as bytes (0xff where negative): v_perm_b32
+// selector 9 / 11 replicate bit 31 of the low / high source, 12 gives 0x00.
+__device__ __forceinline__ uint32_t sign_bytes(float e0, float e1, float e2, float e3) {
+  const uint32_t lo = __builtin_amdgcn_perm(__float_as_uint(e1), __float_as_uint(e0), 0x0C0C0B09u);
+  const uint32_t hi = __builtin_amdgcn_perm(__float_as_uint(e3), __float_as_uint(e2), 0x0B090C0Cu);
+  return lo | hi;
+}
+
+// Eight results -> eight e2m1 nibbles, 1.0 where the result is negative:
+// results 0..3 in the low nibbles of bytes 0..3, results 4..7 in the high ones.
+__device__ __forceinline__ uint32_t pack_signs8(const mf_v16f &acc, int base) {
+  const uint32_t s0 = sign_bytes(acc[base + 0], acc[base + 1], acc[base + 2], acc[base + 3]);
+  const uint32_t s1 = sign_bytes(acc[base + 4], acc[base + 5], acc[base + 6], acc[base + 7]);
+  return (s0 & 0x02020202u) | (s1 & 0x20202020u);
+}
+
+// 32 sender bits -> the 4 VGPRs of one lane's B fragment (nibble i of VGPR v
+// = bit 4i + v of the word, as e2m1 1.0).
+__device__ __forceinline__ mf_v4i expand_votes(uint32_t w) {
+  return mf_v4i{(int)((w << 1) & 0x22222222u), (int)(w & 0x22222222u), (int)((w >> 1) & 0x22222222u),
+                (int)((w >> 2) & 0x22222222u)};
+}
+
+template <int W, bool HALF>
+__global__ void __launch_bounds__(256) benor_mfma_sure_kernel(KParams p) {
+  constexpr int MT = 2 * W - (HALF ? 1 : 0);   // 32-receiver tiles (HALF: the last chunk holds <= 32 senders)
+  constexpr int KP = (MT + 1) / 2;             // P-phase K chunks: two tiles' results each
+  constexpr int NB = (W + 1) / 2;              // Philox init blocks per trial (128 senders each)
+  constexpr int NJ = (NB + 1) / 2;             // blocks per lane: half h draws blocks h, h + 2, ...
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t lane = threadIdx.x & 63u, h = lane >> 5;
+  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  uint32_t m = p.m, hist_len = p.hist_len, trial_count = (uint32_t)p.trial_count;
+  asm volatile("" : "+s"(m), "+s"(hist_len), "+s"(trial_count));
+
+  uint32_t *lhist = reinterpret_cast<uint32_t *>(smem);
+  uint32_t *keys = reinterpret_cast<uint32_t *>(smem + p.hist_bytes - kParamBytes);   // as the W kernel
+  for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) lhist[i] = 0u;
+  if (threadIdx.x == 0) {
+    keys[0] = (uint32_t)p.seed;
+    keys[1] = (uint32_t)(p.seed >> 32);
+    keys[2] = (uint32_t)p.trial_begin;
+    keys[3] = (uint32_t)(p.trial_begin >> 32);
+  }
+  __syncthreads();
+
+  const bool random_init = p.init_mode == BO_INIT_RANDOM;
+  // R-phase threshold: M = m - init_q binary votes (odd), p1 <=> c1 > M >> 1.
+  const float bias_r = -((float)((m - p.init_q) >> 1) + 0.5f);
+  const float bias_p = -((float)p.F + 0.5f);
+  mf_v16f cr, cp;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    cr[j] = bias_r;
+    cp[j] = bias_p;
+  }
+  // Receiver rows of the last tile that exist: nibble masks for its packed
+  // results, and a per-register bitmask for the outcome.
+  const uint32_t mrem = m - 32u * (uint32_t)(MT - 1);   // 1..32
+  uint32_t tail0 = 0, tail1 = 0, vbits = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const uint32_t row = (uint32_t)((j & 3) + 8 * (j >> 2)) + 4u * h;
+    if (row < mrem) {
+      vbits |= 1u << j;
+      const uint32_t nib = ((j & 4) ? 0x20u : 0x02u) << (8 * (j & 3));
+      if (j < 8) tail0 |= nib;
+      else tail1 |= nib;
+    }
+  }
+  // Fixed initial values: the same x1 words for every trial.
+  uint32_t fixed_w[W];
+  if (!random_init) {
+#pragma unroll
+    for (int c = 0; c < W; ++c) {
+      const uint4 q = p.init_plane[c];
+      fixed_w[c] = h ? q.w : q.z;
+    }
+  }
+  // Valid sender bits of this lane's word in the last chunk (word 2(W-1) + h).
+  const int last_bits = (int)m - 32 * (2 * (W - 1) + (int)h);
+  const uint32_t last_mask = last_bits >= 32 ? ~0u : (last_bits <= 0 ? 0u : ((1u << last_bits) - 1u));
+
+  mf_v4i ones = {0x22222222, 0x22222222, 0x22222222, 0x22222222};
+  uint32_t f_all = 0, f_1 = 0, f_2 = 0;   // halts, halts with some x = 1, with both values
+  const uint32_t ngroups = (trial_count + 31u) >> 5;
+  const uint32_t waves_total = gridDim.x * kWavesPerBlock;
+  for (uint32_t g = blockIdx.x * kWavesPerBlock + wv; g < ngroups; g += waves_total) {
+    const uint32_t t = (g << 5) + (lane & 31u);
+    const bool valid = t < trial_count;
+    // ---- /start (node.ts:167-188): this lane's x1 words 2c + h, c < W.
+    uint32_t xw[W];
+    if (random_init) {
+      const uint64_t trial = lds_u64(keys + 2) + t;
+      const uint2 kk = lds_keys(keys);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        // Block b = 2j + h: words 4b .. 4b+3 = chunks 2b, 2b+1.  Half h keeps
+        // words 4b + h, 4b + 2 + h and trades the other two with lane l ^ 32.
+        const uint4 r = philox4x32_10(kk.x, kk.y,
+                                      make_uint4((uint32_t)trial, (uint32_t)(trial >> 32), 2u * j + h, kStreamInit << 24));
+        const uint32_t keep_a = h ? r.y : r.x, keep_b = h ? r.w : r.z;
+        const uint32_t give_a = h ? r.x : r.y, give_b = h ? r.z : r.w;
+        const uint32_t recv_a = (uint32_t)__shfl_xor((int)give_a, 32);
+        const uint32_t recv_b = (uint32_t)__shfl_xor((int)give_b, 32);
+        if (4 * j + 0 < W) xw[4 * j + 0] = h ? recv_a : keep_a;
+        if (4 * j + 1 < W) xw[4 * j + 1] = h ? recv_b : keep_b;
+        if (4 * j + 2 < W) xw[4 * j + 2] = h ? keep_a : recv_a;
+        if (4 * j + 3 < W) xw[4 * j + 3] = h ? keep_b : recv_b;
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < W; ++c) xw[c] = fixed_w[c];
+    }
+    xw[W - 1] &= last_mask;
+    mf_v4i bx[W];
+#pragma unroll
+    for (int c = 0; c < W; ++c) bx[c] = expand_votes(xw[c]);
+
+    // ---- R-phase ("proposal phase", node.ts:46-82): every receiver tile
+    // counts the x plane; the sign of c1 - hi - 0.5 is its proposal p0.
+    uint32_t bp[MT][2];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      asm volatile("" : "+v"(ones));
+      mf_v16f acc = mfma_count(ones, bx[0], cr);
+#pragma unroll
+      for (int c = 1; c < W; ++c) acc = mfma_count(ones, bx[c], acc);
+      bp[i][0] = pack_signs8(acc, 0);
+      bp[i][1] = pack_signs8(acc, 8);
+      __builtin_amdgcn_sched_barrier(0);   // one tile's accumulator live at a time
+    }
+    bp[MT - 1][0] &= tail0;
+    bp[MT - 1][1] &= tail1;
+    mf_v4i pb[KP];
+#pragma unroll
+    for (int c = 0; c < KP; ++c)
+      pb[c] = mf_v4i{(int)bp[2 * c][0], (int)bp[2 * c][1], 2 * c + 1 < MT ? (int)bp[2 * c + 1][0] : 0,
+                     2 * c + 1 < MT ? (int)bp[2 * c + 1][1] : 0};
+
+    // ---- P-phase ("voting phase", node.ts:83-158): every receiver tile
+    // counts the p0 plane; the sign of c0 - F - 0.5 is "not d0" -> x = 1
+    // (every receiver decides: node.ts:99-105, m > 2F).
+    uint32_t s_or = 0u, s_and = ~0u;
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      asm volatile("" : "+v"(ones));
+      mf_v16f acc = mfma_count(ones, pb[0], cp);
+#pragma unroll
+      for (int c = 1; c < KP; ++c) acc = mfma_count(ones, pb[c], acc);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const uint32_t u = __float_as_uint(acc[j]);
+        if (i < MT - 1) {
+          s_or |= u;
+          s_and &= u;
+        } else {
+          const bool live = (vbits >> j) & 1u;
+          s_or |= live ? u : 0u;
+          s_and &= live ? u : ~0u;
+        }
+      }
+      asm volatile("" : "+v"(s_or), "+v"(s_and));   // fold tile by tile: one accumulator live
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // ---- outcome: bins 3 + v (R = 1), per trial column (lanes n, n + 32)
+    const uint64_t b1 = ballot(valid && (s_or >> 31));          // some receiver decided 1
+    const uint64_t b0 = ballot(valid && !(s_and >> 31));        // some receiver decided 0
+    const uint64_t bv = ballot(valid);
+    const uint32_t any1 = (uint32_t)b1 | (uint32_t)(b1 >> 32);
+    const uint32_t any0 = (uint32_t)b0 | (uint32_t)(b0 >> 32);
+    f_all += (uint32_t)__builtin_popcount((uint32_t)bv);
+    f_1 += (uint32_t)__builtin_popcount(any1);
+    f_2 += (uint32_t)__builtin_popcount(any1 & any0);
+  }
+
+  const uint32_t hc = lane == 3u ? f_all - f_1 : (lane == 4u ? f_1 - f_2 : (lane == 5u ? f_2 : 0u));
+  if (hc) atomicAdd(&lhist[lane], hc);
+  if (lane == 0 && f_2) atomicAdd(&lhist[hist_len - 1u], f_2);                   // disagreement counter
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) {
+    const uint32_t c = lhist[i];
+    if (c) atomicAdd(&p.hist[i], (unsigned long long)c);
+  }
+}
+
+template <int W>
+hipError_t launch_mfma(const KParams &p, int grid, hipStream_t s) {
+  if (p.m <= 64u * (uint32_t)(W - 1) + 32u)
+    hipLaunchKernelGGL((benor_mfma_sure_kernel<W, true>), dim3(grid), dim3(64 * kWavesPerBlock), p.hist_bytes, s, p);
+  else
+    hipLaunchKernelGGL((benor_mfma_sure_kernel<W, false>), dim3(grid), dim3(64 * kWavesPerBlock), p.hist_bytes, s, p);
+  return hipGetLastError();
+}
+
+}  // namespace benor
