@@ -39,6 +39,16 @@ BO_MODE_EVENT = 2
 NEVER = 0xFFFFFFFF             # crash_at entry: never stopped
 BO_INIT_RANDOM = 0
 BO_INIT_FIXED = 1
+BO_KERNEL_NONE = -1
+BO_KERNEL_BLOCKED = 0
+BO_KERNEL_W = 1
+BO_KERNEL_RANDOM = 2
+BO_KERNEL_EVENT = 4
+BO_KERNEL_LANE = 6
+BO_KERNEL_MFMA = 7
+KERNEL_NAMES = {BO_KERNEL_NONE: "none", BO_KERNEL_BLOCKED: "blocked popcount", BO_KERNEL_W: "W popcount",
+                BO_KERNEL_RANDOM: "random delivery", BO_KERNEL_EVENT: "event level", BO_KERNEL_LANE: "lane",
+                BO_KERNEL_MFMA: "matrix core (e2m1 MFMA)"}
 BO_MAX_N = 4096
 BO_MAX_K = 1024
 
@@ -51,7 +61,8 @@ EXPORTED_SYMBOLS = (
     "bo_get_state", "bo_status", "bo_network_size", "bo_network_destroy", "bo_hist_len",
     "bo_plan_create", "bo_plan_launch", "bo_plan_run", "bo_plan_popc_words_per_node_round",
     "bo_plan_live_nodes", "bo_plan_destroy", "bo_run_trials", "bo_run_trial_states",
-    "bo_popc_peak", "bo_last_error", "bo_abi_version", "bo_kernel_version",
+    "bo_popc_peak", "bo_last_error", "bo_abi_version", "bo_kernel_version", "bo_plan_kernel", "bo_kernel_for",
+    "bo_mfma_peak",
 )
 
 
@@ -117,6 +128,11 @@ def lib() -> ctypes.CDLL:
     L.bo_run_trial_states.argtypes = [P(TrialsCfgC), ctypes.c_uint64, P(NodeStateC), P(ctypes.c_uint32)]
     L.bo_popc_peak.argtypes = [ctypes.c_uint32]
     L.bo_popc_peak.restype = ctypes.c_double
+    L.bo_mfma_peak.argtypes = [ctypes.c_uint32]
+    L.bo_mfma_peak.restype = ctypes.c_double
+    L.bo_plan_kernel.argtypes = [ctypes.c_void_p]
+    L.bo_plan_kernel.restype = ctypes.c_int
+    L.bo_kernel_for.argtypes = [P(TrialsCfgC), P(ctypes.c_int)]
     L.bo_last_error.restype = ctypes.c_char_p
     L.bo_abi_version.restype = ctypes.c_int
     L.bo_kernel_version.restype = ctypes.c_char_p
@@ -275,6 +291,35 @@ def hist_len(k_max: int) -> int:
     return (k_max + 1) * 3 + 1
 
 
+def _trials_cfg(N, F, faulty=None, *, seed=0, k_max=DEFAULT_K_MAX, initial_values=None, mode=BO_MODE_LOCKSTEP,
+                crash_at=None, crash_count=0, crash_window=0):
+    """bo_trials_cfg for a shape, and the ctypes arrays it points into."""
+    if faulty is None:                       # start.ts:7-18 placement: the first F nodes
+        faulty = [i < F for i in range(N)]
+    fl = (ctypes.c_uint8 * max(1, N))(*[1 if v else 0 for v in faulty])
+    if initial_values is None:
+        init = (ctypes.c_int8 * max(1, N))()
+        init_mode = BO_INIT_RANDOM
+    else:
+        init = (ctypes.c_int8 * max(1, N))(*[_VAL[v] for v in initial_values])
+        init_mode = BO_INIT_FIXED
+    crash = _crash_array(N, crash_at)
+    cfg = TrialsCfgC(N, F, k_max, init_mode, mode, 0, seed,
+                     ctypes.cast(fl, ctypes.POINTER(ctypes.c_uint8)),
+                     ctypes.cast(init, ctypes.POINTER(ctypes.c_int8)),
+                     ctypes.cast(crash, ctypes.POINTER(ctypes.c_uint32)) if crash else None,
+                     crash_count, crash_window)
+    return cfg, (fl, init, crash)
+
+
+def kernel_for(N: int, F: int, faulty: Sequence[bool] | None = None, **kw) -> int:
+    """The kernel family a TrialsPlan of this shape runs (bo_kernel_for; host only)."""
+    cfg, _keep = _trials_cfg(N, F, faulty, **kw)
+    k = ctypes.c_int()
+    _check(lib().bo_kernel_for(ctypes.byref(cfg), ctypes.byref(k)))
+    return k.value
+
+
 class TrialsPlan:
     """Many independent trials of one (N, F, faulty) network shape on the
     current device (bo_plan_*)."""
@@ -283,23 +328,11 @@ class TrialsPlan:
                  k_max: int = DEFAULT_K_MAX, initial_values: Sequence | None = None,
                  mode: int = BO_MODE_LOCKSTEP, crash_at: Sequence | None = None, crash_count: int = 0,
                  crash_window: int = 0):
-        if faulty is None:                       # start.ts:7-18 placement: the first F nodes
-            faulty = [i < F for i in range(N)]
         self.N, self.F, self.k_max, self.seed = N, F, k_max, seed
-        self._fl = (ctypes.c_uint8 * max(1, N))(*[1 if v else 0 for v in faulty])
-        if initial_values is None:
-            self._init = (ctypes.c_int8 * max(1, N))()
-            init_mode = BO_INIT_RANDOM
-        else:
-            self._init = (ctypes.c_int8 * max(1, N))(*[_VAL[v] for v in initial_values])
-            init_mode = BO_INIT_FIXED
         self.mode = mode
-        self._crash = _crash_array(N, crash_at)
-        self._cfg = TrialsCfgC(N, F, k_max, init_mode, mode, 0, seed,
-                               ctypes.cast(self._fl, ctypes.POINTER(ctypes.c_uint8)),
-                               ctypes.cast(self._init, ctypes.POINTER(ctypes.c_int8)),
-                               ctypes.cast(self._crash, ctypes.POINTER(ctypes.c_uint32)) if self._crash else None,
-                               crash_count, crash_window)
+        self._cfg, self._keep = _trials_cfg(N, F, faulty, seed=seed, k_max=k_max, initial_values=initial_values,
+                                            mode=mode, crash_at=crash_at, crash_count=crash_count,
+                                            crash_window=crash_window)
         h = ctypes.c_void_p()
         _check(lib().bo_plan_create(ctypes.byref(self._cfg), ctypes.byref(h)))
         self._h = h
@@ -317,6 +350,11 @@ class TrialsPlan:
     @property
     def popc_words_per_node_round(self) -> int:
         return lib().bo_plan_popc_words_per_node_round(self._h)
+
+    @property
+    def kernel(self) -> int:
+        """BO_KERNEL_* family of this plan's batch launches (bo_plan_kernel)."""
+        return lib().bo_plan_kernel(self._h)
 
     @property
     def hist_len(self) -> int:
@@ -366,3 +404,8 @@ def kernel_version() -> str:
 
 def popc_peak(iters: int = 20) -> float:
     return float(lib().bo_popc_peak(iters))
+
+
+def mfma_peak(iters: int = 10) -> float:
+    """Measured e2m1 32x32x64 MFMA multiply-adds per second (bo_mfma_peak)."""
+    return float(lib().bo_mfma_peak(iters))

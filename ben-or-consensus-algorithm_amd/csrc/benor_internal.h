@@ -87,6 +87,9 @@ hipError_t launch_mfma(const KParams &p, int grid_blocks, hipStream_t stream);
 // Grid size that fills the current device for this configuration.
 int lockstep_grid(const KParams &p, int device);
 
+// Matrix-core microbenchmark: e2m1 32x32x64 multiply-adds executed per launch.
+hipError_t launch_mfma_peak(float *sink, int grid_blocks, int iters, hipStream_t stream, double *terms_per_launch);
+
 // v_bcnt_u32_b32 microbenchmark: popcount words executed per launch.
 hipError_t launch_popc_peak(uint32_t *sink, int grid_blocks, int iters, hipStream_t stream,
                             double *words_per_launch);

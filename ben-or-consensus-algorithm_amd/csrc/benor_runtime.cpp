@@ -243,9 +243,11 @@ int bo_consensus_start(bo_network *net, uint64_t seed, uint32_t k_max) {   // co
 }
 
 // -------------------------------------------------------------- batch API
-int bo_plan_create(const bo_trials_cfg *cfg, bo_plan **out) {
-  if (!cfg || !out) return fail(BO_ERR_INVALID_ARGUMENT, "NULL argument");
-  *out = nullptr;
+// Validation and kernel planning of a trial configuration, host only: the
+// live-node map, the fixed-init plane and the KParams shape (no device fields).
+static int plan_host(const bo_trials_cfg *cfg, std::vector<uint32_t> &live, std::vector<uint4> &plane,
+                     benor::KParams &kp) {
+  if (!cfg) return fail(BO_ERR_INVALID_ARGUMENT, "NULL argument");
   if (cfg->N < 1 || cfg->N > BO_MAX_N) return fail(BO_ERR_UNSUPPORTED, "N must be in [1, 4096]");
   if (cfg->k_max < 1 || cfg->k_max > BO_MAX_K) return fail(BO_ERR_INVALID_ARGUMENT, "k_max must be in [1, 1024]");
   if (cfg->mode != BO_MODE_LOCKSTEP && cfg->mode != BO_MODE_RANDOM_DELIVERY && cfg->mode != BO_MODE_EVENT)
@@ -264,20 +266,11 @@ int bo_plan_create(const bo_trials_cfg *cfg, bo_plan **out) {
     return fail(BO_ERR_FAULTY_COUNT, "faultyList doesnt have F faulties");
   if (cfg->mode == BO_MODE_RANDOM_DELIVERY && f > cfg->F)
     return fail(BO_ERR_FAULTY_COUNT, "random delivery needs at most F crash-faulty nodes");
-  int dev = 0;
-  int rc = check_device(&dev);
-  if (rc) return rc;
-
-  auto *pl = new bo_plan();
-  pl->cfg = *cfg;
-  pl->cfg.faulty = nullptr;
-  pl->cfg.init = nullptr;
-  pl->cfg.crash_at = nullptr;
-  pl->device = dev;
+  live.clear();
   for (uint32_t i = 0; i < cfg->N; ++i)
-    if (!cfg->faulty[i]) pl->live_ids.push_back(i);
-  const uint32_t m = (uint32_t)pl->live_ids.size();
-  benor::KParams &kp = pl->kp;
+    if (!cfg->faulty[i]) live.push_back(i);
+  const uint32_t m = (uint32_t)live.size();
+  kp = benor::KParams{};
   kp.N = cfg->N;
   kp.F = cfg->F;
   kp.m = m;
@@ -291,20 +284,60 @@ int bo_plan_create(const bo_trials_cfg *cfg, bo_plan **out) {
   kp.crash_window = cfg->crash_window;
   for (uint32_t i = 0; i < cfg->N && i < 4u * 64u; ++i)
     if (cfg->faulty[i]) kp.faulty_mask[i >> 6] |= 1ull << (i & 63u);
-  if (m > 0) {
-    benor::plan_geometry(kp);
-    std::vector<uint4> plane(kp.W, make_uint4(0, 0, 0, 0));
-    if (cfg->init_mode == BO_INIT_FIXED) {
-      for (uint32_t c = 0; c < m; ++c) {
-        const int8_t v = cfg->init[pl->live_ids[c]];
-        if (v < 0 || v > 2) { delete pl; return fail(BO_ERR_INVALID_ARGUMENT, "initial value must be 0, 1 or '?'(2)"); }
-        const uint32_t w = c >> 6, b = c & 63u;
-        uint32_t *r = reinterpret_cast<uint32_t *>(&plane[w]);
-        if (v == 0) r[b >> 5] |= 1u << (b & 31u);
-        if (v == 1) r[2 + (b >> 5)] |= 1u << (b & 31u);
-        if (v == 2) ++kp.init_q;
-      }
+  if (m == 0) {
+    kp.hist_len = bo_hist_len(cfg->k_max);
+    return BO_OK;
+  }
+  plane.assign(kp.W, make_uint4(0, 0, 0, 0));
+  if (cfg->init_mode == BO_INIT_FIXED) {
+    for (uint32_t c = 0; c < m; ++c) {
+      const int8_t v = cfg->init[live[c]];
+      if (v < 0 || v > 2) return fail(BO_ERR_INVALID_ARGUMENT, "initial value must be 0, 1 or '?'(2)");
+      const uint32_t w = c >> 6, b = c & 63u;
+      uint32_t *r = reinterpret_cast<uint32_t *>(&plane[w]);
+      if (v == 0) r[b >> 5] |= 1u << (b & 31u);
+      if (v == 1) r[2 + (b >> 5)] |= 1u << (b & 31u);
+      if (v == 2) ++kp.init_q;
     }
+  }
+  benor::plan_geometry(kp);   // after init_q: the kernel choice depends on the round-1 vote parity
+  return BO_OK;
+}
+
+int bo_kernel_for(const bo_trials_cfg *cfg, int *kernel_out) {
+  if (!kernel_out) return fail(BO_ERR_INVALID_ARGUMENT, "NULL argument");
+  std::vector<uint32_t> live;
+  std::vector<uint4> plane;
+  benor::KParams kp;
+  const int rc = plan_host(cfg, live, plane, kp);
+  if (rc) return rc;
+  *kernel_out = kp.m == 0 ? BO_KERNEL_NONE : (int)kp.variant;
+  return BO_OK;
+}
+
+int bo_plan_create(const bo_trials_cfg *cfg, bo_plan **out) {
+  if (!cfg || !out) return fail(BO_ERR_INVALID_ARGUMENT, "NULL argument");
+  *out = nullptr;
+  std::vector<uint32_t> live;
+  std::vector<uint4> plane;
+  benor::KParams kp0;
+  int rc = plan_host(cfg, live, plane, kp0);
+  if (rc) return rc;
+  int dev = 0;
+  rc = check_device(&dev);
+  if (rc) return rc;
+
+  auto *pl = new bo_plan();
+  pl->cfg = *cfg;
+  pl->cfg.faulty = nullptr;
+  pl->cfg.init = nullptr;
+  pl->cfg.crash_at = nullptr;
+  pl->device = dev;
+  pl->live_ids = live;
+  pl->kp = kp0;
+  benor::KParams &kp = pl->kp;
+  const uint32_t m = kp.m;
+  if (m > 0) {
     hipError_t e = hipMalloc(&pl->d_live, sizeof(uint32_t) * m);
     if (e == hipSuccess) e = hipMalloc(&pl->d_init, sizeof(uint4) * kp.W);
     if (e == hipSuccess) e = hipMemcpy(pl->d_live, pl->live_ids.data(), sizeof(uint32_t) * m, hipMemcpyHostToDevice);
@@ -345,8 +378,6 @@ int bo_plan_create(const bo_trials_cfg *cfg, bo_plan **out) {
       kp.crash_at = pl->d_crash;
       kp.scratch = pl->d_scratch;
     }
-  } else {
-    kp.hist_len = bo_hist_len(cfg->k_max);
   }
   *out = pl;
   return BO_OK;
@@ -363,6 +394,11 @@ void bo_plan_destroy(bo_plan *pl) {
 }
 
 uint32_t bo_plan_live_nodes(const bo_plan *pl) { return pl ? pl->kp.m : 0u; }
+
+int bo_plan_kernel(const bo_plan *pl) {
+  if (!pl) return -BO_ERR_INVALID_ARGUMENT;
+  return pl->kp.m == 0 ? BO_KERNEL_NONE : (int)pl->kp.variant;
+}
 
 // Lockstep: the R-phase needs c1 only (c0 = M - c1, M binary votes,
 // node.ts:52,56-62).  The P-phase needs c0 and c1 (node.ts:92-98) unless M
@@ -498,6 +534,32 @@ double bo_popc_peak(uint32_t iters) {
   (void)hipFree(sink);
   if (ms <= 0) return 0.0;
   return words * iters / (ms * 1e-3);
+}
+
+double bo_mfma_peak(uint32_t iters) {
+  if (check_device(nullptr)) return 0.0;
+  int dev = 0, cus = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  float *sink = nullptr;
+  const int grid = cus * 2, inner = 4096;   // 2 waves per SIMD
+  if (hipMalloc(&sink, sizeof(float) * grid) != hipSuccess) return 0.0;
+  double terms = 0;
+  hipEvent_t a, b;
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  (void)benor::launch_mfma_peak(sink, grid, inner, nullptr, &terms);   // warm-up
+  (void)hipEventRecord(a, nullptr);
+  for (uint32_t i = 0; i < iters; ++i) (void)benor::launch_mfma_peak(sink, grid, inner, nullptr, &terms);
+  (void)hipEventRecord(b, nullptr);
+  (void)hipEventSynchronize(b);
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, a, b);
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  (void)hipFree(sink);
+  if (ms <= 0) return 0.0;
+  return terms * iters / (ms * 1e-3);
 }
 
 }  // extern "C"

@@ -55,6 +55,26 @@ METRIC = "simulated node-rounds/sec at N=1024,F=341, 1–8 GPUs; % of INT/popcou
 # lane-op issue peak for 4-cycle VALU ops (v_cmp, SGPR-operand ops, Philox's
 # v_mad_u64_u32 / v_bitop3_b32), used for the small-network kernel.
 SPEC_PEAK_POPC = 256 * 4 * 16 * 2.4e9
+# Matrix-core kernel (BO_KERNEL_MFMA): v_mfma_scale_f32_32x32x64_f8f6f4 on e2m1
+# operands; dense FP4 peak ~10 PFLOP/s (MI355X_MICROARCH.md, Matrix cores),
+# i.e. 5e15 receiver-sender multiply-adds per second.
+SPEC_PEAK_MFMA_FLOPS = 10e15
+
+
+def mfma_roofline(m, node_rounds_per_launch, kernel_s):
+    """Roofline of the matrix-core kernel.  Algorithmic work: every live
+    receiver sums the votes of the m live senders in the R- and the P-phase,
+    2m multiply-adds (4m FLOP) per live node-round.  Executed work adds the
+    padding of 32-row receiver tiles and 64-sender chunks: per 32-trial tile
+    ceil(m/32) * (ceil(m/64) + ceil(ceil(m/32)/2)) instructions of 65536
+    multiply-adds (benor_mfma.h)."""
+    mt, w = (m + 31) // 32, (m + 63) // 64
+    executed_per_trial = mt * (w + (mt + 1) // 2) * 65536 / 32
+    flops = node_rounds_per_launch * 4 * m / kernel_s
+    return {"bound": "mfma (v_mfma_scale_f32_32x32x64_f8f6f4, e2m1 0/1 operands)", "kernel": "matrix core",
+            "achieved": flops / 1e12, "peak": SPEC_PEAK_MFMA_FLOPS / 1e12, "unit": "TFLOP/s",
+            "frac": flops / SPEC_PEAK_MFMA_FLOPS, "terms_per_node_round": 2 * m,
+            "padding_efficiency": 2 * m * m / executed_per_trial}
 
 
 def parse(argv=None):
@@ -163,7 +183,9 @@ def other_configs(benor, torch, k_max, seed):
         nr, rounds = node_rounds(hist, m, k_max)
         undecided = int(hist[0] + hist[1] + hist[2])
         words = plan.popc_words_per_node_round
-        if m > 64:
+        if plan.kernel == benor.BO_KERNEL_MFMA:
+            roof = mfma_roofline(m, nr, ms * 1e-3)
+        elif m > 64:
             roof = {"bound": "valu (v_bcnt_u32_b32 issue)", "kernel": "lockstep W kernel",
                     "unit": "Tpopc/s", "popc_words_per_node_round": words,
                     "achieved": nr * words / (ms * 1e-3) / 1e12}
@@ -174,8 +196,9 @@ def other_configs(benor, torch, k_max, seed):
             roof = {"bound": "valu issue (tallies, compares, Philox coins)", "kernel": "lane (one trial per lane)",
                     "unit": "T lane-ops/s", "lane_ops_per_node_round": ops / max(nr, 1),
                     "achieved": ops / (ms * 1e-3) / 1e12}
-        roof["peak"] = SPEC_PEAK_POPC / 1e12
-        roof["frac"] = roof["achieved"] / roof["peak"]
+        if plan.kernel != benor.BO_KERNEL_MFMA:
+            roof["peak"] = SPEC_PEAK_POPC / 1e12
+            roof["frac"] = roof["achieved"] / roof["peak"]
         out[name] = {"trials": T, "kernel_ms": ms, "node_rounds_per_s": nr / (ms * 1e-3),
                      "trials_per_s": T / (ms * 1e-3), "mean_rounds": rounds / T, "undecided_trials": undecided,
                      "roofline": roof}
@@ -337,10 +360,11 @@ def main():
     my_trials = rank_range(args.scaling, args.warmup, rank, world, T)[1]
     per_launch_nr = live_nr * my_trials / total_trials
     avg_kernel_s = float(np.mean(kern_ms)) * 1e-3
+    mfma = plan.kernel == benor.BO_KERNEL_MFMA
     achieved = per_launch_nr * words_per_nr / avg_kernel_s
     peak_measured = None
     if not args.no_peak_probe:
-        peak_measured = benor.popc_peak(10)
+        peak_measured = 2 * benor.mfma_peak(10) if mfma else benor.popc_peak(10)
     kver = benor.kernel_version()
     traffic = None
     tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -356,17 +380,22 @@ def main():
     out = {
         "metric": METRIC, "value": value, "unit": "node-rounds/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True,
-        "scaling": args.scaling, "vs_baseline": None, "dtype": "u32", "data": "synthetic (Philox initial values)",
+        "scaling": args.scaling, "vs_baseline": None,
+        "dtype": "e2m1 0/1 votes -> f32 exact integer counts" if mfma else "u32",
+        "data": "synthetic (Philox initial values)",
         "config": {"workload": f"N={N},F={F} lockstep crash faults, {T} trials {per_gpu} per step, k_max={k_max}",
                    "N": N, "F": F, "live_nodes": m, "trials_per_step": total_trials // args.steps,
                    "trials_per_gpu_per_step": my_trials, "k_max": k_max,
                    "parallelism": f"dp{world} (trial-id sharding, RCCL histogram all-reduce)"},
         "dist": {"world": world, "backend": backend if distributed else None, "ranks_merged_per_step":
                  merged_ranks / args.steps, "hist_sha256": hist_digest(h)},
-        "roofline": {"bound": "valu (v_bcnt_u32_b32 issue)", "achieved": achieved / 1e12, "peak": SPEC_PEAK_POPC / 1e12,
-                     "unit": "Tpopc/s", "frac": achieved / SPEC_PEAK_POPC, "traffic": traffic,
-                     "kernel_ms": float(np.mean(kern_ms)), "popc_words_per_node_round": words_per_nr,
-                     "peak_probe": (peak_measured / 1e12) if peak_measured else None, "kernel_version": kver},
+        "roofline": dict(
+            (mfma_roofline(m, per_launch_nr, avg_kernel_s) if mfma else
+             {"bound": "valu (v_bcnt_u32_b32 issue)", "achieved": achieved / 1e12, "peak": SPEC_PEAK_POPC / 1e12,
+              "unit": "Tpopc/s", "frac": achieved / SPEC_PEAK_POPC, "popc_words_per_node_round": words_per_nr}),
+            traffic=traffic, kernel_ms=float(np.mean(kern_ms)),
+            peak_probe=(peak_measured / 1e12) if peak_measured else None, kernel_version=kver,
+            kernel=benor.KERNEL_NAMES.get(plan.kernel, str(plan.kernel))),
         "all_node_rounds_per_s": rounds * N / elapsed,
         "trials_per_s": total_trials / elapsed,
         "agreement_violations": int(h[-1]),

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define BENOR_ABI_VERSION 3
+#define BENOR_ABI_VERSION 4
 
 /* Return codes.  The first two are the reference's two launch errors. */
 enum {
@@ -169,6 +169,29 @@ int bo_plan_run(bo_plan *plan, uint64_t trial_begin, uint64_t trial_count, uint6
 uint64_t bo_plan_popc_words_per_node_round(const bo_plan *plan);
 uint32_t bo_plan_live_nodes(const bo_plan *plan);
 
+/* Kernel families.  BO_KERNEL_MFMA counts inboxes on the matrix cores
+ * (e2m1 operands, exact f32 sums): lockstep, 64 < m <= 1024, m odd, an even
+ * number of "?" initial values and m > 2F -- every trial halts in round 1.
+ * Its roofline unit is receiver-sender terms, 2m per live node-round. */
+enum {
+  BO_KERNEL_NONE = -1, /* no live node: outcomes need no kernel */
+  BO_KERNEL_BLOCKED = 0,
+  BO_KERNEL_W = 1,
+  BO_KERNEL_RANDOM = 2,
+  BO_KERNEL_EVENT = 4,
+  BO_KERNEL_LANE = 6,
+  BO_KERNEL_MFMA = 7
+};
+
+/* The kernel family bo_plan_launch runs for this plan.  (The per-node-state
+ * launch behind the network API runs the W kernel for an MFMA shape.) */
+int bo_plan_kernel(const bo_plan *plan);
+
+/* The same choice for a configuration, made on the host (no device needed):
+ * *kernel_out = BO_KERNEL_* (BO_KERNEL_NONE for no live node).  Returns
+ * bo_plan_create's validation error for an invalid cfg. */
+int bo_kernel_for(const bo_trials_cfg *cfg, int *kernel_out);
+
 void bo_plan_destroy(bo_plan *plan);
 
 /* One-shot convenience: create plan, run trial ids [trial_begin, +trial_count), destroy. */
@@ -184,6 +207,11 @@ int bo_run_trial_states(const bo_trials_cfg *cfg, uint64_t trial, bo_node_state 
 /* Time the v_bcnt_u32_b32 peak microbenchmark: returns popcount words/s
  * measured on the current device over `iters` launches (0 on error). */
 double bo_popc_peak(uint32_t iters);
+
+/* Time the matrix-core peak microbenchmark (v_mfma_scale_f32_32x32x64_f8f6f4,
+ * e2m1 operands, the BO_KERNEL_MFMA instruction): multiply-adds per second on
+ * the current device over `iters` launches (0 on error). */
+double bo_mfma_peak(uint32_t iters);
 
 /* Message of the last error on this thread ("" if none). */
 const char *bo_last_error(void);

@@ -91,7 +91,10 @@ def test_bench_single_gpu_line():
     assert c1["reference_assertions_hold"] and 0 < c1["median_ms"] < 50
     for k, v in oc.items():
         assert 0 < v["roofline"]["frac"] < 1.0 and v["roofline"]["bound"], k
-    assert oc["C3 N=256,F=85"]["roofline"]["popc_words_per_node_round"] == 12
+    # N=256/F=85 and the headline run on the matrix cores (m odd, m > 2F): 2m terms per node-round
+    assert oc["C3 N=256,F=85"]["roofline"]["terms_per_node_round"] == 2 * 171
+    assert d["roofline"]["kernel"].startswith("matrix core") and d["roofline"]["terms_per_node_round"] == 2 * 683
+    assert d["roofline"]["unit"] == "TFLOP/s" and 0.9 < d["roofline"]["padding_efficiency"] <= 1.0
 
 
 @pytest.mark.gpu

@@ -1,0 +1,155 @@
+"""The matrix-core lockstep kernel (csrc/benor_mfma.h, BO_KERNEL_MFMA).
+
+CPU: the host-side kernel choice (bo_kernel_for) -- which shapes go to the
+matrix cores and which stay on the popcount / lane / random / event kernels.
+GPU: bit-exact histograms against the oracle on every chunk count W = 2..16
+(both tile parities), with fixed initial values and "?" inputs, partial
+32-trial tiles and 64-bit trial offsets; equality with the popcount W kernel
+(BENOR_NO_MFMA=1) over 10^6 trials; the network API (per-node state) on an
+MFMA shape; and the init_q parity regression (the kernel choice depends on
+the number of "?" initial values, which must be known before planning).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import benor
+import oracle
+
+
+def first_f(N, F):
+    return [i < F for i in range(N)]
+
+
+def mfma_shapes():
+    """(N, F) with f = F crashed, m = N - F odd, m > 2F, 64 < m <= 1024: both
+    tile parities (m - 64 (W-1) <= 32 or > 32) for every W, F at the bound and
+    below it."""
+    out = []
+    for W in range(2, 17):
+        for off in (1, 33, 63):
+            m = 64 * (W - 1) + off
+            for F in ((m - 1) // 2, (m - 1) // 5):
+                out.append((m + F, F))
+    return out
+
+
+def plan(N, F, mfma=True, **kw):
+    if mfma:
+        os.environ.pop("BENOR_NO_MFMA", None)
+    else:
+        os.environ["BENOR_NO_MFMA"] = "1"
+    try:
+        return benor.TrialsPlan(N, F, **kw)
+    finally:
+        os.environ.pop("BENOR_NO_MFMA", None)
+
+
+# ------------------------------------------------------------------ CPU
+def test_kernel_choice():
+    K = benor
+    assert K.kernel_for(1024, 341) == K.BO_KERNEL_MFMA            # headline: m = 683 odd, m > 2F
+    assert K.kernel_for(256, 85) == K.BO_KERNEL_MFMA              # configs[2]
+    for N, F in mfma_shapes():
+        assert K.kernel_for(N, F) == K.BO_KERNEL_MFMA, (N, F)
+    assert K.kernel_for(1000, 300) == K.BO_KERNEL_W               # m = 700 even: ties, coins, more rounds
+    assert K.kernel_for(1025, 512) == K.BO_KERNEL_W               # m = 513 odd but m <= 2F: undecided receivers
+    assert K.kernel_for(1537, 512) == K.BO_KERNEL_W               # m = 1025 > kMaxMfmaM
+    assert K.kernel_for(4096, 1365) == K.BO_KERNEL_BLOCKED        # m = 2731
+    assert K.kernel_for(10, 4) == K.BO_KERNEL_LANE                # m <= 64
+    assert K.kernel_for(96, 31) == K.BO_KERNEL_MFMA               # m = 65
+    assert K.kernel_for(1024, 341, mode=K.BO_MODE_RANDOM_DELIVERY) == K.BO_KERNEL_RANDOM
+    assert K.kernel_for(10, 4, mode=K.BO_MODE_EVENT) == K.BO_KERNEL_EVENT
+    assert K.kernel_for(3, 3) == K.BO_KERNEL_NONE
+    # fixed initial values: an odd number of "?" makes round 1's vote count even
+    vals = [1] * 1024
+    vals[500] = "?"
+    assert K.kernel_for(1024, 341, initial_values=vals) == K.BO_KERNEL_W
+    vals[501] = "?"
+    assert K.kernel_for(1024, 341, initial_values=vals) == K.BO_KERNEL_MFMA
+    os.environ["BENOR_NO_MFMA"] = "1"
+    try:
+        assert K.kernel_for(1024, 341) == K.BO_KERNEL_W
+    finally:
+        os.environ.pop("BENOR_NO_MFMA", None)
+
+
+def test_kernel_choice_validates_like_plan_create():
+    with pytest.raises(benor.Error, match="faultyList doesnt have F faulties"):
+        benor.kernel_for(10, 4, [True] * 3 + [False] * 7)
+    with pytest.raises(RuntimeError, match="k_max"):
+        benor.kernel_for(10, 4, k_max=0)
+
+
+# ------------------------------------------------------------------ GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,F", mfma_shapes())
+def test_mfma_matches_oracle(N, F):
+    seed = (N * 7919 + F) & 0xFFFF
+    T = 977 + (N % 64)                       # partial last tile of 32 trials
+    begin = (1 << 33) + N                    # 64-bit trial ids
+    p = plan(N, F, seed=seed, k_max=8)
+    assert p.kernel == benor.BO_KERNEL_MFMA
+    got = p.run(begin, T)
+    ref = oracle.run_trials(N, F, first_f(N, F), seed=seed, trial_begin=begin, trial_count=T, k_max=8)
+    np.testing.assert_array_equal(got, ref.hist)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,F,q", [(300, 99, 2), (1024, 341, 10), (129, 40, 4), (97, 32, 0), (1001, 300, 6)])
+def test_mfma_fixed_init_matches_oracle(N, F, q):
+    rng = np.random.default_rng(N + q)
+    vals = [int(v) for v in rng.integers(0, 2, N)]
+    for j in rng.choice(np.arange(F, N), q, replace=False):
+        vals[j] = "?"
+    p = plan(N, F, seed=11, k_max=8, initial_values=vals)
+    assert p.kernel == benor.BO_KERNEL_MFMA
+    got = p.run(3, 333)
+    ref = oracle.run_trials(N, F, first_f(N, F), seed=11, trial_begin=3, trial_count=333, k_max=8,
+                            initial_values=vals)
+    np.testing.assert_array_equal(got, ref.hist)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,F", [(1024, 341), (256, 85), (97, 32), (1500, 477)])
+def test_mfma_equals_popcount_kernel(N, F):
+    a = plan(N, F, True, seed=99, k_max=16)
+    b = plan(N, F, False, seed=99, k_max=16)
+    assert a.kernel == benor.BO_KERNEL_MFMA and b.kernel == benor.BO_KERNEL_W
+    np.testing.assert_array_equal(a.run(5, 1_000_003), b.run(5, 1_000_003))
+
+
+@pytest.mark.gpu
+def test_mfma_shape_network_api_per_node_state():
+    """The per-node-state launch of an MFMA shape runs the W kernel; its
+    states equal the oracle's (one trial)."""
+    N, F = 256, 85
+    rounds, st = benor.run_trial_states(N, F, first_f(N, F), seed=5, trial=42, k_max=8)
+    ref = oracle.run_trials(N, F, first_f(N, F), seed=5, trial_begin=42, trial_count=1, k_max=8, want_states=True)
+    assert rounds == 1
+    assert st == ref.states
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,F,init", [
+    (7, 0, [1, 0, "?", 1, 0, 1, 0]),                  # lane kernel: m = 7, one "?": round-1 M = 6 (ties)
+    (11, 2, [1, 1, 0, "?", 0, 1, 0, 1, 1, 0, "?"]),    # m = 9, two "?" on live nodes
+    (301, 100, None),                                 # W kernel: m = 201, one "?" below
+])
+def test_question_mark_parity_picks_the_right_kernel(N, F, init):
+    if init is None:
+        rng = np.random.default_rng(0)
+        init = [int(v) for v in rng.integers(0, 2, N)]
+        init[150] = "?"
+    p = benor.TrialsPlan(N, F, seed=21, k_max=12, initial_values=init)
+    got = p.run(0, 4000)
+    ref = oracle.run_trials(N, F, first_f(N, F), seed=21, trial_begin=0, trial_count=4000, k_max=12,
+                            initial_values=init)
+    np.testing.assert_array_equal(got, ref.hist)
+
+
+@pytest.mark.gpu
+def test_mfma_peak_probe():
+    peak = benor.mfma_peak(3)
+    assert 1e15 < peak < 6e15                # dense e2m1 spec: 5e15 multiply-adds/s
