@@ -22,12 +22,15 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def pmc_per_dispatch(path, kernel_sub="lockstep"):
+KERNELS = ("lockstep", "mfma")   # the bench shape's kernel: popcount (lockstep_*) or matrix core (mfma_*)
+
+
+def pmc_per_dispatch(path, kernel_subs=KERNELS):
     agg = defaultdict(list)
     meta = {}
     for f in glob.glob(os.path.join(path, "pmc*", "*counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            if kernel_sub not in r["Kernel_Name"]:
+            if not any(k in r["Kernel_Name"] for k in kernel_subs):
                 continue
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
             meta = {k: r[k] for k in ("Kernel_Name", "Grid_Size", "Workgroup_Size", "LDS_Block_Size",
@@ -47,12 +50,22 @@ def main(tag, trials, N=1024, F=341):
         shutil.copy(probe, os.path.join(dst, f"{tag}_valu_probe.txt"))
     c, meta = pmc_per_dispatch(src)
     m = N - F
-    lines = [f"# Profile {tag}: lockstep kernel, N={N}, F={F}, {trials} trials per launch", ""]
+    kname = meta.get("Kernel_Name", "")
+    lines = [f"# Profile {tag}: {'matrix-core' if 'mfma' in kname else 'lockstep'} kernel, N={N}, F={F}, "
+             f"{trials} trials per launch", ""]
     lines += [f"- {k}: {v}" for k, v in meta.items()]
     lines += ["", "| counter | per launch | per trial |", "|---|---|---|"]
     for k in sorted(c):
         lines.append(f"| {k} | {c[k]:.6g} | {c[k] / trials:.4g} |")
-    if "SQ_INSTS_VALU" in c:
+    if "SQ_INSTS_VALU" in c and "mfma" in kname:
+        W = (m + 63) // 64
+        MT = 2 * W - (1 if m <= 64 * (W - 1) + 32 else 0)   # 32-receiver tiles (benor_mfma.h)
+        KP = (MT + 1) // 2
+        mfma = (MT * W + MT * KP) / 32.0                      # R-phase MT x W, P-phase MT x KP, per 32 trials
+        lines += ["", f"- MFMA (32x32x64 e2m1) per trial: {mfma:.2f} (R-phase {MT}x{W} + P-phase {MT}x{KP} per 32 trials)",
+                  f"- VALU instructions per trial (SQ_INSTS_VALU, MFMA included): {c['SQ_INSTS_VALU'] / trials:.1f} "
+                  f"(non-MFMA: {c['SQ_INSTS_VALU'] / trials - mfma:.1f})"]
+    elif "SQ_INSTS_VALU" in c:
         W = (m + 63) // 64
         per = 4 if m % 2 else 6   # words per receiver group / W: 2 (R-phase c1) + 2 (P c1, odd m) or 4 (P c0, c1)
         bcnt = per * W * W
@@ -61,7 +74,7 @@ def main(tag, trials, N=1024, F=341):
                   f"(non-v_bcnt: {c['SQ_INSTS_VALU'] / trials - bcnt:.1f})"]
     if "GRBM_GUI_ACTIVE" in c and stats:
         for r in csv.DictReader(open(stats[0])):
-            if "lockstep" in r["Name"]:
+            if any(k in r["Name"] for k in KERNELS):
                 avg_ns = float(r["AverageNs"])
                 lines.append(f"- kernel-trace average duration (bench launches): {avg_ns / 1e6:.3f} ms")
     hbm = None
@@ -87,5 +100,7 @@ def main(tag, trials, N=1024, F=341):
 
 
 if __name__ == "__main__":
+    if len(sys.argv) < 2 or sys.argv[1].startswith("-"):
+        sys.exit(__doc__ + "\nusage: python tools/summarize_profile.py <tag> [trials] [N F]")
     main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 10_000_000,
          *(int(x) for x in sys.argv[3:5]))
