@@ -270,6 +270,16 @@ __device__ __forceinline__ uint32_t sgpr32(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
 }
 
+// Global trial id of launch offset t from the W kernel's parameter block
+// ([2,3] trial_begin, [4,5] trial list or 0): trial_begin + t, or in
+// trial-list mode trial_begin + list[t] (the matrix-core kernel's deferred
+// trials, benor_mfma.h).
+__device__ __forceinline__ uint64_t trial_id(const uint32_t *keys, uint32_t t) {
+  const uint64_t lp = lds_u64(keys + 4);
+  if (lp) t = reinterpret_cast<const uint32_t *>(lp)[t];
+  return lds_u64(keys + 2) + t;
+}
+
 // Per-lane select by a wave lane mask: lanes whose bit is set take `b`
 // (one v_cndmask_b32 with an SGPR mask; a C select would shift the mask by
 // the lane id in 64-bit VALU ops).

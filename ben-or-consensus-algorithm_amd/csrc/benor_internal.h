@@ -30,9 +30,10 @@ struct KParams {
   uint32_t N, F;            // network size, fault parameter
   uint32_t m;               // live (non-crashed) nodes = senders = receivers
   uint32_t W;               // u64 words per plane = ceil(m / 64) = receiver groups
-  uint32_t G;               // receiver groups per tally block (template parameter); lane kernel: its KIND
+  uint32_t G;               // receiver groups per tally block (template parameter); lane and matrix-core kernels: KIND
   uint32_t nblocks;         // ceil(W / G)
-  uint32_t variant;         // 7: matrix-core lockstep (benor_mfma.h; the W kernel serves its state launches),
+  uint32_t variant;         // 7: matrix-core lockstep, round 1 (benor_mfma.h; the W kernel serves its state
+                            //    launches and the trials it defers),
                             // 6: lane lockstep (m <= 64), 1: W-specialised lockstep (W <= kMaxWSpecialised = 32),
                             // 0: blocked lockstep, 2: random delivery, 4: event level
   uint32_t mode;            // BO_MODE_LOCKSTEP / BO_MODE_RANDOM_DELIVERY
@@ -40,6 +41,7 @@ struct KParams {
   uint32_t k_max;
   uint32_t init_mode;       // BO_INIT_RANDOM / BO_INIT_FIXED
   uint32_t init_q;          // live nodes whose fixed initial value is "?" (0 for random init)
+  uint32_t init_tie;        // fixed init: as many live 0s as 1s (every trial ties in round 1)
   uint32_t hist_len;        // (k_max + 1) * 3 + 1
   uint32_t lds_bytes;       // dynamic LDS per workgroup
   uint32_t wave_bytes;      // per-wave LDS region
@@ -63,7 +65,18 @@ struct KParams {
   uint32_t rd_a, rd_b;
   uint64_t ev_lanes;               // lanes the scratch buffer holds
   uint32_t *scratch;               // [ev_lanes][ev_stride]
+  // matrix-core kernel (variant 7, KIND > 0): trials that do not halt in round 1,
+  // as offsets within the launch: wave w writes them to its segment
+  // defer_seg[w * defer_seg_cap ...], then appends them to defer_list
+  // (capacity trial_count) at defer_len
+  uint32_t *defer_list, *defer_len, *defer_seg;
+  uint32_t defer_seg_cap;
+  // W kernel trial-list mode: run the trials trial_begin + trial_list[i],
+  // i < min(*trial_list_len, trial_count), instead of a contiguous range
+  const uint32_t *trial_list, *trial_list_len;
 };
+
+constexpr uint64_t kDeferChunk = 1ull << 22;   // trials per matrix-core launch when trials can be deferred
 
 // Pick the tally block size G and fill nblocks / LDS sizes.
 void plan_geometry(KParams &p);

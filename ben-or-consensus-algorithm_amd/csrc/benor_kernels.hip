@@ -761,12 +761,19 @@ void plan_geometry(KParams &p) {
     p.nblocks = 1;
     p.variant = 1;
     p.wave_bytes = (tb * WP + 2u * WP) * 8u;            // init ring, final x1 plane, decided bits
-    // Matrix-core kernel (benor_mfma.h) where every trial halts in round 1:
-    // all vote counts odd (m odd, even number of "?") and m > 2F.  Its state
-    // launches (network API) still run here, so the W kernel's LDS plan stays.
+    // Matrix-core kernel (benor_mfma.h) for round 1 wherever a trial can halt
+    // there (m > F; not a fixed start whose round 1 ties for every trial).
+    // KIND 0: all vote counts odd (m odd, even number of "?") and m > 2F --
+    // every trial halts in round 1; KIND 1: m > 2F; KIND 2: F < m <= 2F.
+    // Trials that do not halt in round 1 go to this W kernel (trial-list
+    // mode), as do the state launches (network API), so its LDS plan stays.
     const bool sure = (p.m & 1u) && !(p.init_q & 1u) && p.m > 2u * p.F;
+    const bool can_halt = p.m > p.F && !(p.init_mode == BO_INIT_FIXED && p.init_tie);
     const char *no_mfma = getenv("BENOR_NO_MFMA");
-    if (sure && p.m <= kMaxMfmaM && !(no_mfma && no_mfma[0] == '1')) p.variant = 7;
+    if (can_halt && p.m <= kMaxMfmaM && !(no_mfma && no_mfma[0] == '1')) {
+      p.variant = 7;
+      p.G = sure ? 0u : (p.m > 2u * p.F ? 1u : 2u);
+    }
   } else {
     // Blocks of G = ceil(W / nb) in 11..22 groups: the fewest padded groups nb * G,
     // ties to fewer blocks (larger G: more v_bcnt per LDS read and loop step, which

@@ -1,6 +1,7 @@
 // benor_mfma.h -- the matrix-core lockstep kernel: every receiver's inbox
-// count as a product on the gfx950 MFMA units, for the shapes whose trials all
-// halt in round 1 (node.ts:99-105 with every receiver deciding).
+// count as a product on the gfx950 MFMA units.  It runs round 1 of every
+// trial; a trial that does not halt there is handed to the popcount W kernel
+// (trial-list mode), which re-runs it from round 1.
 //
 // Formulation.  In one phase, receiver r of trial t counts the votes of the
 // senders it hears: c[r][t] = sum_s D[r][s] * v[s][t], D the delivery matrix
@@ -14,12 +15,20 @@
 // 65536 receiver-sender terms; tools/mfma_probe.hip measured it at 16.1 ns per
 // SIMD under full load, 3.5x the v_bcnt_u32_b32 rate in terms per second.
 //
-// Eligible shapes (plan_geometry, variant 7): lockstep, 64 < m <= 1024, every
-// vote count odd (m odd, an even number of "?" initial values) and m > 2F.
-// Then no R-phase count ties (no "?" proposal, p0 = not p1) and every receiver
-// decides in the P-phase (decide_k's SURE case), so the trial halts in round 1
-// with x = the decided value: the whole round loop is R-phase, P-phase,
-// outcome.  That covers the headline N=1024/F=341 and configs[2] N=256/F=85.
+// Eligible shapes (plan_geometry, variant 7): lockstep, 64 < m <= 1024, m > F
+// (decisions possible).  KIND (KParams::G):
+//  0 "sure": every vote count odd (m odd, an even number of "?" initial
+//    values) and m > 2F.  No R-phase count ties (no "?" proposal) and every
+//    receiver decides in the P-phase (decide_k's SURE case), so every trial
+//    halts in round 1 with x = the decided value.  The headline N=1024/F=341
+//    and configs[2] N=256/F=85.
+//  1 m > 2F, ties possible (even vote count): a trial halts in round 1 unless
+//    some receiver proposed "?" (node.ts:63-69) -- then it is deferred.
+//  2 F < m <= 2F: a receiver decides only when one value has more than F
+//    votes; a trial with a "?" proposal or an undecided receiver is deferred.
+// Deferred trials (their offsets within the launch) are appended to
+// p.defer_list; the host runs them through the W kernel in trial-list mode
+// right after, on the same stream, so every trial is counted exactly once.
 // The network API's single-trial launch (per-node state) stays on the W kernel.
 //
 // Layout (one wave = one tile of 32 trials, trial t0 + (lane & 31)):
@@ -34,13 +43,17 @@
 //    (cdna_hip_programming.md section 3) -- the same column as the B operand,
 //    so a tile's 16 results per lane become the next phase's B operand in
 //    place: no LDS, no lane exchange.
-//  * Thresholds ride in the accumulator's initial value: C = -(hi + 0.5) makes
-//    the sign bit of the result the proposal p0 = (c1 <= hi) (node.ts:63-69,
-//    c1 > c0 <=> c1 > M/2 for odd M), and C = -(F + 0.5) in the P-phase makes
-//    the sign bit "not d0" = (c0 <= F) (node.ts:99).  v_perm_b32 gathers four
-//    sign bits as bytes; two such words mask-merge into 8 e2m1 nibbles.
+//  * R-phase: A carries scale 2^4, C = -8M (M binary votes), so the result is
+//    8 (c1 - c0) (node.ts:63-69): positive for p1, negative for p0, zero for a
+//    tie ("?").  v_cvt_scalef32_pk_fp4_f32 packs two results per byte and
+//    saturates: the proposal plane is +6 / -6 / 0 nibbles, the next product's
+//    B operand in place.
+//  * P-phase: S = sum of proposals = 6 (n1 - n0); with no "?" among them
+//    n0 + n1 = m, so thresholds on S are thresholds on c0 = n0 and c1 = n1
+//    (node.ts:99-105), again carried by C.
 //  * Padding: senders >= m are zero bits in the x words; receiver rows >= m in
-//    the last tile are masked out of the P-phase operand and the outcome.
+//    the last tile are masked out of the P-phase operand and start their
+//    P-phase accumulator at NaN, which the min / max reductions skip.
 #pragma once
 
 #include "benor_device.h"
@@ -51,11 +64,13 @@ typedef int mf_v4i __attribute__((ext_vector_type(4)));
 typedef int mf_v8i __attribute__((ext_vector_type(8)));
 typedef float mf_v16f __attribute__((ext_vector_type(16)));
 
-// 32 receivers x 32 trials x 64 senders, e2m1 operands, unit scales (E8M0 127 = 2^0).
+// 32 receivers x 32 trials x 64 senders, e2m1 operands; A scaled by 2^SA
+// (E8M0 127 + SA), B unit scale.
+template <int SA = 0>
 __device__ __forceinline__ mf_v16f mfma_count(mf_v4i a, mf_v4i b, mf_v16f c) {
   const mf_v8i a8 = __builtin_shufflevector(a, a, 0, 1, 2, 3, -1, -1, -1, -1);   // fp4 reads the low 4 VGPRs
   const mf_v8i b8 = __builtin_shufflevector(b, b, 0, 1, 2, 3, -1, -1, -1, -1);
-  return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, c, 4, 4, 0, 127, 0, 127);
+  return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, c, 4, 4, 0, 127 + SA, 0, 127);
 }
 
 // Sign bits of four f32 results as bytes (0xff where negative): v_perm_b32
@@ -74,6 +89,20 @@ __device__ __forceinline__ uint32_t pack_signs8(const mf_v16f &acc, int base) {
   return (s0 & 0x02020202u) | (s1 & 0x20202020u);
 }
 
+// Eight results -> eight e2m1 nibbles: v_cvt_scalef32_pk_fp4_f32 rounds two
+// f32 into byte k (src0 in bits 8k..8k+3, src1 in 8k+4..8k+7) and saturates:
+// every R-phase result has |value| >= 8 (the count is scaled by 16 through
+// the MFMA's A scale and the threshold sits half a vote from it), so each
+// nibble is exactly +6.0 (0x7, proposal 1) or -6.0 (0xF, proposal 0).
+__device__ __forceinline__ uint32_t pack_fp4_8(const mf_v16f &acc, int base) {
+  uint32_t r = 0u;
+  r = __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(r, acc[base + 0], acc[base + 1], 1.0f, 0);
+  r = __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(r, acc[base + 2], acc[base + 3], 1.0f, 1);
+  r = __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(r, acc[base + 4], acc[base + 5], 1.0f, 2);
+  r = __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(r, acc[base + 6], acc[base + 7], 1.0f, 3);
+  return r;
+}
+
 // 32 sender bits -> the 4 VGPRs of one lane's B fragment (nibble i of VGPR v
 // = bit 4i + v of the word, as e2m1 1.0).
 __device__ __forceinline__ mf_v4i expand_votes(uint32_t w) {
@@ -81,12 +110,13 @@ __device__ __forceinline__ mf_v4i expand_votes(uint32_t w) {
                 (int)((w >> 2) & 0x22222222u)};
 }
 
-template <int W, bool HALF>
-__global__ void __launch_bounds__(256) benor_mfma_sure_kernel(KParams p) {
+template <int W, bool HALF, int KIND>
+__global__ void __launch_bounds__(256) benor_mfma_kernel(KParams p) {
   constexpr int MT = 2 * W - (HALF ? 1 : 0);   // 32-receiver tiles (HALF: the last chunk holds <= 32 senders)
   constexpr int KP = (MT + 1) / 2;             // P-phase K chunks: two tiles' results each
   constexpr int NB = (W + 1) / 2;              // Philox init blocks per trial (128 senders each)
   constexpr int NJ = (NB + 1) / 2;             // blocks per lane: half h draws blocks h, h + 2, ...
+  constexpr bool SURE = KIND == 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t lane = threadIdx.x & 63u, h = lane >> 5;
   const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -105,28 +135,41 @@ __global__ void __launch_bounds__(256) benor_mfma_sure_kernel(KParams p) {
   __syncthreads();
 
   const bool random_init = p.init_mode == BO_INIT_RANDOM;
-  // R-phase threshold: M = m - init_q binary votes (odd), p1 <=> c1 > M >> 1.
-  const float bias_r = -((float)((m - p.init_q) >> 1) + 0.5f);
-  const float bias_p = -((float)p.F + 0.5f);
-  mf_v16f cr, cp;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    cr[j] = bias_r;
-    cp[j] = bias_p;
-  }
+  const uint32_t M1 = m - p.init_q;            // round-1 binary votes ("?" inputs excluded)
+  // KIND 0: every vote count odd, so p0 = (c1 <= M1 >> 1) is the sign of
+  //   c1 - (M1 >> 1) - 0.5 (node.ts:63-69), packed by v_perm as a 0/1 plane
+  //   (e2m1 1.0 = p0); in the P-phase the sign of c0 - F - 0.5 is "not d0"
+  //   = x1 (node.ts:99-105: every receiver decides, m > 2F).
+  // KIND 1, 2: the count enters scaled by 16 (A scale 2^4) against C = -8 M1,
+  //   so acc = 8 (c1 - c0): >= 8 for p1, <= -8 for p0, 0 for "?"; the fp4
+  //   conversion saturates it to +6 / -6 and keeps 0.  The P-phase sum is
+  //   S = 6 (n1 - n0), and where no proposal is "?", n0 + n1 = m:
+  //   KIND 1 (m > 2F): acc = S - 6 (m - 2F) + 3 = 12 (F - c0) + 3, negative
+  //     exactly when c0 > F (decide 0, node.ts:99-101), else c1 >= m - F > F
+  //     (decide 1, node.ts:102-105);
+  //   KIND 2 (F < m <= 2F): acc = S = 6 (c1 - c0); the receiver decides iff
+  //     |c1 - c0| > 2F - m (c0 > F or c1 > F), for the value of the sign.
+  const float bias_r = SURE ? -((float)(M1 >> 1) + 0.5f) : -8.0f * (float)M1;
+  const float bias_p = SURE ? -((float)p.F + 0.5f) : (KIND == 2 ? 0.0f : 3.0f - 6.0f * (float)(m - 2u * p.F));
+  const float dec_thr = 6.0f * (float)(2u * p.F - m) + 3.0f;   // KIND 2: |acc| > dec_thr <=> decided
+  mf_v16f cr, cp, cp_tail;
   // Receiver rows of the last tile that exist: nibble masks for its packed
-  // results, and a per-register bitmask for the outcome.
+  // R-phase results; KIND 0 masks its P-phase results per register (vbits),
+  // KIND 1, 2 start them from NaN where no receiver exists, which
+  // v_min3_f32 / v_max3_f32 skip (IEEE minNum / maxNum).
   const uint32_t mrem = m - 32u * (uint32_t)(MT - 1);   // 1..32
   uint32_t tail0 = 0, tail1 = 0, vbits = 0;
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
     const uint32_t row = (uint32_t)((j & 3) + 8 * (j >> 2)) + 4u * h;
-    if (row < mrem) {
-      vbits |= 1u << j;
-      const uint32_t nib = ((j & 4) ? 0x20u : 0x02u) << (8 * (j & 3));
-      if (j < 8) tail0 |= nib;
-      else tail1 |= nib;
-    }
+    const bool live = row < mrem;
+    cr[j] = bias_r;
+    cp[j] = bias_p;
+    cp_tail[j] = live ? bias_p : __builtin_nanf("");
+    if (live) vbits |= 1u << j;
+    const uint32_t nib = !live ? 0u : SURE ? ((j & 4) ? 0x20u : 0x02u) << (8 * (j & 3)) : 0xFu << (4 * (j & 7));
+    if (j < 8) tail0 |= nib;
+    else tail1 |= nib;
   }
   // Fixed initial values: the same x1 words for every trial.
   uint32_t fixed_w[W];
@@ -145,7 +188,13 @@ __global__ void __launch_bounds__(256) benor_mfma_sure_kernel(KParams p) {
   uint32_t f_all = 0, f_1 = 0, f_2 = 0;   // halts, halts with some x = 1, with both values
   const uint32_t ngroups = (trial_count + 31u) >> 5;
   const uint32_t waves_total = gridDim.x * kWavesPerBlock;
-  for (uint32_t g = blockIdx.x * kWavesPerBlock + wv; g < ngroups; g += waves_total) {
+  const uint32_t wave_id = blockIdx.x * kWavesPerBlock + wv;
+  // KIND > 0: this wave's deferred trials go to its own segment of
+  // p.defer_seg (no contended atomics in the loop), copied to the compact
+  // list p.defer_list at the end with one atomic per wave.
+  uint32_t n_def = 0;
+  uint32_t *seg = SURE ? nullptr : p.defer_seg + (size_t)wave_id * p.defer_seg_cap;
+  for (uint32_t g = wave_id; g < ngroups; g += waves_total) {
     const uint32_t t = (g << 5) + (lane & 31u);
     const bool valid = t < trial_count;
     // ---- /start (node.ts:167-188): this lane's x1 words 2c + h, c < W.
@@ -178,16 +227,29 @@ __global__ void __launch_bounds__(256) benor_mfma_sure_kernel(KParams p) {
     for (int c = 0; c < W; ++c) bx[c] = expand_votes(xw[c]);
 
     // ---- R-phase ("proposal phase", node.ts:46-82): every receiver tile
-    // counts the x plane; the sign of c1 - hi - 0.5 is its proposal p0.
+    // counts the x plane; the packed result is its proposal.
     uint32_t bp[MT][2];
+    uint32_t qz = 0u;                          // KIND > 0: a live receiver proposed "?"
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
       asm volatile("" : "+v"(ones));
-      mf_v16f acc = mfma_count(ones, bx[0], cr);
+      if constexpr (SURE) {
+        mf_v16f acc = mfma_count(ones, bx[0], cr);
 #pragma unroll
-      for (int c = 1; c < W; ++c) acc = mfma_count(ones, bx[c], acc);
-      bp[i][0] = pack_signs8(acc, 0);
-      bp[i][1] = pack_signs8(acc, 8);
+        for (int c = 1; c < W; ++c) acc = mfma_count(ones, bx[c], acc);
+        bp[i][0] = pack_signs8(acc, 0);
+        bp[i][1] = pack_signs8(acc, 8);
+      } else {
+        mf_v16f acc = mfma_count<4>(ones, bx[0], cr);
+#pragma unroll
+        for (int c = 1; c < W; ++c) acc = mfma_count<4>(ones, bx[c], acc);
+        bp[i][0] = pack_fp4_8(acc, 0);
+        bp[i][1] = pack_fp4_8(acc, 8);
+        // a "?" nibble is 0: bit 1 clear (+6 = 0x7, -6 = 0xF)
+        const uint32_t l0 = i == MT - 1 ? (tail0 & 0x22222222u) : 0x22222222u;
+        const uint32_t l1 = i == MT - 1 ? (tail1 & 0x22222222u) : 0x22222222u;
+        qz |= (~bp[i][0] & l0) | (~bp[i][1] & l1);
+      }
       __builtin_amdgcn_sched_barrier(0);   // one tile's accumulator live at a time
     }
     bp[MT - 1][0] &= tail0;
@@ -199,39 +261,82 @@ __global__ void __launch_bounds__(256) benor_mfma_sure_kernel(KParams p) {
                      2 * c + 1 < MT ? (int)bp[2 * c + 1][1] : 0};
 
     // ---- P-phase ("voting phase", node.ts:83-158): every receiver tile
-    // counts the p0 plane; the sign of c0 - F - 0.5 is "not d0" -> x = 1
-    // (every receiver decides: node.ts:99-105, m > 2F).
-    uint32_t s_or = 0u, s_and = ~0u;
+    // counts the proposals; the sign of its result is its decision.  The
+    // outcome needs, per trial, whether some receiver decided 0 and whether
+    // some decided 1 (and for KIND 2 whether every receiver decided).
+    uint32_t any1, any0, halt = (uint32_t)ballot(valid);
+    if constexpr (SURE) {
+      uint32_t s_or = 0u, s_and = ~0u;        // sign bit = "not d0" = x1
 #pragma unroll
-    for (int i = 0; i < MT; ++i) {
-      asm volatile("" : "+v"(ones));
-      mf_v16f acc = mfma_count(ones, pb[0], cp);
+      for (int i = 0; i < MT; ++i) {
+        asm volatile("" : "+v"(ones));
+        mf_v16f acc = mfma_count(ones, pb[0], cp);
 #pragma unroll
-      for (int c = 1; c < KP; ++c) acc = mfma_count(ones, pb[c], acc);
+        for (int c = 1; c < KP; ++c) acc = mfma_count(ones, pb[c], acc);
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const uint32_t u = __float_as_uint(acc[j]);
-        if (i < MT - 1) {
-          s_or |= u;
-          s_and &= u;
-        } else {
-          const bool live = (vbits >> j) & 1u;
-          s_or |= live ? u : 0u;
-          s_and &= live ? u : ~0u;
+        for (int j = 0; j < 16; ++j) {
+          const uint32_t u = __float_as_uint(acc[j]);
+          if (i < MT - 1) {
+            s_or |= u;
+            s_and &= u;
+          } else {
+            const bool live = (vbits >> j) & 1u;
+            s_or |= live ? u : 0u;
+            s_and &= live ? u : ~0u;
+          }
         }
+        asm volatile("" : "+v"(s_or), "+v"(s_and));   // fold tile by tile: one accumulator live
+        __builtin_amdgcn_sched_barrier(0);
       }
-      asm volatile("" : "+v"(s_or), "+v"(s_and));   // fold tile by tile: one accumulator live
-      __builtin_amdgcn_sched_barrier(0);
+      const uint64_t b1 = ballot(s_or >> 31);          // some receiver decided 1
+      const uint64_t b0 = ballot(!(s_and >> 31));      // some receiver decided 0
+      any1 = (uint32_t)b1 | (uint32_t)(b1 >> 32);
+      any0 = (uint32_t)b0 | (uint32_t)(b0 >> 32);
+    } else {
+      float mn = __builtin_inff(), mx = -__builtin_inff(), ma = __builtin_inff();
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        asm volatile("" : "+v"(ones));
+        mf_v16f acc = mfma_count(ones, pb[0], i < MT - 1 ? cp : cp_tail);
+#pragma unroll
+        for (int c = 1; c < KP; ++c) acc = mfma_count(ones, pb[c], acc);
+#pragma unroll
+        for (int j = 0; j < 16; j += 2) {
+          mn = fminf(fminf(mn, acc[j]), acc[j + 1]);
+          mx = fmaxf(fmaxf(mx, acc[j]), acc[j + 1]);
+          if constexpr (KIND == 2) ma = fminf(fminf(ma, __builtin_fabsf(acc[j])), __builtin_fabsf(acc[j + 1]));
+        }
+        asm volatile("" : "+v"(mn), "+v"(mx), "+v"(ma));   // fold tile by tile: one accumulator live
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // ---- columns with a "?" proposal or an undecided receiver are deferred
+      const bool defer = qz != 0u || (KIND == 2 && !(ma > dec_thr));
+      const uint64_t bd = ballot(valid && defer);
+      const uint32_t dcols = (uint32_t)bd | (uint32_t)(bd >> 32);
+      halt &= ~dcols;
+      if (dcols) {
+        if (lane < 32u && ((dcols >> lane) & 1u))
+          seg[n_def + (uint32_t)__builtin_popcount(dcols & ((1u << lane) - 1u))] = t;
+        n_def += (uint32_t)__builtin_popcount(dcols);
+      }
+      const uint64_t b1 = ballot(mx > 0.0f);            // some receiver decided 1
+      const uint64_t b0 = ballot(mn < 0.0f);            // some receiver decided 0
+      any1 = (uint32_t)b1 | (uint32_t)(b1 >> 32);
+      any0 = (uint32_t)b0 | (uint32_t)(b0 >> 32);
     }
     // ---- outcome: bins 3 + v (R = 1), per trial column (lanes n, n + 32)
-    const uint64_t b1 = ballot(valid && (s_or >> 31));          // some receiver decided 1
-    const uint64_t b0 = ballot(valid && !(s_and >> 31));        // some receiver decided 0
-    const uint64_t bv = ballot(valid);
-    const uint32_t any1 = (uint32_t)b1 | (uint32_t)(b1 >> 32);
-    const uint32_t any0 = (uint32_t)b0 | (uint32_t)(b0 >> 32);
-    f_all += (uint32_t)__builtin_popcount((uint32_t)bv);
+    any1 &= halt;
+    any0 &= halt;
+    f_all += (uint32_t)__builtin_popcount(halt);
     f_1 += (uint32_t)__builtin_popcount(any1);
     f_2 += (uint32_t)__builtin_popcount(any1 & any0);
+  }
+  if (!SURE && n_def) {                        // this wave's deferred trials -> the compact list
+    __threadfence();
+    uint32_t base = 0u;
+    if (lane == 0) base = atomicAdd(p.defer_len, n_def);
+    base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+    for (uint32_t i = lane; i < n_def; i += 64u) p.defer_list[base + i] = seg[i];
   }
 
   const uint32_t hc = lane == 3u ? f_all - f_1 : (lane == 4u ? f_1 - f_2 : (lane == 5u ? f_2 : 0u));
@@ -244,12 +349,19 @@ __global__ void __launch_bounds__(256) benor_mfma_sure_kernel(KParams p) {
   }
 }
 
+template <int W, int KIND>
+static inline void launch_mfma_kind(const KParams &p, int grid, hipStream_t s) {
+  if (p.m <= 64u * (uint32_t)(W - 1) + 32u)
+    hipLaunchKernelGGL((benor_mfma_kernel<W, true, KIND>), dim3(grid), dim3(64 * kWavesPerBlock), p.hist_bytes, s, p);
+  else
+    hipLaunchKernelGGL((benor_mfma_kernel<W, false, KIND>), dim3(grid), dim3(64 * kWavesPerBlock), p.hist_bytes, s, p);
+}
+
 template <int W>
 hipError_t launch_mfma(const KParams &p, int grid, hipStream_t s) {
-  if (p.m <= 64u * (uint32_t)(W - 1) + 32u)
-    hipLaunchKernelGGL((benor_mfma_sure_kernel<W, true>), dim3(grid), dim3(64 * kWavesPerBlock), p.hist_bytes, s, p);
-  else
-    hipLaunchKernelGGL((benor_mfma_sure_kernel<W, false>), dim3(grid), dim3(64 * kWavesPerBlock), p.hist_bytes, s, p);
+  if (p.G == 0u) launch_mfma_kind<W, 0>(p, grid, s);
+  else if (p.G == 1u) launch_mfma_kind<W, 1>(p, grid, s);
+  else launch_mfma_kind<W, 2>(p, grid, s);
   return hipGetLastError();
 }
 

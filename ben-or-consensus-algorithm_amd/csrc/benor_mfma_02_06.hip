@@ -1,5 +1,6 @@
-// Matrix-core kernel instantiations W = 2..10 (benor_mfma.h), split from
-// W = 11..16 so the unrolled instantiations build in parallel.
+// Matrix-core kernel instantiations W = 2..6 (benor_mfma.h: KIND 0..2 x both
+// tile parities each), split over four units so the unrolled instantiations
+// build in parallel.
 #include "benor_mfma.h"
 
 namespace benor {
@@ -8,10 +9,6 @@ template hipError_t launch_mfma<3>(const KParams &, int, hipStream_t);
 template hipError_t launch_mfma<4>(const KParams &, int, hipStream_t);
 template hipError_t launch_mfma<5>(const KParams &, int, hipStream_t);
 template hipError_t launch_mfma<6>(const KParams &, int, hipStream_t);
-template hipError_t launch_mfma<7>(const KParams &, int, hipStream_t);
-template hipError_t launch_mfma<8>(const KParams &, int, hipStream_t);
-template hipError_t launch_mfma<9>(const KParams &, int, hipStream_t);
-template hipError_t launch_mfma<10>(const KParams &, int, hipStream_t);
 }  // namespace benor
 
 namespace benor {

@@ -83,6 +83,8 @@ struct bo_plan {
   int8_t *d_init_x = nullptr;      // event mode
   uint32_t *d_crash = nullptr;     // event mode
   uint32_t *d_scratch = nullptr;   // event mode
+  uint32_t *d_defer = nullptr;     // matrix-core KIND > 0: deferred-trial list, its length, per-wave segments
+  uint64_t defer_words = 0;
   int device = 0;
 };
 
@@ -290,15 +292,17 @@ static int plan_host(const bo_trials_cfg *cfg, std::vector<uint32_t> &live, std:
   }
   plane.assign(kp.W, make_uint4(0, 0, 0, 0));
   if (cfg->init_mode == BO_INIT_FIXED) {
+    uint32_t n0 = 0, n1 = 0;
     for (uint32_t c = 0; c < m; ++c) {
       const int8_t v = cfg->init[live[c]];
       if (v < 0 || v > 2) return fail(BO_ERR_INVALID_ARGUMENT, "initial value must be 0, 1 or '?'(2)");
       const uint32_t w = c >> 6, b = c & 63u;
       uint32_t *r = reinterpret_cast<uint32_t *>(&plane[w]);
-      if (v == 0) r[b >> 5] |= 1u << (b & 31u);
-      if (v == 1) r[2 + (b >> 5)] |= 1u << (b & 31u);
+      if (v == 0) { r[b >> 5] |= 1u << (b & 31u); ++n0; }
+      if (v == 1) { r[2 + (b >> 5)] |= 1u << (b & 31u); ++n1; }
       if (v == 2) ++kp.init_q;
     }
+    kp.init_tie = n0 == n1 ? 1u : 0u;
   }
   benor::plan_geometry(kp);   // after init_q: the kernel choice depends on the round-1 vote parity
   return BO_OK;
@@ -390,6 +394,7 @@ void bo_plan_destroy(bo_plan *pl) {
   if (pl->d_init_x) (void)hipFree(pl->d_init_x);
   if (pl->d_crash) (void)hipFree(pl->d_crash);
   if (pl->d_scratch) (void)hipFree(pl->d_scratch);
+  if (pl->d_defer) (void)hipFree(pl->d_defer);
   delete pl;
 }
 
@@ -426,6 +431,47 @@ static int plan_launch_impl(bo_plan *pl, uint64_t trial_begin, uint64_t trial_co
   kp.hist = reinterpret_cast<unsigned long long *>(hist_dev);
   kp.node_out = node_out;
   kp.rounds_out = rounds_out;
+  if (kp.variant == 7 && kp.G > 0u && !node_out && !rounds_out) {
+    // Matrix-core round 1 with deferral (benor_mfma.h, KIND > 0): per chunk of
+    // at most kDeferChunk trials, the matrix-core launch records the trials
+    // that do not halt in round 1, and the W kernel runs exactly those from
+    // round 1 (trial-list mode; the list length is read on the device, so
+    // the two launches queue back to back with no host sync).
+    const uint64_t cap = std::min<uint64_t>(trial_count, benor::kDeferChunk);
+    kp.trial_count = cap;
+    const int grid = benor::lockstep_grid(kp, pl->device);
+    const uint64_t waves = (uint64_t)grid * benor::kWavesPerBlock;
+    const uint64_t seg_cap = ((cap + 31u) / 32u + waves - 1u) / waves * 32u;   // a wave's trials per launch, at most
+    const uint64_t words = cap + 64u + waves * seg_cap;                        // list, its length (padded), segments
+    if (pl->defer_words < words) {
+      if (pl->d_defer) (void)hipFree(pl->d_defer);
+      pl->d_defer = nullptr;
+      pl->defer_words = 0;
+      HIP_TRY(hipMalloc(&pl->d_defer, sizeof(uint32_t) * words));
+      pl->defer_words = words;
+    }
+    uint32_t *len = pl->d_defer + cap;
+    for (uint64_t done = 0; done < trial_count;) {
+      const uint64_t n = std::min<uint64_t>(trial_count - done, cap);
+      HIP_TRY(hipMemsetAsync(len, 0, sizeof(uint32_t), s));
+      kp.trial_begin = trial_begin + done;
+      kp.trial_count = n;
+      kp.defer_list = pl->d_defer;
+      kp.defer_len = len;
+      kp.defer_seg = pl->d_defer + cap + 64u;
+      kp.defer_seg_cap = (uint32_t)seg_cap;
+      HIP_TRY(benor::launch_lockstep(kp, grid, s));
+      benor::KParams kw = kp;
+      kw.variant = 1;
+      kw.G = kw.W;
+      kw.defer_list = kw.defer_len = kw.defer_seg = nullptr;
+      kw.trial_list = pl->d_defer;
+      kw.trial_list_len = len;
+      HIP_TRY(benor::launch_lockstep(kw, benor::lockstep_grid(kw, pl->device), s));
+      done += n;
+    }
+    return BO_OK;
+  }
   // Launches of at most 2^31 trials: the kernels index trials within a launch in 32 bits.
   for (uint64_t done = 0; done < trial_count;) {
     const uint64_t n = std::min<uint64_t>(trial_count - done, benor::kMaxTrialsPerLaunch);

@@ -84,13 +84,18 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
   uint32_t m = p.m, F = p.F, k_max = p.k_max, hist_len = p.hist_len;
   // trial offsets within the launch are 32-bit (the host splits launches at 2^31)
   uint32_t trial_count = (uint32_t)p.trial_count;
+  const bool listed = p.trial_list_len != nullptr;
+  if (listed) {                    // trial-list mode: the list's length, set on the device
+    const uint32_t n = *p.trial_list_len;
+    trial_count = n < trial_count ? n : trial_count;
+  }
   asm volatile("" : "+s"(m), "+s"(F), "+s"(k_max), "+s"(hist_len), "+s"(trial_count));
 
   uint32_t *lhist = reinterpret_cast<uint32_t *>(smem);
   uint2 *ring = reinterpret_cast<uint2 *>(smem + p.hist_bytes + wv * p.wave_bytes);   // [TB][WP] x1 words
   uint2 *X = ring + TB * WP;       // [WP] final x1 plane (GET /getState only)
   uint2 *D = X + WP;               // [WP] sticky decided bits, kept only while some receiver is undecided
-  // parameter block: [0,1] Philox key (seed), [2,3] trial_begin
+  // parameter block: [0,1] Philox key (seed), [2,3] trial_begin, [4,5] trial list (or 0)
   uint32_t *keys = reinterpret_cast<uint32_t *>(smem + p.hist_bytes - kParamBytes);
 
   for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) lhist[i] = 0u;
@@ -99,6 +104,8 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
     keys[1] = (uint32_t)(p.seed >> 32);
     keys[2] = (uint32_t)p.trial_begin;
     keys[3] = (uint32_t)(p.trial_begin >> 32);
+    keys[4] = (uint32_t)(uintptr_t)p.trial_list;
+    keys[5] = (uint32_t)((uintptr_t)p.trial_list >> 32);
   }
   if (p.init_mode != BO_INIT_RANDOM && lane < (uint32_t)W) {
     const uint4 q = p.init_plane[lane];
@@ -122,7 +129,7 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
       const uint32_t s = lane / NPH, b = lane - s * NPH;
       const uint32_t t = base + s * waves_total;
       if (s < (uint32_t)TB && t < trial_count) {
-        const uint64_t trial = lds_u64(keys + 2) + t;
+        const uint64_t trial = trial_id(keys, t);
         const uint2 kk = lds_keys(keys);           // keep the round keys out of long-lived SGPRs
         const uint4 r = philox4x32_10(kk.x, kk.y, make_uint4((uint32_t)trial, (uint32_t)(trial >> 32), b, kStreamInit << 24));
         const uint64_t v0 = group_mask(2u * b, m), v1 = group_mask(2u * b + 1u, m);
@@ -201,7 +208,7 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
             const uint64_t tie = ballot_s(a1g == a0g) & rest;            // node.ts:110-111
             x1 |= ad1;
             if (tie) {                                                  // node.ts:111
-              const uint64_t trial = lds_u64(keys + 2) + t;
+              const uint64_t trial = trial_id(keys, t);
               x1 |= coin_ballot(keys, (uint32_t)trial, (uint32_t)(trial >> 32), g, r, tie);
             }
           }
@@ -273,7 +280,9 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
       if (t >= trial_count) break;
       uint32_t slow = 1u, nk = 1u;              // trials (bit k: s + k) to run alone; trials consumed
       if constexpr (K > 1 && !STATE) {
-        if (s + K - 1 < TB && t + (uint32_t)(K - 1) * waves_total < trial_count) {
+        // (not in trial-list mode: the matrix-core kernel's deferred trials
+        // never halt in round 1, so the interleaved pass would only be redone)
+        if (!listed && s + K - 1 < TB && t + (uint32_t)(K - 1) * waves_total < trial_count) {
           // ---- round 1 of K trials interleaved; a trial that does not halt in
           // round 1 (some receiver undecided) is re-run alone from round 1.
           uint32_t c1[K][W], a0[K][W], a1[K][W];

@@ -8,6 +8,10 @@ GPU: bit-exact histograms against the oracle on every chunk count W = 2..16
 (BENOR_NO_MFMA=1) over 10^6 trials; the network API (per-node state) on an
 MFMA shape; and the init_q parity regression (the kernel choice depends on
 the number of "?" initial values, which must be known before planning).
+Deferral (KIND 1: m > 2F with ties; KIND 2: F < m <= 2F): trials that do not
+halt in round 1 go to the W kernel's trial-list mode -- oracle histograms on
+both kinds and both m parities, several chunks of deferred trials, and
+equality with the W kernel alone.
 """
 import os
 
@@ -53,8 +57,9 @@ def test_kernel_choice():
     assert K.kernel_for(256, 85) == K.BO_KERNEL_MFMA              # configs[2]
     for N, F in mfma_shapes():
         assert K.kernel_for(N, F) == K.BO_KERNEL_MFMA, (N, F)
-    assert K.kernel_for(1000, 300) == K.BO_KERNEL_W               # m = 700 even: ties, coins, more rounds
-    assert K.kernel_for(1025, 512) == K.BO_KERNEL_W               # m = 513 odd but m <= 2F: undecided receivers
+    assert K.kernel_for(1000, 300) == K.BO_KERNEL_MFMA            # m = 700 even: round 1 here, tied trials deferred
+    assert K.kernel_for(1025, 512) == K.BO_KERNEL_MFMA            # m = 513 <= 2F: undecided trials deferred
+    assert K.kernel_for(1024, 512) == K.BO_KERNEL_W               # m = F: no receiver can ever decide
     assert K.kernel_for(1537, 512) == K.BO_KERNEL_W               # m = 1025 > kMaxMfmaM
     assert K.kernel_for(4096, 1365) == K.BO_KERNEL_BLOCKED        # m = 2731
     assert K.kernel_for(10, 4) == K.BO_KERNEL_LANE                # m <= 64
@@ -65,9 +70,13 @@ def test_kernel_choice():
     # fixed initial values: an odd number of "?" makes round 1's vote count even
     vals = [1] * 1024
     vals[500] = "?"
-    assert K.kernel_for(1024, 341, initial_values=vals) == K.BO_KERNEL_W
+    assert K.kernel_for(1024, 341, initial_values=vals) == K.BO_KERNEL_MFMA   # M even: ties deferred
     vals[501] = "?"
     assert K.kernel_for(1024, 341, initial_values=vals) == K.BO_KERNEL_MFMA
+    tied = [i % 2 for i in range(1024)]                                      # live 341..1023: 342 ones, 341 zeros
+    assert K.kernel_for(1024, 341, initial_values=tied) == K.BO_KERNEL_MFMA
+    tied[1023] = "?"                                                         # 341 / 341: every trial ties in round 1
+    assert K.kernel_for(1024, 341, initial_values=tied) == K.BO_KERNEL_W
     os.environ["BENOR_NO_MFMA"] = "1"
     try:
         assert K.kernel_for(1024, 341) == K.BO_KERNEL_W
@@ -147,6 +156,61 @@ def test_question_mark_parity_picks_the_right_kernel(N, F, init):
     ref = oracle.run_trials(N, F, first_f(N, F), seed=21, trial_begin=0, trial_count=4000, k_max=12,
                             initial_values=init)
     np.testing.assert_array_equal(got, ref.hist)
+
+
+def deferral_shapes():
+    """(N, F, kind): KIND 1 (m > 2F, m even: ties) and KIND 2 (F < m <= 2F,
+    both parities), across tile parities and chunk counts."""
+    return [(100, 0, 1), (256, 0, 1), (700, 200, 1), (1024, 0, 1), (1000, 333, 1), (97, 31, 1),
+            (129, 64, 2), (130, 64, 2), (300, 140, 2), (513, 256, 2), (1024, 500, 2), (1500, 700, 2)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,F,kind", deferral_shapes())
+def test_mfma_deferral_matches_oracle(N, F, kind):
+    seed = (N * 31 + F) & 0xFFFF
+    T = 1500 + (N % 97)
+    begin = (1 << 34) + 17 * N
+    p = plan(N, F, seed=seed, k_max=12)
+    assert p.kernel == benor.BO_KERNEL_MFMA
+    got = p.run(begin, T)
+    ref = oracle.run_trials(N, F, first_f(N, F), seed=seed, trial_begin=begin, trial_count=T, k_max=12)
+    np.testing.assert_array_equal(got, ref.hist)
+    # even m at m > 2F defers exactly the round-1 ties (q(m) of the trials)
+    assert got[3:6].sum() < T or (N - F) % 2 == 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,F,q", [(300, 99, 1), (1024, 341, 3), (129, 40, 1), (500, 200, 5)])
+def test_mfma_deferral_fixed_init_matches_oracle(N, F, q):
+    """Fixed starts with an odd number of "?" inputs: round 1 has an even vote
+    count; a tied start is planned on the W kernel."""
+    rng = np.random.default_rng(N * 3 + q)
+    vals = [int(v) for v in rng.integers(0, 2, N)]
+    for j in rng.choice(np.arange(F, N), q, replace=False):
+        vals[j] = "?"
+    p = plan(N, F, seed=13, k_max=10, initial_values=vals)
+    live = vals[F:]
+    tie = live.count(0) == live.count(1)
+    assert p.kernel == (benor.BO_KERNEL_W if tie else benor.BO_KERNEL_MFMA)
+    got = p.run(7, 777)
+    ref = oracle.run_trials(N, F, first_f(N, F), seed=13, trial_begin=7, trial_count=777, k_max=10,
+                            initial_values=vals)
+    np.testing.assert_array_equal(got, ref.hist)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,F,T", [(128, 0, 9_000_001), (1024, 0, 1_000_003), (600, 250, 2_000_001), (257, 127, 5_000_000)])
+def test_mfma_deferral_equals_popcount_kernel(N, F, T):
+    """Over several deferral chunks (kDeferChunk = 2^22 trials): the same
+    histogram as the popcount kernels alone, and a split launch sums to it."""
+    a = plan(N, F, True, seed=5, k_max=24)
+    b = plan(N, F, False, seed=5, k_max=24)
+    assert a.kernel == benor.BO_KERNEL_MFMA and b.kernel != benor.BO_KERNEL_MFMA
+    ha = a.run(11, T)
+    np.testing.assert_array_equal(ha, b.run(11, T))
+    cut = T // 3 + 5
+    np.testing.assert_array_equal(ha, a.run(11, cut) + a.run(11 + cut, T - cut))
 
 
 @pytest.mark.gpu
