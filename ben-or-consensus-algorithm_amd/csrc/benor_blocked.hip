@@ -94,6 +94,10 @@ __global__ void __launch_bounds__(256) benor_lockstep_blocked_kernel(KParams p) 
   // Round-loop scalars in registers; the rest re-read where used (as the W kernel).
   uint32_t m = p.m, F = p.F, W = p.W, NB = p.nblocks, k_max = p.k_max, hist_len = p.hist_len;
   uint32_t trial_count = (uint32_t)p.trial_count;     // launches are split at 2^31 trials
+  if (p.trial_list_len) {                    // trial-list mode (as the W kernel): the list's length
+    const uint32_t n = *p.trial_list_len;
+    trial_count = n < trial_count ? n : trial_count;
+  }
   asm volatile("" : "+s"(m), "+s"(F), "+s"(W), "+s"(NB));
   asm volatile("" : "+s"(k_max), "+s"(hist_len), "+s"(trial_count));
   const uint32_t nph = (W + 1u) >> 1, tb = 64u / nph, WP = 2u * nph;
@@ -113,6 +117,8 @@ __global__ void __launch_bounds__(256) benor_lockstep_blocked_kernel(KParams p) 
     keys[1] = (uint32_t)(p.seed >> 32);
     keys[2] = (uint32_t)p.trial_begin;
     keys[3] = (uint32_t)(p.trial_begin >> 32);
+    keys[4] = (uint32_t)(uintptr_t)p.trial_list;
+    keys[5] = (uint32_t)((uintptr_t)p.trial_list >> 32);
   }
   if (p.init_mode != BO_INIT_RANDOM)
     for (uint32_t w = lane; w < WP; w += 64u) {
@@ -132,7 +138,7 @@ __global__ void __launch_bounds__(256) benor_lockstep_blocked_kernel(KParams p) 
       const uint32_t s = lane / nph, bk = lane - s * nph;
       const uint32_t t = base + s * waves_total;
       if (s < tb && t < trial_count) {
-        const uint64_t trial = lds_u64(keys + 2) + t;
+        const uint64_t trial = trial_id(keys, t);
         const uint2 kk = lds_keys(keys);
         const uint4 r = philox4x32_10(kk.x, kk.y, make_uint4((uint32_t)trial, (uint32_t)(trial >> 32), bk, kStreamInit << 24));
         const uint64_t v0 = group_mask(2u * bk, m), v1 = group_mask(2u * bk + 1u, m);
@@ -222,7 +228,7 @@ __global__ void __launch_bounds__(256) benor_lockstep_blocked_kernel(KParams p) 
                 const uint64_t tie = ballot_s(a1[g] == a0g) & rest;        // node.ts:110-111
                 x1 |= ad1;
                 if (tie) {                                                // node.ts:111
-                  const uint64_t trial = lds_u64(keys + 2) + t;
+                  const uint64_t trial = trial_id(keys, t);
                   x1 |= coin_ballot(keys, (uint32_t)trial, (uint32_t)(trial >> 32), b * G + g, r, tie);
                 }
               }

@@ -21,7 +21,8 @@ constexpr int kWavesPerBlock = 4;          // 256-thread workgroups, one trial p
 constexpr uint32_t kMaxW = BO_MAX_N / 64;  // u64 words per bit plane at N = 4096
 constexpr int kMaxWSpecialised = 32;       // m <= 2048: fully unrolled W-specialised kernel
 constexpr uint32_t kMaxLaneM = 64;         // m <= 64: lane kernel, one trial per lane (benor_lane.h)
-constexpr uint32_t kMaxMfmaM = 1024;       // matrix-core kernel (benor_mfma.h): W <= 16, operands in registers
+constexpr uint32_t kMaxMfmaM = 1024;       // matrix-core kernel (benor_mfma.h): W <= 16, operands in registers;
+                                           // beyond, the big-network form (runtime W, proposals in LDS) to BO_MAX_N
 constexpr uint32_t kMaxEventN = 256;       // event level: node ids in 8 bits of a message
 constexpr uint64_t kMaxTrialsPerLaunch = 1ull << 31;   // trial offsets within a launch fit 32 bits
 constexpr uint32_t kParamBytes = 32;       // LDS parameter block after the histogram (W kernel)
@@ -36,6 +37,8 @@ struct KParams {
                             //    launches and the trials it defers),
                             // 6: lane lockstep (m <= 64), 1: W-specialised lockstep (W <= kMaxWSpecialised = 32),
                             // 0: blocked lockstep, 2: random delivery, 4: event level
+  uint32_t base_variant;    // variant 7: the popcount kernel (1 W, 0 blocked) that serves the state
+  uint32_t base_G;          //   launches and the deferred trials, and its G
   uint32_t mode;            // BO_MODE_LOCKSTEP / BO_MODE_RANDOM_DELIVERY
   uint32_t q;               // quorum N - F (messages each receiver tallies per phase)
   uint32_t k_max;
@@ -93,9 +96,12 @@ hipError_t launch_b(const KParams &p, int grid_blocks, hipStream_t stream);
 template <int MM>
 hipError_t launch_lane_m(const KParams &p, int grid_blocks, hipStream_t stream);
 
-// Matrix-core kernel (benor_mfma.h), W = 2..16, instantiated in benor_mfma_*.hip.
+// Matrix-core kernel (benor_mfma.h), W = 2..16, instantiated in benor_mfma_*.hip;
+// W = 17..64 (m <= 4096): the big-network form, benor_mfma_big.hip.
 template <int W>
 hipError_t launch_mfma(const KParams &p, int grid_blocks, hipStream_t stream);
+hipError_t launch_mfma_big(const KParams &p, int grid_blocks, hipStream_t stream);
+uint32_t mfma_big_lds_bytes(const KParams &p);   // dynamic LDS of one workgroup of the big form
 
 // Grid size that fills the current device for this configuration.
 int lockstep_grid(const KParams &p, int device);

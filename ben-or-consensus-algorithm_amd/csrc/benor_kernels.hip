@@ -761,19 +761,6 @@ void plan_geometry(KParams &p) {
     p.nblocks = 1;
     p.variant = 1;
     p.wave_bytes = (tb * WP + 2u * WP) * 8u;            // init ring, final x1 plane, decided bits
-    // Matrix-core kernel (benor_mfma.h) for round 1 wherever a trial can halt
-    // there (m > F; not a fixed start whose round 1 ties for every trial).
-    // KIND 0: all vote counts odd (m odd, even number of "?") and m > 2F --
-    // every trial halts in round 1; KIND 1: m > 2F; KIND 2: F < m <= 2F.
-    // Trials that do not halt in round 1 go to this W kernel (trial-list
-    // mode), as do the state launches (network API), so its LDS plan stays.
-    const bool sure = (p.m & 1u) && !(p.init_q & 1u) && p.m > 2u * p.F;
-    const bool can_halt = p.m > p.F && !(p.init_mode == BO_INIT_FIXED && p.init_tie);
-    const char *no_mfma = getenv("BENOR_NO_MFMA");
-    if (can_halt && p.m <= kMaxMfmaM && !(no_mfma && no_mfma[0] == '1')) {
-      p.variant = 7;
-      p.G = sure ? 0u : (p.m > 2u * p.F ? 1u : 2u);
-    }
   } else {
     // Blocks of G = ceil(W / nb) in 11..22 groups: the fewest padded groups nb * G,
     // ties to fewer blocks (larger G: more v_bcnt per LDS read and loop step, which
@@ -795,6 +782,24 @@ void plan_geometry(KParams &p) {
     p.nblocks = nb;
     p.variant = 0;
     p.wave_bytes = (tb * WP + XW) * 8u + G * nb * 16u + nb * 256u;   // ring, x1 plane, {p0,p1} plane, decided bits
+  }
+  // Matrix-core kernel (benor_mfma.h) for round 1 wherever a trial can halt
+  // there (m > F; not a fixed start whose round 1 ties for every trial).
+  // KIND 0: all vote counts odd (m odd, even number of "?") and m > 2F --
+  // every trial halts in round 1; KIND 1: m > 2F; KIND 2: F < m <= 2F.
+  // Trials that do not halt in round 1 go to the popcount kernel planned
+  // above (trial-list mode), as do the state launches (network API), so its
+  // LDS plan stays.
+  const bool sure = (p.m & 1u) && !(p.init_q & 1u) && p.m > 2u * p.F;
+  const bool can_halt = p.m > p.F && !(p.init_mode == BO_INIT_FIXED && p.init_tie);
+  const char *no_mfma = getenv("BENOR_NO_MFMA");
+  const char *no_big = getenv("BENOR_NO_MFMA_BIG");
+  const bool big_ok = !(no_big && no_big[0] == '1');
+  if (can_halt && (p.m <= kMaxMfmaM || big_ok) && !(no_mfma && no_mfma[0] == '1')) {
+    p.base_variant = p.variant;
+    p.base_G = p.G;
+    p.variant = 7;
+    p.G = sure ? 0u : (p.m > 2u * p.F ? 1u : 2u);
   }
   p.lds_bytes = p.hist_bytes + kWavesPerBlock * p.wave_bytes;
 }
@@ -844,9 +849,17 @@ hipError_t launch_lockstep(const KParams &p, int grid, hipStream_t s) {
     hipLaunchKernelGGL(benor_random_kernel, dim3(grid), dim3(64 * kWavesPerBlock), p.lds_bytes, s, p);
     return hipGetLastError();
   }
-  if (p.variant == 7 && !p.node_out && !p.rounds_out)
+  if (p.variant == 7 && !p.node_out && !p.rounds_out) {
+    if (p.W > 16u) return launch_mfma_big(p, grid, s);                                                        // W = 17..64
     return dispatch_mfma(p, grid, s, std::make_integer_sequence<int, 15>{});                                  // W = 2..16
-  if (p.variant == 1 || p.variant == 7)
+  }
+  if (p.variant == 7) {                      // state launch of a matrix-core shape: its popcount kernel
+    KParams q = p;
+    q.variant = p.base_variant;
+    q.G = p.base_G;
+    return launch_lockstep(q, grid, s);
+  }
+  if (p.variant == 1)
     return dispatch_w(p, grid, s, std::make_integer_sequence<int, kMaxWSpecialised - 1>{});                    // W = 2..32
   return dispatch_b(p, grid, s, std::make_integer_sequence<int, 12>{});
 }
@@ -866,7 +879,8 @@ int lockstep_grid(const KParams &p, int device) {
   const uint64_t waves_needed = (p.trial_count + per_wave - 1u) / per_wave;
   const uint64_t blocks_needed = (waves_needed + kWavesPerBlock - 1) / kWavesPerBlock;
   uint64_t per_cu = 8;
-  const uint32_t lds = mfma ? p.hist_bytes : p.lds_bytes;   // the matrix-core kernel uses no wave slices
+  // the matrix-core kernel uses no wave slices (its big-network form: proposal planes)
+  const uint32_t lds = mfma ? (p.W > 16u ? mfma_big_lds_bytes(p) : p.hist_bytes) : p.lds_bytes;
   if (lds > 0) {
     const uint64_t lds_fit = (160u * 1024u) / lds;
     if (lds_fit < per_cu) per_cu = lds_fit ? lds_fit : 1;

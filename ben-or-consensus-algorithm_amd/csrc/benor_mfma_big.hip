@@ -1,0 +1,247 @@
+// benor_mfma_big.hip -- the matrix-core round-1 kernel for big networks,
+// 1024 < m <= 4096 (W = ceil(m / 64) = 17..64 sender chunks): the same
+// formulation, KINDs and deferral as benor_mfma.h, with the chunk count a
+// runtime value.
+//
+// What changes with size.  benor_mfma.h keeps every operand of a trial group
+// in registers, fully unrolled per W; at W = 64 that would be 4W VGPRs of
+// expanded votes plus 2 * ceil(m/32) of packed proposals.  Here
+//  * the x plane stays as bits in the wave's LDS slice, one word per lane
+//    per chunk, read and expanded to e2m1 nibbles right before each product
+//    (one ds_read_b32 and 4 VALU per two products; runtime loops, so the code
+//    does not grow with W and no operand array lives in registers);
+//  * the proposal plane goes to LDS as bits too, one word per lane per pair of
+//    receiver tiles: the fp4-converted R-phase results (+6 / -6 / 0 nibbles,
+//    as KIND 1, 2 of benor_mfma.h) keep their sign bits, four nibble words
+//    folding into one 32-bit word (bit 4i + 3 - s of word s), so the P-phase
+//    counts c0 = the receivers whose proposal is 0 (node.ts:63-69);
+//  * two receiver tiles run side by side on one expanded operand (two
+//    independent accumulator chains: half the expansion VALU per product).
+// The layout of accumulators, trial columns and thresholds is benor_mfma.h's;
+// the P-phase thresholds are on c0 (A scale 2^0, or 2^1 for KIND 2):
+//  KIND 0, 1: acc = c0 - F - 0.5, negative exactly when c0 <= F: with no "?"
+//    proposal c1 = m - c0 >= m - F > F, so the receiver decides 1
+//    (node.ts:102-105); positive: c0 > F, decide 0 (node.ts:99-101);
+//  KIND 2: acc = 2 c0 - m; decided iff |acc| > 2F - m (c0 > F or c1 > F),
+//    0 for acc > 0, 1 for acc < 0.
+// Trials with a "?" proposal (KIND 1, 2) or an undecided receiver (KIND 2)
+// are deferred to the popcount kernel exactly as in benor_mfma.h.
+#include "benor_mfma.h"
+
+namespace benor {
+
+constexpr uint32_t kBigMaxW = kMaxW;   // 64 chunks at N = 4096
+
+// Words per lane of a wave's x plane: the W x1 words rounded up to whole
+// Philox blocks per lane half (4 words each); the slice adds the KP <= W
+// proposal words.
+__host__ __device__ constexpr uint32_t big_plane_words(uint32_t W) { return 4u * ((((W + 1u) >> 1) + 1u) >> 1); }
+__host__ __device__ constexpr uint32_t big_slice_words(uint32_t W) { return big_plane_words(W) + W; }
+
+template <int KIND>
+__global__ void __launch_bounds__(256) benor_mfma_big_kernel(KParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t lane = threadIdx.x & 63u, h = lane >> 5;
+  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  uint32_t m = p.m, W = p.W, hist_len = p.hist_len, trial_count = (uint32_t)p.trial_count;
+  asm volatile("" : "+s"(m), "+s"(W), "+s"(hist_len), "+s"(trial_count));
+  const uint32_t MT = (m + 31u) >> 5;         // 32-receiver tiles
+  const uint32_t KP = (MT + 1u) >> 1;         // P-phase K chunks (tile pairs)
+
+  uint32_t *lhist = reinterpret_cast<uint32_t *>(smem);
+  uint32_t *keys = reinterpret_cast<uint32_t *>(smem + p.hist_bytes - kParamBytes);
+  // The wave's LDS slice: X [plane_words][64] x1 bits, then P [W][64]
+  // proposal bits.  Each lane reads back only its own words (its trial
+  // column and half), so no barrier orders them.
+  uint32_t *X = reinterpret_cast<uint32_t *>(smem + p.hist_bytes) + (size_t)wv * big_slice_words(W) * 64u;
+  uint32_t *PL = X + big_plane_words(W) * 64u;
+  for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) lhist[i] = 0u;
+  if (threadIdx.x == 0) {
+    keys[0] = (uint32_t)p.seed;
+    keys[1] = (uint32_t)(p.seed >> 32);
+    keys[2] = (uint32_t)p.trial_begin;
+    keys[3] = (uint32_t)(p.trial_begin >> 32);
+  }
+  __syncthreads();
+
+  const bool random_init = p.init_mode == BO_INIT_RANDOM;
+  const float bias_r = -8.0f * (float)(m - p.init_q);   // acc = 8 (c1 - c0): p1 > 0, p0 < 0, "?" = 0
+  const float bias_p = KIND == 2 ? -(float)m : -((float)p.F + 0.5f);
+  const float dec_thr = (float)(2u * p.F - m) + 0.5f;   // KIND 2: |2 c0 - m| > 2F - m <=> decided
+  const uint32_t mrem = m - 32u * (MT - 1u);             // live rows of the last tile, 1..32
+  uint32_t tail0 = 0, tail1 = 0;                         // its nibble masks (KIND-1-style packing)
+  uint32_t live_last = 0;                                // its live accumulator registers
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const uint32_t row = (uint32_t)((j & 3) + 8 * (j >> 2)) + 4u * h;
+    if (row < mrem) {
+      live_last |= 1u << j;
+      if (j < 8) tail0 |= 0xFu << (4 * (j & 7));
+      else tail1 |= 0xFu << (4 * (j & 7));
+    }
+  }
+  const int last_bits = (int)m - 32 * (2 * ((int)W - 1) + (int)h);
+  const uint32_t last_mask = last_bits >= 32 ? ~0u : (last_bits <= 0 ? 0u : ((1u << last_bits) - 1u));
+
+  mf_v4i ones0 = {0x22222222, 0x22222222, 0x22222222, 0x22222222};
+  mf_v4i ones1 = ones0;
+  uint32_t f_all = 0, f_1 = 0, f_2 = 0;
+  const uint32_t ngroups = (trial_count + 31u) >> 5;
+  const uint32_t waves_total = gridDim.x * kWavesPerBlock;
+  const uint32_t wave_id = blockIdx.x * kWavesPerBlock + wv;
+  uint32_t n_def = 0;
+  uint32_t *seg = KIND == 0 ? nullptr : p.defer_seg + (size_t)wave_id * p.defer_seg_cap;
+  for (uint32_t g = wave_id; g < ngroups; g += waves_total) {
+    const uint32_t t = (g << 5) + (lane & 31u);
+    const bool valid = t < trial_count;
+    // ---- /start (node.ts:167-188): x1 words 2c + h of this lane's trial, c < W
+    if (random_init) {                         // whole Philox blocks, the halves trading words
+      const uint64_t trial = lds_u64(keys + 2) + t;
+      const uint32_t NJ = (((W + 1u) >> 1) + 1u) >> 1;   // blocks per lane half
+      for (uint32_t j = 0; j < NJ; ++j) {
+        const uint2 kk = lds_keys(keys);
+        const uint4 r = philox4x32_10(kk.x, kk.y,
+                                      make_uint4((uint32_t)trial, (uint32_t)(trial >> 32), 2u * j + h, kStreamInit << 24));
+        const uint32_t keep_a = h ? r.y : r.x, keep_b = h ? r.w : r.z;
+        const uint32_t give_a = h ? r.x : r.y, give_b = h ? r.z : r.w;
+        const uint32_t recv_a = (uint32_t)__shfl_xor((int)give_a, 32);
+        const uint32_t recv_b = (uint32_t)__shfl_xor((int)give_b, 32);
+        X[(4u * j + 0u) * 64u + lane] = h ? recv_a : keep_a;
+        X[(4u * j + 1u) * 64u + lane] = h ? recv_b : keep_b;
+        X[(4u * j + 2u) * 64u + lane] = h ? keep_a : recv_a;
+        X[(4u * j + 3u) * 64u + lane] = h ? keep_b : recv_b;
+      }
+    } else {
+      for (uint32_t c = 0; c < W; ++c) {
+        const uint4 q = p.init_plane[c];
+        X[c * 64u + lane] = h ? q.w : q.z;
+      }
+    }
+    X[(W - 1u) * 64u + lane] &= last_mask;
+
+    // ---- R-phase (node.ts:46-82): tiles i, i + 1 on the same expanded x
+    // chunk; proposals to LDS as sign bits (1 = proposal 0).
+    uint32_t qz = 0u;
+    for (uint32_t i = 0; i < MT; i += 2u) {
+      asm volatile("" : "+v"(ones0), "+v"(ones1));
+      mf_v16f acc0, acc1;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc0[j] = acc1[j] = bias_r;
+      for (uint32_t c = 0; c < W; ++c) {
+        const mf_v4i b = expand_votes(X[c * 64u + lane]);
+        acc0 = mfma_count<4>(ones0, b, acc0);
+        acc1 = mfma_count<4>(ones1, b, acc1);
+      }
+      // nibble masks of the two tiles: full, the last (partial) tile, or none (past MT)
+      const uint32_t m00 = i < MT - 1u ? ~0u : tail0, m01 = i < MT - 1u ? ~0u : tail1;
+      const uint32_t m10 = i + 1u < MT - 1u ? ~0u : (i + 1u == MT - 1u ? tail0 : 0u);
+      const uint32_t m11 = i + 1u < MT - 1u ? ~0u : (i + 1u == MT - 1u ? tail1 : 0u);
+      const uint32_t n0 = pack_fp4_8(acc0, 0) & m00, n1 = pack_fp4_8(acc0, 8) & m01;
+      const uint32_t n2 = pack_fp4_8(acc1, 0) & m10, n3 = pack_fp4_8(acc1, 8) & m11;
+      if constexpr (KIND > 0)                  // a live "?" nibble is 0: bit 1 clear
+        qz |= (~n0 & m00 & 0x22222222u) | (~n1 & m01 & 0x22222222u) | (~n2 & m10 & 0x22222222u) |
+              (~n3 & m11 & 0x22222222u);
+      const uint32_t s = 0x88888888u;
+      PL[(i >> 1) * 64u + lane] = (n0 & s) | ((n1 & s) >> 1) | ((n2 & s) >> 2) | ((n3 & s) >> 3);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+
+    // ---- P-phase (node.ts:83-158): every receiver tile counts the 0-proposals
+    float mn = __builtin_inff(), mx = -__builtin_inff(), ma = __builtin_inff();
+    for (uint32_t i = 0; i < MT; i += 2u) {
+      asm volatile("" : "+v"(ones0), "+v"(ones1));
+      const float nanf = __builtin_nanf("");
+      mf_v16f acc0, acc1;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {           // rows with no receiver start at NaN: the reductions skip them
+        const bool l0 = i < MT - 1u || ((live_last >> j) & 1u);
+        const bool l1 = i + 1u < MT - 1u || (i + 1u == MT - 1u && ((live_last >> j) & 1u));
+        acc0[j] = l0 ? bias_p : nanf;
+        acc1[j] = l1 ? bias_p : nanf;
+      }
+      for (uint32_t k = 0; k < KP; ++k) {
+        const mf_v4i b = expand_votes(PL[k * 64u + lane]);
+        if constexpr (KIND == 2) {
+          acc0 = mfma_count<1>(ones0, b, acc0);
+          acc1 = mfma_count<1>(ones1, b, acc1);
+        } else {
+          acc0 = mfma_count(ones0, b, acc0);
+          acc1 = mfma_count(ones1, b, acc1);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 16; j += 2) {
+        mn = fminf(fminf(mn, acc0[j]), acc0[j + 1]);
+        mx = fmaxf(fmaxf(mx, acc0[j]), acc0[j + 1]);
+        mn = fminf(fminf(mn, acc1[j]), acc1[j + 1]);
+        mx = fmaxf(fmaxf(mx, acc1[j]), acc1[j + 1]);
+        if constexpr (KIND == 2) {
+          ma = fminf(fminf(ma, __builtin_fabsf(acc0[j])), __builtin_fabsf(acc0[j + 1]));
+          ma = fminf(fminf(ma, __builtin_fabsf(acc1[j])), __builtin_fabsf(acc1[j + 1]));
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+
+    // ---- outcome: bins 3 + v (R = 1); KIND > 0 defers as benor_mfma.h
+    uint32_t halt = (uint32_t)ballot(valid);
+    if constexpr (KIND > 0) {
+      const bool defer = qz != 0u || (KIND == 2 && !(ma > dec_thr));
+      const uint64_t bd = ballot(valid && defer);
+      const uint32_t dcols = (uint32_t)bd | (uint32_t)(bd >> 32);
+      halt &= ~dcols;
+      if (dcols) {
+        if (lane < 32u && ((dcols >> lane) & 1u))
+          seg[n_def + (uint32_t)__builtin_popcount(dcols & ((1u << lane) - 1u))] = t;
+        n_def += (uint32_t)__builtin_popcount(dcols);
+      }
+    }
+    // KIND 0, 1: acc < 0 <=> decided 1; KIND 2: acc < 0 <=> decided 1 as well (2 c0 - m < 0)
+    const uint64_t b1 = ballot(mn < 0.0f);
+    const uint64_t b0 = ballot(mx > 0.0f);
+    const uint32_t any1 = ((uint32_t)b1 | (uint32_t)(b1 >> 32)) & halt;
+    const uint32_t any0 = ((uint32_t)b0 | (uint32_t)(b0 >> 32)) & halt;
+    f_all += (uint32_t)__builtin_popcount(halt);
+    f_1 += (uint32_t)__builtin_popcount(any1);
+    f_2 += (uint32_t)__builtin_popcount(any1 & any0);
+  }
+  if (KIND > 0 && n_def) {                     // this wave's deferred trials -> the compact list
+    __threadfence();
+    uint32_t base = 0u;
+    if (lane == 0) base = atomicAdd(p.defer_len, n_def);
+    base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+    for (uint32_t i = lane; i < n_def; i += 64u) p.defer_list[base + i] = seg[i];
+  }
+
+  const uint32_t hc = lane == 3u ? f_all - f_1 : (lane == 4u ? f_1 - f_2 : (lane == 5u ? f_2 : 0u));
+  if (hc) atomicAdd(&lhist[lane], hc);
+  if (lane == 0 && f_2) atomicAdd(&lhist[hist_len - 1u], f_2);
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) {
+    const uint32_t c = lhist[i];
+    if (c) atomicAdd(&p.hist[i], (unsigned long long)c);
+  }
+}
+
+uint32_t mfma_big_lds_bytes(const KParams &p) { return p.hist_bytes + kWavesPerBlock * big_slice_words(p.W) * 64u * 4u; }
+
+template <int KIND>
+static hipError_t launch_big_kind(const KParams &p, int grid, hipStream_t s) {
+  const uint32_t lds = mfma_big_lds_bytes(p);
+  if (lds > 64u * 1024u) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&benor_mfma_big_kernel<KIND>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(benor_mfma_big_kernel<KIND>, dim3(grid), dim3(64 * kWavesPerBlock), lds, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_mfma_big(const KParams &p, int grid, hipStream_t s) {
+  if (p.W < 17u || p.W > kBigMaxW) return hipErrorInvalidValue;
+  if (p.G == 0u) return launch_big_kind<0>(p, grid, s);
+  if (p.G == 1u) return launch_big_kind<1>(p, grid, s);
+  return launch_big_kind<2>(p, grid, s);
+}
+
+}  // namespace benor

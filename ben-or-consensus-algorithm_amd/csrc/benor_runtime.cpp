@@ -462,8 +462,8 @@ static int plan_launch_impl(bo_plan *pl, uint64_t trial_begin, uint64_t trial_co
       kp.defer_seg_cap = (uint32_t)seg_cap;
       HIP_TRY(benor::launch_lockstep(kp, grid, s));
       benor::KParams kw = kp;
-      kw.variant = 1;
-      kw.G = kw.W;
+      kw.variant = kp.base_variant;              // W kernel (W <= 32) or blocked kernel
+      kw.G = kp.base_G;
       kw.defer_list = kw.defer_len = kw.defer_seg = nullptr;
       kw.trial_list = pl->d_defer;
       kw.trial_list_len = len;

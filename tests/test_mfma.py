@@ -60,8 +60,9 @@ def test_kernel_choice():
     assert K.kernel_for(1000, 300) == K.BO_KERNEL_MFMA            # m = 700 even: round 1 here, tied trials deferred
     assert K.kernel_for(1025, 512) == K.BO_KERNEL_MFMA            # m = 513 <= 2F: undecided trials deferred
     assert K.kernel_for(1024, 512) == K.BO_KERNEL_W               # m = F: no receiver can ever decide
-    assert K.kernel_for(1537, 512) == K.BO_KERNEL_W               # m = 1025 > kMaxMfmaM
-    assert K.kernel_for(4096, 1365) == K.BO_KERNEL_BLOCKED        # m = 2731
+    assert K.kernel_for(1537, 512) == K.BO_KERNEL_MFMA            # m = 1025: the big-network form
+    assert K.kernel_for(4096, 1365) == K.BO_KERNEL_MFMA           # m = 2731
+    assert K.kernel_for(4096, 2048) == K.BO_KERNEL_W              # m = F: never decides
     assert K.kernel_for(10, 4) == K.BO_KERNEL_LANE                # m <= 64
     assert K.kernel_for(96, 31) == K.BO_KERNEL_MFMA               # m = 65
     assert K.kernel_for(1024, 341, mode=K.BO_MODE_RANDOM_DELIVERY) == K.BO_KERNEL_RANDOM
@@ -80,8 +81,16 @@ def test_kernel_choice():
     os.environ["BENOR_NO_MFMA"] = "1"
     try:
         assert K.kernel_for(1024, 341) == K.BO_KERNEL_W
+        assert K.kernel_for(4096, 1365) == K.BO_KERNEL_BLOCKED
     finally:
         os.environ.pop("BENOR_NO_MFMA", None)
+    os.environ["BENOR_NO_MFMA_BIG"] = "1"
+    try:
+        assert K.kernel_for(1024, 341) == K.BO_KERNEL_MFMA
+        assert K.kernel_for(2048, 682) == K.BO_KERNEL_W
+        assert K.kernel_for(4096, 1365) == K.BO_KERNEL_BLOCKED
+    finally:
+        os.environ.pop("BENOR_NO_MFMA_BIG", None)
 
 
 def test_kernel_choice_validates_like_plan_create():
@@ -211,6 +220,54 @@ def test_mfma_deferral_equals_popcount_kernel(N, F, T):
     np.testing.assert_array_equal(ha, b.run(11, T))
     cut = T // 3 + 5
     np.testing.assert_array_equal(ha, a.run(11, cut) + a.run(11 + cut, T - cut))
+
+
+def big_shapes():
+    """1024 < m <= 4096 (W = 17..64, the big-network form): every KIND, both
+    m parities, tile-pair parity (odd ceil(m/32)), W kernel (W <= 32) and
+    blocked kernel (W > 32) for the deferred trials."""
+    return [(1100, 0), (1537, 512), (1600, 500), (2047, 1), (2048, 682), (2080, 1000), (2731, 0),
+            (3000, 999), (3333, 1500), (4096, 1365), (4096, 0), (4000, 1900), (4095, 1), (2049, 1024)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,F", big_shapes())
+def test_mfma_big_matches_oracle(N, F):
+    seed = (N * 131 + F) & 0xFFFF
+    T = 333 + (N % 61)
+    begin = (1 << 35) + N
+    p = plan(N, F, seed=seed, k_max=10)
+    assert p.kernel == benor.BO_KERNEL_MFMA
+    got = p.run(begin, T)
+    ref = oracle.run_trials(N, F, first_f(N, F), seed=seed, trial_begin=begin, trial_count=T, k_max=10)
+    np.testing.assert_array_equal(got, ref.hist)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,F,T", [(2048, 0, 300_000), (4096, 1365, 200_001), (3000, 1400, 250_000), (1500, 200, 400_000)])
+def test_mfma_big_equals_popcount_kernels(N, F, T):
+    a = plan(N, F, True, seed=17, k_max=16)
+    os.environ["BENOR_NO_MFMA_BIG"] = "1"
+    try:
+        b = benor.TrialsPlan(N, F, seed=17, k_max=16)
+    finally:
+        os.environ.pop("BENOR_NO_MFMA_BIG", None)
+    assert a.kernel == benor.BO_KERNEL_MFMA and b.kernel != benor.BO_KERNEL_MFMA
+    np.testing.assert_array_equal(a.run(3, T), b.run(3, T))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,F,q", [(2000, 600, 1), (4096, 1000, 2), (1500, 700, 3)])
+def test_mfma_big_fixed_init_matches_oracle(N, F, q):
+    rng = np.random.default_rng(N + 7 * q)
+    vals = [int(v) for v in rng.integers(0, 2, N)]
+    for j in rng.choice(np.arange(F, N), q, replace=False):
+        vals[j] = "?"
+    p = plan(N, F, seed=23, k_max=8, initial_values=vals)
+    got = p.run(1, 200)
+    ref = oracle.run_trials(N, F, first_f(N, F), seed=23, trial_begin=1, trial_count=200, k_max=8,
+                            initial_values=vals)
+    np.testing.assert_array_equal(got, ref.hist)
 
 
 @pytest.mark.gpu
