@@ -18,6 +18,7 @@ constexpr uint32_t kStreamOrder = 3u;
 constexpr uint32_t kStreamCrash = 4u;
 
 constexpr int kWavesPerBlock = 4;          // 256-thread workgroups, one trial per wave
+
 constexpr uint32_t kMaxW = BO_MAX_N / 64;  // u64 words per bit plane at N = 4096
 constexpr int kMaxWSpecialised = 32;       // m <= 2048: fully unrolled W-specialised kernel
 constexpr uint32_t kMaxLaneM = 64;         // m <= 64: lane kernel, one trial per lane (benor_lane.h)
@@ -101,10 +102,13 @@ hipError_t launch_lane_m(const KParams &p, int grid_blocks, hipStream_t stream);
 template <int W>
 hipError_t launch_mfma(const KParams &p, int grid_blocks, hipStream_t stream);
 hipError_t launch_mfma_big(const KParams &p, int grid_blocks, hipStream_t stream);
-uint32_t mfma_big_lds_bytes(const KParams &p);   // dynamic LDS of one workgroup of the big form
+uint32_t mfma_big_lds_bytes(const KParams &p, uint32_t block_waves);   // dynamic LDS of one workgroup of the big form
+uint32_t mfma_big_block_waves(const KParams &p);                       // its waves per workgroup (1, 2 or 4)
 
-// Grid size that fills the current device for this configuration.
+// Grid size that fills the current device for this configuration, in
+// workgroups of block_waves(p) waves.
 int lockstep_grid(const KParams &p, int device);
+uint32_t block_waves(const KParams &p);
 
 // Matrix-core microbenchmark: e2m1 32x32x64 multiply-adds executed per launch.
 hipError_t launch_mfma_peak(float *sink, int grid_blocks, int iters, hipStream_t stream, double *terms_per_launch);

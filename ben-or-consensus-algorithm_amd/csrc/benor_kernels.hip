@@ -864,6 +864,13 @@ hipError_t launch_lockstep(const KParams &p, int grid, hipStream_t s) {
   return dispatch_b(p, grid, s, std::make_integer_sequence<int, 12>{});
 }
 
+// The big-network matrix-core kernel holds 9-33 KB of LDS per wave; its
+// workgroup size is chosen for occupancy (mfma_big_block_waves).  Every other
+// kernel: kWavesPerBlock.
+uint32_t block_waves(const KParams &p) {
+  return (p.variant == 7 && p.W > 16u && !p.node_out && !p.rounds_out) ? mfma_big_block_waves(p) : (uint32_t)kWavesPerBlock;
+}
+
 int lockstep_grid(const KParams &p, int device) {
   int cus = 256;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
@@ -873,14 +880,15 @@ int lockstep_grid(const KParams &p, int device) {
     if (blocks_needed < grid) grid = blocks_needed;
     return (int)(grid < 1 ? 1 : grid);
   }
-  // 8 workgroups (32 waves) per CU when registers and LDS allow it.
+  // 32 waves per CU when registers and LDS allow it.
   const bool mfma = p.variant == 7 && !p.node_out && !p.rounds_out;
   const uint64_t per_wave = p.variant == 6 ? 64u : (mfma ? 32u : 1u);   // trials a wave runs at once
   const uint64_t waves_needed = (p.trial_count + per_wave - 1u) / per_wave;
-  const uint64_t blocks_needed = (waves_needed + kWavesPerBlock - 1) / kWavesPerBlock;
-  uint64_t per_cu = 8;
+  const uint32_t bw = block_waves(p);
+  const uint64_t blocks_needed = (waves_needed + bw - 1) / bw;
+  uint64_t per_cu = 32u / bw;
   // the matrix-core kernel uses no wave slices (its big-network form: proposal planes)
-  const uint32_t lds = mfma ? (p.W > 16u ? mfma_big_lds_bytes(p) : p.hist_bytes) : p.lds_bytes;
+  const uint32_t lds = mfma ? (p.W > 16u ? mfma_big_lds_bytes(p, bw) : p.hist_bytes) : p.lds_bytes;
   if (lds > 0) {
     const uint64_t lds_fit = (160u * 1024u) / lds;
     if (lds_fit < per_cu) per_cu = lds_fit ? lds_fit : 1;

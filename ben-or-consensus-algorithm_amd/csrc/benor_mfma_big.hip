@@ -15,8 +15,9 @@
 //    as KIND 1, 2 of benor_mfma.h) keep their sign bits, four nibble words
 //    folding into one 32-bit word (bit 4i + 3 - s of word s), so the P-phase
 //    counts c0 = the receivers whose proposal is 0 (node.ts:63-69);
-//  * two receiver tiles run side by side on one expanded operand (two
-//    independent accumulator chains: half the expansion VALU per product).
+//  * NT receiver tiles run side by side on one expanded operand (NT
+//    independent accumulator chains: 1/NT of the expansion VALU and LDS
+//    reads per product).
 // The layout of accumulators, trial columns and thresholds is benor_mfma.h's;
 // the P-phase thresholds are on c0 (A scale 2^0, or 2^1 for KIND 2):
 //  KIND 0, 1: acc = c0 - F - 0.5, negative exactly when c0 <= F: with no "?"
@@ -31,15 +32,18 @@
 namespace benor {
 
 constexpr uint32_t kBigMaxW = kMaxW;   // 64 chunks at N = 4096
+#ifndef BENOR_BIG_NT
+#define BENOR_BIG_NT 4                  // receiver tiles per expanded operand
+#endif
 
 // Words per lane of a wave's x plane: the W x1 words rounded up to whole
 // Philox blocks per lane half (4 words each); the slice adds the KP <= W
-// proposal words.
+// proposal words (+1: a tile block may fill word KP when KP is odd).
 __host__ __device__ constexpr uint32_t big_plane_words(uint32_t W) { return 4u * ((((W + 1u) >> 1) + 1u) >> 1); }
-__host__ __device__ constexpr uint32_t big_slice_words(uint32_t W) { return big_plane_words(W) + W; }
+__host__ __device__ constexpr uint32_t big_slice_words(uint32_t W) { return big_plane_words(W) + W + 1u; }
 
-template <int KIND>
-__global__ void __launch_bounds__(256) benor_mfma_big_kernel(KParams p) {
+template <int KIND, int NT, int BW>
+__global__ void __launch_bounds__(64 * BW) benor_mfma_big_kernel(KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t lane = threadIdx.x & 63u, h = lane >> 5;
   const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -83,12 +87,13 @@ __global__ void __launch_bounds__(256) benor_mfma_big_kernel(KParams p) {
   const int last_bits = (int)m - 32 * (2 * ((int)W - 1) + (int)h);
   const uint32_t last_mask = last_bits >= 32 ? ~0u : (last_bits <= 0 ? 0u : ((1u << last_bits) - 1u));
 
-  mf_v4i ones0 = {0x22222222, 0x22222222, 0x22222222, 0x22222222};
-  mf_v4i ones1 = ones0;
+  mf_v4i ones[NT];                             // one opaque copy per tile: no two tiles' products merge
+#pragma unroll
+  for (int u = 0; u < NT; ++u) ones[u] = mf_v4i{0x22222222, 0x22222222, 0x22222222, 0x22222222};
   uint32_t f_all = 0, f_1 = 0, f_2 = 0;
   const uint32_t ngroups = (trial_count + 31u) >> 5;
-  const uint32_t waves_total = gridDim.x * kWavesPerBlock;
-  const uint32_t wave_id = blockIdx.x * kWavesPerBlock + wv;
+  const uint32_t waves_total = gridDim.x * BW;
+  const uint32_t wave_id = blockIdx.x * BW + wv;
   uint32_t n_def = 0;
   uint32_t *seg = KIND == 0 ? nullptr : p.defer_seg + (size_t)wave_id * p.defer_seg_cap;
   for (uint32_t g = wave_id; g < ngroups; g += waves_total) {
@@ -119,65 +124,68 @@ __global__ void __launch_bounds__(256) benor_mfma_big_kernel(KParams p) {
     }
     X[(W - 1u) * 64u + lane] &= last_mask;
 
-    // ---- R-phase (node.ts:46-82): tiles i, i + 1 on the same expanded x
+    // ---- R-phase (node.ts:46-82): NT receiver tiles on each expanded x
     // chunk; proposals to LDS as sign bits (1 = proposal 0).
     uint32_t qz = 0u;
-    for (uint32_t i = 0; i < MT; i += 2u) {
-      asm volatile("" : "+v"(ones0), "+v"(ones1));
-      mf_v16f acc0, acc1;
+    for (uint32_t i = 0; i < MT; i += (uint32_t)NT) {
+      mf_v16f acc[NT];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) acc0[j] = acc1[j] = bias_r;
+      for (int u = 0; u < NT; ++u) {
+        asm volatile("" : "+v"(ones[u]));
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[u][j] = bias_r;
+      }
       for (uint32_t c = 0; c < W; ++c) {
         const mf_v4i b = expand_votes(X[c * 64u + lane]);
-        acc0 = mfma_count<4>(ones0, b, acc0);
-        acc1 = mfma_count<4>(ones1, b, acc1);
+#pragma unroll
+        for (int u = 0; u < NT; ++u) acc[u] = mfma_count<4>(ones[u], b, acc[u]);
       }
-      // nibble masks of the two tiles: full, the last (partial) tile, or none (past MT)
-      const uint32_t m00 = i < MT - 1u ? ~0u : tail0, m01 = i < MT - 1u ? ~0u : tail1;
-      const uint32_t m10 = i + 1u < MT - 1u ? ~0u : (i + 1u == MT - 1u ? tail0 : 0u);
-      const uint32_t m11 = i + 1u < MT - 1u ? ~0u : (i + 1u == MT - 1u ? tail1 : 0u);
-      const uint32_t n0 = pack_fp4_8(acc0, 0) & m00, n1 = pack_fp4_8(acc0, 8) & m01;
-      const uint32_t n2 = pack_fp4_8(acc1, 0) & m10, n3 = pack_fp4_8(acc1, 8) & m11;
-      if constexpr (KIND > 0)                  // a live "?" nibble is 0: bit 1 clear
-        qz |= (~n0 & m00 & 0x22222222u) | (~n1 & m01 & 0x22222222u) | (~n2 & m10 & 0x22222222u) |
-              (~n3 & m11 & 0x22222222u);
-      const uint32_t s = 0x88888888u;
-      PL[(i >> 1) * 64u + lane] = (n0 & s) | ((n1 & s) >> 1) | ((n2 & s) >> 2) | ((n3 & s) >> 3);
+#pragma unroll
+      for (int q = 0; q < NT / 2; ++q) {      // tile pair (i + 2q, i + 2q + 1) -> proposal word (i >> 1) + q
+        uint32_t n[4];
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+          const uint32_t ti = i + 2u * q + v;  // nibble masks: full, the last (partial) tile, or none (past MT)
+          const uint32_t k0 = ti < MT - 1u ? ~0u : (ti == MT - 1u ? tail0 : 0u);
+          const uint32_t k1 = ti < MT - 1u ? ~0u : (ti == MT - 1u ? tail1 : 0u);
+          n[2 * v] = pack_fp4_8(acc[2 * q + v], 0) & k0;
+          n[2 * v + 1] = pack_fp4_8(acc[2 * q + v], 8) & k1;
+          if constexpr (KIND > 0)              // a live "?" nibble is 0: bit 1 clear
+            qz |= (~n[2 * v] & k0 & 0x22222222u) | (~n[2 * v + 1] & k1 & 0x22222222u);
+        }
+        const uint32_t s = 0x88888888u;
+        PL[((i >> 1) + q) * 64u + lane] = (n[0] & s) | ((n[1] & s) >> 1) | ((n[2] & s) >> 2) | ((n[3] & s) >> 3);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
 
     // ---- P-phase (node.ts:83-158): every receiver tile counts the 0-proposals
     float mn = __builtin_inff(), mx = -__builtin_inff(), ma = __builtin_inff();
-    for (uint32_t i = 0; i < MT; i += 2u) {
-      asm volatile("" : "+v"(ones0), "+v"(ones1));
+    for (uint32_t i = 0; i < MT; i += (uint32_t)NT) {
       const float nanf = __builtin_nanf("");
-      mf_v16f acc0, acc1;
+      mf_v16f acc[NT];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {           // rows with no receiver start at NaN: the reductions skip them
-        const bool l0 = i < MT - 1u || ((live_last >> j) & 1u);
-        const bool l1 = i + 1u < MT - 1u || (i + 1u == MT - 1u && ((live_last >> j) & 1u));
-        acc0[j] = l0 ? bias_p : nanf;
-        acc1[j] = l1 ? bias_p : nanf;
+      for (int u = 0; u < NT; ++u) {
+        asm volatile("" : "+v"(ones[u]));
+        const uint32_t ti = i + u;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {         // rows with no receiver start at NaN: the reductions skip them
+          const bool live = ti < MT - 1u || (ti == MT - 1u && ((live_last >> j) & 1u));
+          acc[u][j] = live ? bias_p : nanf;
+        }
       }
       for (uint32_t k = 0; k < KP; ++k) {
         const mf_v4i b = expand_votes(PL[k * 64u + lane]);
-        if constexpr (KIND == 2) {
-          acc0 = mfma_count<1>(ones0, b, acc0);
-          acc1 = mfma_count<1>(ones1, b, acc1);
-        } else {
-          acc0 = mfma_count(ones0, b, acc0);
-          acc1 = mfma_count(ones1, b, acc1);
-        }
+#pragma unroll
+        for (int u = 0; u < NT; ++u) acc[u] = KIND == 2 ? mfma_count<1>(ones[u], b, acc[u]) : mfma_count(ones[u], b, acc[u]);
       }
 #pragma unroll
-      for (int j = 0; j < 16; j += 2) {
-        mn = fminf(fminf(mn, acc0[j]), acc0[j + 1]);
-        mx = fmaxf(fmaxf(mx, acc0[j]), acc0[j + 1]);
-        mn = fminf(fminf(mn, acc1[j]), acc1[j + 1]);
-        mx = fmaxf(fmaxf(mx, acc1[j]), acc1[j + 1]);
-        if constexpr (KIND == 2) {
-          ma = fminf(fminf(ma, __builtin_fabsf(acc0[j])), __builtin_fabsf(acc0[j + 1]));
-          ma = fminf(fminf(ma, __builtin_fabsf(acc1[j])), __builtin_fabsf(acc1[j + 1]));
+      for (int u = 0; u < NT; ++u) {
+#pragma unroll
+        for (int j = 0; j < 16; j += 2) {
+          mn = fminf(fminf(mn, acc[u][j]), acc[u][j + 1]);
+          mx = fmaxf(fmaxf(mx, acc[u][j]), acc[u][j + 1]);
+          if constexpr (KIND == 2) ma = fminf(fminf(ma, __builtin_fabsf(acc[u][j])), __builtin_fabsf(acc[u][j + 1]));
         }
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -223,25 +231,53 @@ __global__ void __launch_bounds__(256) benor_mfma_big_kernel(KParams p) {
   }
 }
 
-uint32_t mfma_big_lds_bytes(const KParams &p) { return p.hist_bytes + kWavesPerBlock * big_slice_words(p.W) * 64u * 4u; }
+uint32_t mfma_big_lds_bytes(const KParams &p, uint32_t bw) { return p.hist_bytes + bw * big_slice_words(p.W) * 64u * 4u; }
 
-template <int KIND>
+// Waves per workgroup: the most resident waves per CU -- LDS (160 KB) against
+// the ~2 waves/SIMD its registers allow -- with ties to larger workgroups,
+// which spread over the CU's four SIMDs.  (Measured at NT = 4: 1-wave groups
+// +22 % at N=4096, F=1365, where LDS admits 7 single waves but one 4-wave
+// group; -10..-30 % where both fill the CU.)
+uint32_t mfma_big_block_waves(const KParams &p) {
+  constexpr uint32_t kRegWaves = 8;          // per CU at ~184 VGPRs (2 per SIMD)
+  uint32_t best = 4, best_waves = 0;
+  for (uint32_t bw = 4; bw >= 1; bw >>= 1) {
+    uint32_t w = (160u * 1024u) / mfma_big_lds_bytes(p, bw) * bw;
+    if (w > kRegWaves) w = kRegWaves;
+    if (w > best_waves) {
+      best_waves = w;
+      best = bw;
+    }
+  }
+  return best;
+}
+
+template <int KIND, int BW>
 static hipError_t launch_big_kind(const KParams &p, int grid, hipStream_t s) {
-  const uint32_t lds = mfma_big_lds_bytes(p);
+  constexpr int NT = BENOR_BIG_NT;
+  const uint32_t lds = mfma_big_lds_bytes(p, BW);
   if (lds > 64u * 1024u) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&benor_mfma_big_kernel<KIND>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&benor_mfma_big_kernel<KIND, NT, BW>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(benor_mfma_big_kernel<KIND>, dim3(grid), dim3(64 * kWavesPerBlock), lds, s, p);
+  hipLaunchKernelGGL((benor_mfma_big_kernel<KIND, NT, BW>), dim3(grid), dim3(64 * BW), lds, s, p);
   return hipGetLastError();
+}
+
+template <int KIND>
+static hipError_t launch_big_bw(const KParams &p, int grid, hipStream_t s) {
+  const uint32_t bw = mfma_big_block_waves(p);
+  if (bw == 4u) return launch_big_kind<KIND, 4>(p, grid, s);
+  if (bw == 2u) return launch_big_kind<KIND, 2>(p, grid, s);
+  return launch_big_kind<KIND, 1>(p, grid, s);
 }
 
 hipError_t launch_mfma_big(const KParams &p, int grid, hipStream_t s) {
   if (p.W < 17u || p.W > kBigMaxW) return hipErrorInvalidValue;
-  if (p.G == 0u) return launch_big_kind<0>(p, grid, s);
-  if (p.G == 1u) return launch_big_kind<1>(p, grid, s);
-  return launch_big_kind<2>(p, grid, s);
+  if (p.G == 0u) return launch_big_bw<0>(p, grid, s);
+  if (p.G == 1u) return launch_big_bw<1>(p, grid, s);
+  return launch_big_bw<2>(p, grid, s);
 }
 
 }  // namespace benor

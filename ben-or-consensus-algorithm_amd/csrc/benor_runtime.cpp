@@ -440,7 +440,7 @@ static int plan_launch_impl(bo_plan *pl, uint64_t trial_begin, uint64_t trial_co
     const uint64_t cap = std::min<uint64_t>(trial_count, benor::kDeferChunk);
     kp.trial_count = cap;
     const int grid = benor::lockstep_grid(kp, pl->device);
-    const uint64_t waves = (uint64_t)grid * benor::kWavesPerBlock;
+    const uint64_t waves = (uint64_t)grid * benor::block_waves(kp);
     const uint64_t seg_cap = ((cap + 31u) / 32u + waves - 1u) / waves * 32u;   // a wave's trials per launch, at most
     const uint64_t words = cap + 64u + waves * seg_cap;                        // list, its length (padded), segments
     if (pl->defer_words < words) {
