@@ -893,6 +893,22 @@ int lockstep_grid(const KParams &p, int device) {
     const uint64_t lds_fit = (160u * 1024u) / lds;
     if (lds_fit < per_cu) per_cu = lds_fit ? lds_fit : 1;
   }
+  // Lane kernel, general case (KIND 0: coin rounds, so a geometric number of
+  // rounds per trial): a wave ends with its slowest queued trial, so a short
+  // launch spread over every wave slot (~2 trials per lane at 10^6 trials)
+  // spends most of its time in that tail.  Fewer, longer-lived waves: at
+  // least ~8 trials per lane, 2..8 workgroups per CU (tools/lane_grid_sweep.py,
+  // N=10 F=4 at 10^6 trials: 8 per CU 41-57 us, 2 per CU 25 us; at 10^7
+  // trials 8 per CU stays best).
+  if (p.variant == 6 && p.G == 0u) {
+    const uint64_t want = p.trial_count / ((uint64_t)cus * 64u * kWavesPerBlock * 8u);
+    const uint64_t v = want < 2u ? 2u : want;
+    if (v < per_cu) per_cu = v;
+  }
+  if (const char *ev = getenv("BENOR_BLOCKS_PER_CU")) {   // tuning knob (tools/lane_grid_sweep.py)
+    const uint64_t v = strtoull(ev, nullptr, 10);
+    if (v >= 1u && v < per_cu) per_cu = v;
+  }
   uint64_t grid = (uint64_t)cus * per_cu;
   if (blocks_needed < grid) grid = blocks_needed;
   if (grid < 1) grid = 1;

@@ -154,11 +154,11 @@ __global__ void __launch_bounds__(256) benor_mfma_kernel(KParams p) {
   const float dec_thr = 6.0f * (float)(2u * p.F - m) + 3.0f;   // KIND 2: |acc| > dec_thr <=> decided
   mf_v16f cr, cp, cp_tail;
   // Receiver rows of the last tile that exist: nibble masks for its packed
-  // R-phase results; KIND 0 masks its P-phase results per register (vbits),
-  // KIND 1, 2 start them from NaN where no receiver exists, which
-  // v_min3_f32 / v_max3_f32 skip (IEEE minNum / maxNum).
+  // R-phase results; KIND 1, 2 start their P-phase results from NaN where no
+  // receiver exists, which v_min3_f32 / v_max3_f32 skip (IEEE minNum /
+  // maxNum).  KIND 0 needs no mask there (see the P-phase).
   const uint32_t mrem = m - 32u * (uint32_t)(MT - 1);   // 1..32
-  uint32_t tail0 = 0, tail1 = 0, vbits = 0;
+  uint32_t tail0 = 0, tail1 = 0;
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
     const uint32_t row = (uint32_t)((j & 3) + 8 * (j >> 2)) + 4u * h;
@@ -166,7 +166,6 @@ __global__ void __launch_bounds__(256) benor_mfma_kernel(KParams p) {
     cr[j] = bias_r;
     cp[j] = bias_p;
     cp_tail[j] = live ? bias_p : __builtin_nanf("");
-    if (live) vbits |= 1u << j;
     const uint32_t nib = !live ? 0u : SURE ? ((j & 4) ? 0x20u : 0x02u) << (8 * (j & 3)) : 0xFu << (4 * (j & 7));
     if (j < 8) tail0 |= nib;
     else tail1 |= nib;
@@ -273,17 +272,16 @@ __global__ void __launch_bounds__(256) benor_mfma_kernel(KParams p) {
         mf_v16f acc = mfma_count(ones, pb[0], cp);
 #pragma unroll
         for (int c = 1; c < KP; ++c) acc = mfma_count(ones, pb[c], acc);
+        // Padded receiver rows of the last tile need no mask here: A is all
+        // ones on every row and C is the same bias, so a padded row computes
+        // exactly the count of the live rows of its trial column (the padded
+        // senders are masked out of the operand).  Folding it in changes
+        // neither the OR nor the AND of the sign bits (r02: N=256 +6 %).
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
           const uint32_t u = __float_as_uint(acc[j]);
-          if (i < MT - 1) {
-            s_or |= u;
-            s_and &= u;
-          } else {
-            const bool live = (vbits >> j) & 1u;
-            s_or |= live ? u : 0u;
-            s_and &= live ? u : ~0u;
-          }
+          s_or |= u;
+          s_and &= u;
         }
         asm volatile("" : "+v"(s_or), "+v"(s_and));   // fold tile by tile: one accumulator live
         __builtin_amdgcn_sched_barrier(0);

@@ -17,13 +17,15 @@ depends only on the set of trial ids, never on the GPU count (`hist_sha256`).
 value  = live node-rounds simulated by all ranks / timed seconds (max over ranks)
          (a live node-round = one live node executing one R-phase and one
          P-phase: SURVEY §8d primary count)
-roofline: per-receiver tally popcount words per live node-round (m = N - F
-         live nodes: c1 in the R-phase; c1 in the P-phase when the binary vote
-         count is odd -- no "?" proposal, c0 = m - c1 -- else c0 and c1: 2 or
-         3 * ceil(m/32), 44 at the bench shape) / average kernel
-         duration from HIP events on the launch stream, against the gfx950
-         v_bcnt_u32_b32 issue peak (256 CU x 4 SIMD x 16 lanes x 2.4 GHz =
-         39.3 T words/s).
+roofline: of the kernel the plan picked, from the average kernel duration
+         (HIP events on the launch stream).  The bench shape runs the
+         matrix-core kernel: algorithmic e2m1 FLOP/s -- every
+         live receiver sums the m live votes in each phase, 4m FLOP per live
+         node-round -- against the dense FP4 peak (~10 PFLOP/s).  With
+         BENOR_NO_MFMA=1 it runs the popcount W kernel: tally popcount words
+         per live node-round (2 or 3 * ceil(m/32), 44 at the bench shape;
+         DESIGN.md §4) against the v_bcnt_u32_b32 issue peak (256 CU x 4 SIMD
+         x 16 lanes x 2.4 GHz = 39.3 T words/s).
 cpu_baseline: the oracle's bit-plane restatement (oracle/benor_oracle.c,
          OpenMP over trials) on a bounded sample, rank 0 at N = 1 only, on
          every host thread and on one core.
@@ -146,6 +148,7 @@ def launch_ranks(n, argv):
 # reported beside the headline, not part of `value`.
 OTHER_CONFIGS = [("C2 N=10,F=4", 10, 4, 1_000_000), ("C2 N=10,F=5 (F>N/2, no decision)", 10, 5, 1_000_000),
                  ("C3 N=256,F=85", 256, 85, 10_000_000)]
+OTHER_REPS = 10          # back-to-back launches per config, each of its T trials
 
 
 def other_configs(benor, torch, k_max, seed):
@@ -172,16 +175,22 @@ def other_configs(benor, torch, k_max, seed):
         plan.launch(0, T, h.data_ptr(), stream.cuda_stream)          # warm-up launch
         torch.cuda.synchronize()
         h.zero_()
+        # A launch of 10^6 trials lasts tens of microseconds: timed alone, the
+        # host's enqueue latency after the start event would count as kernel
+        # time.  So OTHER_REPS launches of T distinct trials each go back to back
+        # between the events, and kernel_ms is their average.
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
-        plan.launch(T, T, h.data_ptr(), stream.cuda_stream)
+        for r in range(OTHER_REPS):
+            plan.launch((1 + r) * T, T, h.data_ptr(), stream.cuda_stream)
         e1.record(stream)
         torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1)
+        ms = e0.elapsed_time(e1) / OTHER_REPS
         hist = h.cpu().numpy().astype(np.uint64)
         m = plan.live_nodes
-        nr, rounds = node_rounds(hist, m, k_max)
-        undecided = int(hist[0] + hist[1] + hist[2])
+        nr, rounds = node_rounds(hist, m, k_max)             # per launch: the histogram holds OTHER_REPS launches
+        nr, rounds = nr / OTHER_REPS, rounds / OTHER_REPS
+        undecided = int(hist[0] + hist[1] + hist[2]) // OTHER_REPS
         words = plan.popc_words_per_node_round
         if plan.kernel == benor.BO_KERNEL_MFMA:
             roof = mfma_roofline(m, nr, ms * 1e-3)
@@ -199,14 +208,14 @@ def other_configs(benor, torch, k_max, seed):
         if plan.kernel != benor.BO_KERNEL_MFMA:
             roof["peak"] = SPEC_PEAK_POPC / 1e12
             roof["frac"] = roof["achieved"] / roof["peak"]
-        out[name] = {"trials": T, "kernel_ms": ms, "node_rounds_per_s": nr / (ms * 1e-3),
+        out[name] = {"trials": T, "launches_timed": OTHER_REPS, "kernel_ms": ms, "node_rounds_per_s": nr / (ms * 1e-3),
                      "trials_per_s": T / (ms * 1e-3), "mean_rounds": rounds / T, "undecided_trials": undecided,
                      "roofline": roof}
         if ms < 1.0:
             # a launch this short is mostly ramp-up: also time 20x the trials for the steady state
             h.zero_()
             e0.record(stream)
-            plan.launch(2 * T, 20 * T, h.data_ptr(), stream.cuda_stream)
+            plan.launch((1 + OTHER_REPS) * T, 20 * T, h.data_ptr(), stream.cuda_stream)
             e1.record(stream)
             torch.cuda.synchronize()
             ms20 = e0.elapsed_time(e1)
