@@ -405,6 +405,19 @@ def main():
             traffic=traffic, kernel_ms=float(np.mean(kern_ms)),
             peak_probe=(peak_measured / 1e12) if peak_measured else None, kernel_version=kver,
             kernel=benor.KERNEL_NAMES.get(plan.kernel, str(plan.kernel))),
+        # BASELINE's metric asks for % of the INT/popcount roofline.  The bench
+        # kernel runs on the matrix cores instead, so this states the rate
+        # against that ceiling: the v_bcnt issue peak over the popcount words a
+        # live node-round needs -- SURVEY §8d's 4*ceil(N/32) (128 at N=1024) and
+        # the compact planes' 2 or 3*ceil(m/32) (44 at m=683).
+        "int_popcount_ceiling": {
+            "peak_popc_words_per_s": SPEC_PEAK_POPC,
+            "survey_words_per_node_round": 4 * ((N + 31) // 32),
+            "survey_ceiling_node_rounds_per_s": SPEC_PEAK_POPC / (4 * ((N + 31) // 32)),
+            "compact_words_per_node_round": words_per_nr,
+            "compact_ceiling_node_rounds_per_s": SPEC_PEAK_POPC / words_per_nr,
+            "value_over_survey_ceiling": value / (world * SPEC_PEAK_POPC / (4 * ((N + 31) // 32))),
+            "value_over_compact_ceiling": value / (world * SPEC_PEAK_POPC / words_per_nr)},
         "all_node_rounds_per_s": rounds * N / elapsed,
         "trials_per_s": total_trials / elapsed,
         "agreement_violations": int(h[-1]),

@@ -18,7 +18,10 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
   python3 "$R/bench.py" $BENCH_ARGS > "$OUT/trace_bench.log" 2>&1; chk $? kernel-trace
 tail -2 "$OUT/trace_bench.log"
 i=0
-for grp in ${PMC_GROUPS:-"SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT" "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INST_CYCLES_VMEM SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA" "FETCH_SIZE" "WRITE_SIZE"}; do
+# PMC_GROUPS: counter groups separated by '|', one rocprofv3 pass each
+GROUPS_STR=${PMC_GROUPS:-"SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT|SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INST_CYCLES_VMEM SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA|FETCH_SIZE|WRITE_SIZE"}
+IFS='|' read -r -a GROUPS_ARR <<< "$GROUPS_STR"
+for grp in "${GROUPS_ARR[@]}"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d "$OUT/pmc$i" -o pmc -- \
     python3 "$R/bench.py" $PMC_ARGS > "$OUT/pmc$i.log" 2>&1; chk $? "pmc$i ($grp)"

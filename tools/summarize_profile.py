@@ -72,6 +72,16 @@ def main(tag, trials, N=1024, F=341):
         lines += ["", f"- v_bcnt per trial (one round; {per}W words per receiver group x W groups, W = ceil(m/64)): {bcnt}",
                   f"- VALU instructions per trial: {c['SQ_INSTS_VALU'] / trials:.1f} "
                   f"(non-v_bcnt: {c['SQ_INSTS_VALU'] / trials - bcnt:.1f})"]
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in c and "GRBM_GUI_ACTIVE" in c:
+        cyc = c["GRBM_GUI_ACTIVE"] / 8.0          # GRBM counts per XCD; 8 XCDs
+        simd_cycles = cyc * 1024.0                # 256 CU x 4 SIMD
+        lines += [f"- kernel cycles (GRBM_GUI_ACTIVE / 8 XCDs): {cyc:.4g}",
+                  f"- matrix-core busy: {c['SQ_VALU_MFMA_BUSY_CYCLES'] / simd_cycles:.3f} of SIMD-cycles "
+                  f"(SQ_VALU_MFMA_BUSY_CYCLES = 32 x SQ_INSTS_MFMA: "
+                  f"{c['SQ_VALU_MFMA_BUSY_CYCLES'] / max(1.0, c.get('SQ_INSTS_MFMA', 0.0)):.1f} per instruction)",
+                  f"- VALU co-executing with the matrix core: {c.get('SQ_VALU_MFMA_COEXEC_CYCLES', 0.0) / simd_cycles:.3f} "
+                  f"of SIMD-cycles ({c.get('SQ_VALU_MFMA_COEXEC_CYCLES', 0.0) / c['SQ_VALU_MFMA_BUSY_CYCLES']:.3f} "
+                  f"of the busy cycles)"]
     if "GRBM_GUI_ACTIVE" in c and stats:
         for r in csv.DictReader(open(stats[0])):
             if any(k in r["Name"] for k in KERNELS):
