@@ -41,17 +41,31 @@
 
 namespace benor {
 
-// One receiver's tally (node.ts:56-62, :92-98) over a 32- or 64-bit plane.
-__device__ __forceinline__ uint32_t own_count(uint32_t plane) {
+// One receiver's tally (node.ts:56-62, :92-98) over a 32- or 64-bit plane,
+// offset by acc: popcount(plane) + acc (mod 2^32).  With acc = -T the sign bit
+// of the result is (count < T), the receiver's comparison against a
+// threshold in the same instruction.  asm volatile: the m identical lockstep
+// counts of a trial are never merged (SURVEY §7 "symmetry trap").
+__device__ __forceinline__ uint32_t own_count(uint32_t plane, uint32_t acc) {
   uint32_t r;
-  asm volatile("v_bcnt_u32_b32 %0, %1, 0" : "=v"(r) : "v"(plane));
+  asm volatile("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(plane), "v"(acc));
   return r;
 }
-__device__ __forceinline__ uint32_t own_count(uint64_t plane) {
+__device__ __forceinline__ uint32_t own_count(uint64_t plane, uint32_t acc) {
   uint32_t r;
-  asm volatile("v_bcnt_u32_b32 %0, %1, 0\n\tv_bcnt_u32_b32 %0, %2, %0" : "=&v"(r) : "v"((uint32_t)plane),
+  asm volatile("v_bcnt_u32_b32 %0, %1, %2\n\tv_bcnt_u32_b32 %0, %3, %0" : "=&v"(r) : "v"((uint32_t)plane), "v"(acc),
                "v"((uint32_t)(plane >> 32)));
   return r;
+}
+
+// Receiver planes are built one receiver at a time, c = m-1 down to 0: the
+// plane shifts left by one and takes the sign bit of the receiver's result
+// (v_alignbit_b32: (plane << 1) | (r >> 31)), so after m receivers receiver c
+// sits at bit c.
+__device__ __forceinline__ void shift_in(uint32_t &plane, uint32_t r) { plane = __builtin_amdgcn_alignbit(plane, r, 31); }
+__device__ __forceinline__ void shift_in(uint64_t &plane, uint32_t r) {
+  const uint32_t lo = (uint32_t)plane, hi = (uint32_t)(plane >> 32);
+  plane = ((uint64_t)__builtin_amdgcn_alignbit(hi, lo, 31) << 32) | __builtin_amdgcn_alignbit(lo, r, 31);
 }
 
 template <int MM, int KIND>
@@ -133,45 +147,54 @@ __global__ void __launch_bounds__(256) benor_lane_kernel(KParams p) {
     if (!act) continue;
 
     ++r;
+    // Every receiver c compares its own counts against the thresholds of
+    // node.ts in the count instruction itself (own_count with acc = -T: sign
+    // bit = count < T) and shifts the sign bits into receiver planes; the
+    // decisions are then combined plane-wide, once per round.
     if (KIND == 2) {
-      // M odd, m > 2F: proposal = majority (c1 > M/2, node.ts:63-69); every
-      // P-phase vote is binary (c0 = m - c1) and every receiver decides:
-      // c1 >= m - F (> F) -> 1, else c0 > F -> 0 (node.ts:99-105)
-      const uint32_t hiT = (r == 1u ? M1 : (uint32_t)MM) >> 1;
-      Plane p1 = 0;
+      // M odd, m > 2F: proposal = majority, p0 = (c1 <= M/2) (node.ts:63-69);
+      // every P-phase vote is binary and every receiver decides: x = 1 iff
+      // c0 <= F, i.e. c1 >= m - F > F (node.ts:99-105)
+      const uint32_t nT = 0u - (((r == 1u ? M1 : (uint32_t)MM) >> 1) + 1u);
+      Plane p0 = 0;
 #pragma unroll
-      for (int c = MM - 1; c >= 0; --c) p1 = p1 + p1 + (own_count(x1) > hiT ? 1u : 0u);
+      for (int c = MM - 1; c >= 0; --c) shift_in(p0, own_count(x1, nT));
       Plane nx = 0;
 #pragma unroll
-      for (int c = MM - 1; c >= 0; --c) nx = nx + nx + (own_count(p1) >= mF ? 1u : 0u);
+      for (int c = MM - 1; c >= 0; --c) shift_in(nx, own_count(p0, 0u - (F + 1u)));
       x1 = nx;
       dec = live;
     } else if (KIND == 1) {
       // M odd, m <= 2F: x = the vote majority (adopting it, node.ts:106-109, or
-      // deciding it); decided iff c1 < m - F (c0 > F) or c1 > F
-      const uint32_t hiT = (r == 1u ? M1 : (uint32_t)MM) >> 1;
-      Plane p1 = 0;
+      // deciding it): c1 > m/2, i.e. c0 < (m+1)/2; decided iff c0 > F or
+      // c1 > F, i.e. undecided iff m - F <= c0 <= F
+      const uint32_t nT = 0u - (((r == 1u ? M1 : (uint32_t)MM) >> 1) + 1u);
+      Plane p0 = 0;
 #pragma unroll
-      for (int c = MM - 1; c >= 0; --c) p1 = p1 + p1 + (own_count(x1) > hiT ? 1u : 0u);
-      Plane nx = 0, nd = 0;
+      for (int c = MM - 1; c >= 0; --c) shift_in(p0, own_count(x1, nT));
+      Plane nx = 0, lo = 0, hi = 0;                                  // lo: c0 < m - F; hi: c0 > F
 #pragma unroll
       for (int c = MM - 1; c >= 0; --c) {
-        const uint32_t v1 = own_count(p1);
-        nx = nx + nx + (v1 > (uint32_t)(MM / 2) ? 1u : 0u);
-        nd = nd + nd + (v1 - mF > F - mF ? 1u : 0u);
+        const uint32_t s = own_count(p0, 0u - (uint32_t)((MM + 1) / 2));   // c0 - (m+1)/2
+        shift_in(nx, s);
+        shift_in(lo, s + (uint32_t)((MM + 1) / 2) - mF);             // c0 - (m - F)
+        shift_in(hi, F - (s + (uint32_t)((MM + 1) / 2)));            // F - c0
       }
       x1 = nx;
-      dec |= nd;
+      dec |= (lo | hi) & live;
     } else {
+      // General: c0 = M - c1 (M binary votes); p1 = c1 > c0, p0 = c0 > c1,
+      // else "?" (node.ts:63-69)
       const uint32_t M = r == 1u ? M1 : (uint32_t)MM;
       const uint32_t hiT = M >> 1, loT = (M + 1u) >> 1;
-      Plane p1 = 0, p0 = 0;
+      Plane p0 = 0, np1 = 0;
 #pragma unroll
       for (int c = MM - 1; c >= 0; --c) {
-        const uint32_t c1 = own_count(x1);                         // c0 = M - c1
-        p1 = p1 + p1 + (c1 > hiT ? 1u : 0u);                       // c1 > c0
-        p0 = p0 + p0 + (c1 < loT ? 1u : 0u);                       // c0 > c1, else "?"
+        const uint32_t s0 = own_count(x1, 0u - loT);                // c1 - loT: sign = p0
+        shift_in(p0, s0);
+        shift_in(np1, s0 + loT - hiT - 1u);                           // c1 - hiT - 1: sign = not p1
       }
+      const Plane p1 = ~np1 & live;
       // Coins (node.ts:111) are flipped only after a tied R-phase (every
       // proposal "?"): this lane's coin block for round r is drawn then, unless
       // it holds it already (rounds 1-4 of m <= 32 come from the ring).
@@ -184,21 +207,22 @@ __global__ void __launch_bounds__(256) benor_lane_kernel(KParams p) {
         cg = g1;
       }
       const Plane cwr = (Plane)(coin_word(cw, r) | (kWide ? (uint64_t)coin_word(cw1, r) << 32 : 0ull));
-      Plane nx = 0, nd = 0;
+      // P-phase (node.ts:88-113), per receiver: a = c0 - F - 1 (sign: not d0),
+      // b = c1 - F - 1 (sign: not d1), a - b = c0 - c1 (sign: c1 > c0),
+      // b - a (sign: c0 > c1)
+      Plane nd0 = 0, nd1 = 0, gt1 = 0, gt0 = 0;
 #pragma unroll
       for (int c = MM - 1; c >= 0; --c) {
-        const uint32_t v0 = own_count(p0), v1 = own_count(p1);
-        const bool d0 = v0 > F, d1 = v1 > F;                       // node.ts:99-105
-        uint32_t x = (uint32_t)(cwr >> c) & 1u;                    // node.ts:111
-        x = v0 > v1 ? 0u : x;                                      // node.ts:106-109
-        x = v1 > v0 ? 1u : x;
-        x = d1 ? 1u : x;
-        x = d0 ? 0u : x;
-        nx = nx + nx + x;
-        nd = nd + nd + ((d0 || d1) ? 1u : 0u);
+        const uint32_t a = own_count(p0, 0u - (F + 1u)), b = own_count(p1, 0u - (F + 1u));
+        shift_in(nd0, a);
+        shift_in(nd1, b);
+        shift_in(gt1, a - b);
+        shift_in(gt0, b - a);
       }
-      x1 = nx;
-      dec |= nd;
+      // x = 0 if d0, else 1 if d1, else the majority (node.ts:106-109), else
+      // the coin (node.ts:111); decided = d0 or d1 (node.ts:99-105)
+      x1 = nd0 & (~nd1 | gt1 | (~gt0 & cwr));
+      dec |= ~(nd0 & nd1) & live;
     }
 
     // ---- halt: every live node decided (auto-stop, node.ts:116-145) or k_max
