@@ -120,7 +120,13 @@ __global__ void __launch_bounds__(256) benor_mfma_kernel(KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t lane = threadIdx.x & 63u, h = lane >> 5;
   const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  uint32_t m = p.m, hist_len = p.hist_len, trial_count = (uint32_t)p.trial_count;
+  // Continuation pass (KIND > 0): round `cont` of the listed trials, every one
+  // of which tied in rounds 1 .. cont-1 -- all proposals "?", all votes "?",
+  // so every receiver took its coin (node.ts:63-69, 110-111) and the x plane
+  // of round cont is the coins of round cont-1.
+  const uint32_t cont = SURE ? 0u : p.cont_round;
+  uint32_t m = p.m, hist_len = p.hist_len;
+  uint32_t trial_count = cont ? *p.trial_list_len : (uint32_t)p.trial_count;
   asm volatile("" : "+s"(m), "+s"(hist_len), "+s"(trial_count));
 
   uint32_t *lhist = reinterpret_cast<uint32_t *>(smem);
@@ -135,7 +141,7 @@ __global__ void __launch_bounds__(256) benor_mfma_kernel(KParams p) {
   __syncthreads();
 
   const bool random_init = p.init_mode == BO_INIT_RANDOM;
-  const uint32_t M1 = m - p.init_q;            // round-1 binary votes ("?" inputs excluded)
+  const uint32_t M1 = cont ? m : m - p.init_q;  // binary votes ("?" inputs excluded in round 1)
   // KIND 0: every vote count odd, so p0 = (c1 <= M1 >> 1) is the sign of
   //   c1 - (M1 >> 1) - 0.5 (node.ts:63-69), packed by v_perm as a 0/1 plane
   //   (e2m1 1.0 = p0); in the P-phase the sign of c0 - F - 0.5 is "not d0"
@@ -196,9 +202,20 @@ __global__ void __launch_bounds__(256) benor_mfma_kernel(KParams p) {
   for (uint32_t g = wave_id; g < ngroups; g += waves_total) {
     const uint32_t t = (g << 5) + (lane & 31u);
     const bool valid = t < trial_count;
+    const uint32_t toff = cont ? (valid ? p.trial_list[t] : 0u) : t;   // the trial's offset in the launch
     // ---- /start (node.ts:167-188): this lane's x1 words 2c + h, c < W.
     uint32_t xw[W];
-    if (random_init) {
+    if (SURE ? false : cont != 0u) {
+      // coins of round cont-1: word (cont-2) & 3 of the block (trial, node
+      // group 2c + h, round group (cont-2) >> 2) of the coin stream (coin_block)
+      const uint64_t trial = lds_u64(keys + 2) + toff;
+      const uint2 kk = lds_keys(keys);
+#pragma unroll
+      for (int c = 0; c < W; ++c) {
+        const uint4 r = coin_block(kk.x, kk.y, (uint32_t)trial, (uint32_t)(trial >> 32), 32u * (2u * c + h), cont - 1u);
+        xw[c] = coin_word(r, cont - 1u);
+      }
+    } else if (random_init) {
       const uint64_t trial = lds_u64(keys + 2) + t;
       const uint2 kk = lds_keys(keys);
 #pragma unroll
@@ -314,7 +331,7 @@ __global__ void __launch_bounds__(256) benor_mfma_kernel(KParams p) {
       halt &= ~dcols;
       if (dcols) {
         if (lane < 32u && ((dcols >> lane) & 1u))
-          seg[n_def + (uint32_t)__builtin_popcount(dcols & ((1u << lane) - 1u))] = t;
+          seg[n_def + (uint32_t)__builtin_popcount(dcols & ((1u << lane) - 1u))] = toff;
         n_def += (uint32_t)__builtin_popcount(dcols);
       }
       const uint64_t b1 = ballot(mx > 0.0f);            // some receiver decided 1
@@ -322,7 +339,7 @@ __global__ void __launch_bounds__(256) benor_mfma_kernel(KParams p) {
       any1 = (uint32_t)b1 | (uint32_t)(b1 >> 32);
       any0 = (uint32_t)b0 | (uint32_t)(b0 >> 32);
     }
-    // ---- outcome: bins 3 + v (R = 1), per trial column (lanes n, n + 32)
+    // ---- outcome: bins 3R + v, per trial column (lanes n, n + 32)
     any1 &= halt;
     any0 &= halt;
     f_all += (uint32_t)__builtin_popcount(halt);
@@ -337,7 +354,9 @@ __global__ void __launch_bounds__(256) benor_mfma_kernel(KParams p) {
     for (uint32_t i = lane; i < n_def; i += 64u) p.defer_list[base + i] = seg[i];
   }
 
-  const uint32_t hc = lane == 3u ? f_all - f_1 : (lane == 4u ? f_1 - f_2 : (lane == 5u ? f_2 : 0u));
+  // outcome bins 3R + v of the halting round R (1, or the continuation's round)
+  const uint32_t rb = 3u * (cont ? cont : 1u);
+  const uint32_t hc = lane == rb ? f_all - f_1 : (lane == rb + 1u ? f_1 - f_2 : (lane == rb + 2u ? f_2 : 0u));
   if (hc) atomicAdd(&lhist[lane], hc);
   if (lane == 0 && f_2) atomicAdd(&lhist[hist_len - 1u], f_2);                   // disagreement counter
   __syncthreads();

@@ -13,6 +13,7 @@
 #include <cstring>
 #include <string>
 #include <algorithm>
+#include <utility>
 #include <cstdlib>
 #include <mutex>
 #include <vector>
@@ -442,7 +443,7 @@ static int plan_launch_impl(bo_plan *pl, uint64_t trial_begin, uint64_t trial_co
     const int grid = benor::lockstep_grid(kp, pl->device);
     const uint64_t waves = (uint64_t)grid * benor::block_waves(kp);
     const uint64_t seg_cap = ((cap + 31u) / 32u + waves - 1u) / waves * 32u;   // a wave's trials per launch, at most
-    const uint64_t words = cap + 64u + waves * seg_cap;                        // list, its length (padded), segments
+    const uint64_t words = 2u * cap + 64u + waves * seg_cap;                   // two lists, their lengths, segments
     if (pl->defer_words < words) {
       if (pl->d_defer) (void)hipFree(pl->d_defer);
       pl->d_defer = nullptr;
@@ -450,22 +451,43 @@ static int plan_launch_impl(bo_plan *pl, uint64_t trial_begin, uint64_t trial_co
       HIP_TRY(hipMalloc(&pl->d_defer, sizeof(uint32_t) * words));
       pl->defer_words = words;
     }
-    uint32_t *len = pl->d_defer + cap;
+    uint32_t *const segs = pl->d_defer + cap + 64u;
+    // Continuation passes (small-network form, W <= 16): a trial that tied in
+    // round 1 starts round 2 from its round-1 coins, so the matrix cores run
+    // rounds 2 .. kMfmaContRounds of the deferred trials too, each pass
+    // deferring its own ties (list ping-pong); whatever is left goes to the
+    // popcount kernel, which re-runs it from round 1.
+    const uint32_t last_round = kp.W <= 16u ? std::min<uint32_t>(benor::kMfmaContRounds, kp.k_max - 1u) : 1u;
     for (uint64_t done = 0; done < trial_count;) {
       const uint64_t n = std::min<uint64_t>(trial_count - done, cap);
+      uint32_t *list = pl->d_defer, *len = pl->d_defer + cap;
+      uint32_t *list2 = segs + waves * seg_cap, *len2 = len + 32u;
       HIP_TRY(hipMemsetAsync(len, 0, sizeof(uint32_t), s));
       kp.trial_begin = trial_begin + done;
       kp.trial_count = n;
-      kp.defer_list = pl->d_defer;
+      kp.defer_list = list;
       kp.defer_len = len;
-      kp.defer_seg = pl->d_defer + cap + 64u;
+      kp.defer_seg = segs;
       kp.defer_seg_cap = (uint32_t)seg_cap;
+      kp.cont_round = 0u;
       HIP_TRY(benor::launch_lockstep(kp, grid, s));
+      for (uint32_t r = 2u; r <= last_round; ++r) {
+        HIP_TRY(hipMemsetAsync(len2, 0, sizeof(uint32_t), s));
+        benor::KParams kc = kp;
+        kc.cont_round = r;
+        kc.trial_list = list;
+        kc.trial_list_len = len;
+        kc.defer_list = list2;
+        kc.defer_len = len2;
+        HIP_TRY(benor::launch_lockstep(kc, grid, s));
+        std::swap(list, list2);
+        std::swap(len, len2);
+      }
       benor::KParams kw = kp;
       kw.variant = kp.base_variant;              // W kernel (W <= 32) or blocked kernel
       kw.G = kp.base_G;
       kw.defer_list = kw.defer_len = kw.defer_seg = nullptr;
-      kw.trial_list = pl->d_defer;
+      kw.trial_list = list;
       kw.trial_list_len = len;
       HIP_TRY(benor::launch_lockstep(kw, benor::lockstep_grid(kw, pl->device), s));
       done += n;
