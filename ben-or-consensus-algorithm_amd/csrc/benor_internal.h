@@ -78,7 +78,7 @@ struct KParams {
   // W kernel trial-list mode: run the trials trial_begin + trial_list[i],
   // i < min(*trial_list_len, trial_count), instead of a contiguous range
   const uint32_t *trial_list, *trial_list_len;
-  // matrix-core continuation pass (KIND > 0, W <= 16): cont_round = r >= 2 runs
+  // matrix-core continuation pass (KIND > 0): cont_round = r >= 2 runs
   // round r of the trials trial_begin + trial_list[i], i < *trial_list_len,
   // which tied in every round before r (x = their round r-1 coins); 0: round 1
   uint32_t cont_round;

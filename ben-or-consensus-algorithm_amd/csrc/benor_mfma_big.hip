@@ -47,7 +47,11 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_big_kernel(KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t lane = threadIdx.x & 63u, h = lane >> 5;
   const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  uint32_t m = p.m, W = p.W, hist_len = p.hist_len, trial_count = (uint32_t)p.trial_count;
+  // Continuation pass (KIND > 0): round `cont` of the listed trials, from the
+  // coins of round cont-1 (benor_mfma.h).
+  const uint32_t cont = KIND == 0 ? 0u : p.cont_round;
+  uint32_t m = p.m, W = p.W, hist_len = p.hist_len;
+  uint32_t trial_count = cont ? *p.trial_list_len : (uint32_t)p.trial_count;
   asm volatile("" : "+s"(m), "+s"(W), "+s"(hist_len), "+s"(trial_count));
   const uint32_t MT = (m + 31u) >> 5;         // 32-receiver tiles
   const uint32_t KP = (MT + 1u) >> 1;         // P-phase K chunks (tile pairs)
@@ -69,7 +73,7 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_big_kernel(KParams p) {
   __syncthreads();
 
   const bool random_init = p.init_mode == BO_INIT_RANDOM;
-  const float bias_r = -8.0f * (float)(m - p.init_q);   // acc = 8 (c1 - c0): p1 > 0, p0 < 0, "?" = 0
+  const float bias_r = -8.0f * (float)(cont ? m : m - p.init_q);   // acc = 8 (c1 - c0): p1 > 0, p0 < 0, "?" = 0
   const float bias_p = KIND == 2 ? -(float)m : -((float)p.F + 0.5f);
   const float dec_thr = (float)(2u * p.F - m) + 0.5f;   // KIND 2: |2 c0 - m| > 2F - m <=> decided
   const uint32_t mrem = m - 32u * (MT - 1u);             // live rows of the last tile, 1..32
@@ -99,8 +103,16 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_big_kernel(KParams p) {
   for (uint32_t g = wave_id; g < ngroups; g += waves_total) {
     const uint32_t t = (g << 5) + (lane & 31u);
     const bool valid = t < trial_count;
+    const uint32_t toff = cont ? (valid ? p.trial_list[t] : 0u) : t;   // the trial's offset in the launch
     // ---- /start (node.ts:167-188): x1 words 2c + h of this lane's trial, c < W
-    if (random_init) {                         // whole Philox blocks, the halves trading words
+    if (KIND != 0 && cont != 0u) {             // continuation: the coins of round cont-1
+      const uint64_t trial = lds_u64(keys + 2) + toff;
+      for (uint32_t c = 0; c < W; ++c) {
+        const uint2 kk = lds_keys(keys);
+        const uint4 r = coin_block(kk.x, kk.y, (uint32_t)trial, (uint32_t)(trial >> 32), 32u * (2u * c + h), cont - 1u);
+        X[c * 64u + lane] = coin_word(r, cont - 1u);
+      }
+    } else if (random_init) {                  // whole Philox blocks, the halves trading words
       const uint64_t trial = lds_u64(keys + 2) + t;
       const uint32_t NJ = (((W + 1u) >> 1) + 1u) >> 1;   // blocks per lane half
       for (uint32_t j = 0; j < NJ; ++j) {
@@ -191,7 +203,7 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_big_kernel(KParams p) {
       __builtin_amdgcn_sched_barrier(0);
     }
 
-    // ---- outcome: bins 3 + v (R = 1); KIND > 0 defers as benor_mfma.h
+    // ---- outcome: bins 3R + v; KIND > 0 defers as benor_mfma.h
     uint32_t halt = (uint32_t)ballot(valid);
     if constexpr (KIND > 0) {
       const bool defer = qz != 0u || (KIND == 2 && !(ma > dec_thr));
@@ -200,7 +212,7 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_big_kernel(KParams p) {
       halt &= ~dcols;
       if (dcols) {
         if (lane < 32u && ((dcols >> lane) & 1u))
-          seg[n_def + (uint32_t)__builtin_popcount(dcols & ((1u << lane) - 1u))] = t;
+          seg[n_def + (uint32_t)__builtin_popcount(dcols & ((1u << lane) - 1u))] = toff;
         n_def += (uint32_t)__builtin_popcount(dcols);
       }
     }
@@ -221,7 +233,8 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_big_kernel(KParams p) {
     for (uint32_t i = lane; i < n_def; i += 64u) p.defer_list[base + i] = seg[i];
   }
 
-  const uint32_t hc = lane == 3u ? f_all - f_1 : (lane == 4u ? f_1 - f_2 : (lane == 5u ? f_2 : 0u));
+  const uint32_t rb = 3u * (cont ? cont : 1u);   // bins 3R + v of the halting round R
+  const uint32_t hc = lane == rb ? f_all - f_1 : (lane == rb + 1u ? f_1 - f_2 : (lane == rb + 2u ? f_2 : 0u));
   if (hc) atomicAdd(&lhist[lane], hc);
   if (lane == 0 && f_2) atomicAdd(&lhist[hist_len - 1u], f_2);
   __syncthreads();

@@ -452,12 +452,12 @@ static int plan_launch_impl(bo_plan *pl, uint64_t trial_begin, uint64_t trial_co
       pl->defer_words = words;
     }
     uint32_t *const segs = pl->d_defer + cap + 64u;
-    // Continuation passes (small-network form, W <= 16): a trial that tied in
+    // Continuation passes: a trial that tied in
     // round 1 starts round 2 from its round-1 coins, so the matrix cores run
     // rounds 2 .. kMfmaContRounds of the deferred trials too, each pass
     // deferring its own ties (list ping-pong); whatever is left goes to the
     // popcount kernel, which re-runs it from round 1.
-    const uint32_t last_round = kp.W <= 16u ? std::min<uint32_t>(benor::kMfmaContRounds, kp.k_max - 1u) : 1u;
+    const uint32_t last_round = std::min<uint32_t>(benor::kMfmaContRounds, kp.k_max - 1u);
     for (uint64_t done = 0; done < trial_count;) {
       const uint64_t n = std::min<uint64_t>(trial_count - done, cap);
       uint32_t *list = pl->d_defer, *len = pl->d_defer + cap;
