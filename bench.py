@@ -194,6 +194,10 @@ def other_configs(benor, torch, k_max, seed):
         words = plan.popc_words_per_node_round
         if plan.kernel == benor.BO_KERNEL_MFMA:
             roof = mfma_roofline(m, nr, ms * 1e-3)
+            # the same rate against the INT/popcount roofline the metric names
+            # (the popcount kernel's algorithmic words per node-round; >1: past it)
+            roof["popcount_equiv"] = {"words_per_node_round": words,
+                                      "frac_of_popc_peak": nr * words / (ms * 1e-3) / SPEC_PEAK_POPC}
         elif m > 64:
             roof = {"bound": "valu (v_bcnt_u32_b32 issue)", "kernel": "lockstep W kernel",
                     "unit": "Tpopc/s", "popc_words_per_node_round": words,
