@@ -32,6 +32,12 @@
 namespace benor {
 
 constexpr uint32_t kBigMaxW = kMaxW;   // 64 chunks at N = 4096
+#ifndef BENOR_BIG_REG_WAVES
+// Waves per CU assumed for the workgroup-size choice.  The kernel takes 124-131
+// VGPRs (3 waves per SIMD), but choosing as if 2 per SIMD fit measured best
+// (12 or 16: -3..-20 % on N=2048..4096 shapes; profiles/r02_big_zero_start_ab.jsonl).
+#define BENOR_BIG_REG_WAVES 8
+#endif
 #ifndef BENOR_BIG_NT
 #define BENOR_BIG_NT 4                  // receiver tiles per expanded operand
 #endif
@@ -91,9 +97,7 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_big_kernel(KParams p) {
   const int last_bits = (int)m - 32 * (2 * ((int)W - 1) + (int)h);
   const uint32_t last_mask = last_bits >= 32 ? ~0u : (last_bits <= 0 ? 0u : ((1u << last_bits) - 1u));
 
-  mf_v4i ones[NT];                             // one opaque copy per tile: no two tiles' products merge
-#pragma unroll
-  for (int u = 0; u < NT; ++u) ones[u] = mf_v4i{0x22222222, 0x22222222, 0x22222222, 0x22222222};
+  mf_v4i ones = {0x22222222, 0x22222222, 0x22222222, 0x22222222};
   uint32_t f_all = 0, f_1 = 0, f_2 = 0;
   const uint32_t ngroups = (trial_count + 31u) >> 5;
   const uint32_t waves_total = gridDim.x * BW;
@@ -140,18 +144,24 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_big_kernel(KParams p) {
     // chunk; proposals to LDS as sign bits (1 = proposal 0).
     uint32_t qz = 0u;
     for (uint32_t i = 0; i < MT; i += (uint32_t)NT) {
+      // Accumulators start at 0 and take their bias after the chunk loop: a
+      // bias-splat start value kept a second 16-register tuple per tile live
+      // across the loop (occupancy 2 -> 3-4 waves per SIMD without it).
       mf_v16f acc[NT];
 #pragma unroll
-      for (int u = 0; u < NT; ++u) {
-        asm volatile("" : "+v"(ones[u]));
-#pragma unroll
-        for (int j = 0; j < 16; ++j) acc[u][j] = bias_r;
-      }
+      for (int u = 0; u < NT; ++u) acc[u] = mf_v16f{};
       for (uint32_t c = 0; c < W; ++c) {
         const mf_v4i b = expand_votes(X[c * 64u + lane]);
 #pragma unroll
-        for (int u = 0; u < NT; ++u) acc[u] = mfma_count<4>(ones[u], b, acc[u]);
+        for (int u = 0; u < NT; ++u) {
+          asm volatile("" : "+v"(ones));       // opaque per tile: no two tiles' products merge
+          acc[u] = mfma_count<4>(ones, b, acc[u]);
+        }
       }
+#pragma unroll
+      for (int u = 0; u < NT; ++u)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[u][j] += bias_r;
 #pragma unroll
       for (int q = 0; q < NT / 2; ++q) {      // tile pair (i + 2q, i + 2q + 1) -> proposal word (i >> 1) + q
         uint32_t n[4];
@@ -177,22 +187,28 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_big_kernel(KParams p) {
       const float nanf = __builtin_nanf("");
       mf_v16f acc[NT];
 #pragma unroll
-      for (int u = 0; u < NT; ++u) {
-        asm volatile("" : "+v"(ones[u]));
-        const uint32_t ti = i + u;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {         // rows with no receiver start at NaN: the reductions skip them
-          const bool live = ti < MT - 1u || (ti == MT - 1u && ((live_last >> j) & 1u));
-          acc[u][j] = live ? bias_p : nanf;
-        }
-      }
+      for (int u = 0; u < NT; ++u) acc[u] = mf_v16f{};
       for (uint32_t k = 0; k < KP; ++k) {
         const mf_v4i b = expand_votes(PL[k * 64u + lane]);
 #pragma unroll
-        for (int u = 0; u < NT; ++u) acc[u] = KIND == 2 ? mfma_count<1>(ones[u], b, acc[u]) : mfma_count(ones[u], b, acc[u]);
+        for (int u = 0; u < NT; ++u) {
+          asm volatile("" : "+v"(ones));
+          acc[u] = KIND == 2 ? mfma_count<1>(ones, b, acc[u]) : mfma_count(ones, b, acc[u]);
+        }
       }
 #pragma unroll
       for (int u = 0; u < NT; ++u) {
+        const uint32_t ti = i + u;
+        if (ti + 1u < MT) {
+#pragma unroll
+          for (int j = 0; j < 16; ++j) acc[u][j] += bias_p;
+        } else {                               // rows with no receiver become NaN: the reductions skip them
+#pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            const bool live = ti == MT - 1u && ((live_last >> j) & 1u);
+            acc[u][j] += live ? bias_p : nanf;
+          }
+        }
 #pragma unroll
         for (int j = 0; j < 16; j += 2) {
           mn = fminf(fminf(mn, acc[u][j]), acc[u][j + 1]);
@@ -252,7 +268,7 @@ uint32_t mfma_big_lds_bytes(const KParams &p, uint32_t bw) { return p.hist_bytes
 // +22 % at N=4096, F=1365, where LDS admits 7 single waves but one 4-wave
 // group; -10..-30 % where both fill the CU.)
 uint32_t mfma_big_block_waves(const KParams &p) {
-  constexpr uint32_t kRegWaves = 8;          // per CU at ~184 VGPRs (2 per SIMD)
+  constexpr uint32_t kRegWaves = BENOR_BIG_REG_WAVES;
   uint32_t best = 4, best_waves = 0;
   for (uint32_t bw = 4; bw >= 1; bw >>= 1) {
     uint32_t w = (160u * 1024u) / mfma_big_lds_bytes(p, bw) * bw;
