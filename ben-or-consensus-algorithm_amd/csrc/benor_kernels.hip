@@ -893,15 +893,18 @@ int lockstep_grid(const KParams &p, int device) {
     const uint64_t lds_fit = (160u * 1024u) / lds;
     if (lds_fit < per_cu) per_cu = lds_fit ? lds_fit : 1;
   }
-  // Lane kernel, general case (KIND 0: coin rounds, so a geometric number of
-  // rounds per trial): a wave ends with its slowest queued trial, so a short
-  // launch spread over every wave slot (~2 trials per lane at 10^6 trials)
-  // spends most of its time in that tail.  Fewer, longer-lived waves: at
-  // least ~8 trials per lane, 2..8 workgroups per CU (tools/lane_grid_sweep.py,
-  // N=10 F=4 at 10^6 trials: 8 per CU 41-57 us, 2 per CU 25 us; at 10^7
+  // Lane kernel: a short launch spread over every wave slot (~2 trials per
+  // lane at 10^6 trials) spends most of its time in per-wave overhead (ring
+  // fills, the LDS histogram) and, with coin rounds (KIND 0), in the tail of
+  // each wave's slowest trial.  Fewer, longer-lived waves: at least ~8
+  // trial-rounds of work per lane, 2..8 workgroups per CU
+  // (tools/lane_grid_sweep.py, profiles/r02_lane_grid.jsonl: N=10 F=4 at
+  // 10^6 trials 41-57 us at 8 per CU, 22.5 us at 2; N=64 F=21 (KIND 2) 28.9 ->
+  // 18.6 us; N=10 F=5 (KIND 1, k_max rounds per trial) keeps 8; at 10^7
   // trials 8 per CU stays best).
-  if (p.variant == 6 && p.G == 0u) {
-    const uint64_t want = p.trial_count / ((uint64_t)cus * 64u * kWavesPerBlock * 8u);
+  if (p.variant == 6) {
+    const uint64_t rounds = p.G == 1u ? (p.m <= p.F ? p.k_max : 2u) : 1u;   // per trial, roughly
+    const uint64_t want = p.trial_count * rounds / ((uint64_t)cus * 64u * kWavesPerBlock * 8u);
     const uint64_t v = want < 2u ? 2u : want;
     if (v < per_cu) per_cu = v;
   }

@@ -16,12 +16,12 @@ def main():
 
     torch.cuda.set_device(0)
     st = torch.cuda.current_stream()
-    shapes = [(10, 4), (10, 5), (5, 1), (256, 85)]
+    shapes = [(10, 4), (5, 1), (20, 6), (64, 21)]
     for N, F in shapes:
         plan = benor.TrialsPlan(N, F, [i < F for i in range(N)], seed=7, k_max=16)
         h = torch.zeros(plan.hist_len, dtype=torch.int64, device="cuda")
-        for T in (10**6, 10**7):
-            for bpc in (8, 4, 2, 1):
+        for T in (10**6, 3 * 10**6, 10**7):
+            for bpc in (8, 6, 4, 3, 2, 1):
                 os.environ["BENOR_BLOCKS_PER_CU"] = str(bpc)
                 plan.launch(0, T, h.data_ptr(), st.cuda_stream)
                 torch.cuda.synchronize()
