@@ -464,7 +464,26 @@ struct EvLane {
   int16_t *ks;         // [N]
 };
 
-template <int NW>
+// Inbox counters {c0, c1, len} of one (node, round slot, phase): in the lane's
+// scratch slice as 10-bit fields of a u32, or -- LBOX, N <= kMaxEventLdsN -- in
+// LDS as 5-bit fields of a u16, laid out [slot][lane of the workgroup].  The
+// counter read-modify-write sits on every event's dependent path (its result
+// decides the trigger, node.ts:52,88); in LDS it costs an LDS round trip
+// instead of a second global-memory one.
+template <bool LBOX>
+struct EvBox {
+  static constexpr uint32_t kSh = LBOX ? 5u : 10u;   // c0: bits 0.., c1: kSh.., len: 2 kSh..
+  uint32_t *g;          // [N][4][2] (scratch)
+  uint16_t *l;          // [N * 8][256] (LDS)
+  uint32_t tid;
+  __device__ __forceinline__ uint32_t get(uint32_t slot) const { return LBOX ? (uint32_t)l[slot * 256u + tid] : g[slot]; }
+  __device__ __forceinline__ void set(uint32_t slot, uint32_t v) {
+    if (LBOX) l[slot * 256u + tid] = (uint16_t)v;
+    else g[slot] = v;
+  }
+};
+
+template <int NW, bool LBOX>
 __global__ void __launch_bounds__(256) benor_event_kernel(KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint32_t *lhist = reinterpret_cast<uint32_t *>(smem);
@@ -489,6 +508,11 @@ __global__ void __launch_bounds__(256) benor_event_kernel(KParams p) {
   L.crash = L.comp + 4 * NW;
   L.xs = reinterpret_cast<int8_t *>(L.crash + N);
   L.ks = reinterpret_cast<int16_t *>(L.xs + ((N + 3u) & ~3u));
+  EvBox<LBOX> box;
+  box.g = L.ibox;
+  box.l = reinterpret_cast<uint16_t *>(smem + p.hist_bytes);
+  box.tid = threadIdx.x;
+  constexpr uint32_t kSh = EvBox<LBOX>::kSh, kMask = (1u << kSh) - 1u;
   const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
 
   auto full = [&](const uint64_t *a, const uint64_t (&b)[NW]) {   // a | b == all
@@ -525,7 +549,7 @@ __global__ void __launch_bounds__(256) benor_event_kernel(KParams p) {
     }
     for (uint32_t i = 0; i < N; ++i)
       if (set_has(killed, i)) { L.xs[i] = -1; L.ks[i] = -1; }
-    for (uint32_t j = 0; j < N * 8u; ++j) L.ibox[j] = 0u;
+    for (uint32_t j = 0; j < N * 8u; ++j) box.set(j, 0u);
     for (int j = 0; j < 4 * NW; ++j) L.comp[j] = 0ull;
     // ---- mid-run /stop schedule, sorted by event index
     uint32_t ncrash = 0;
@@ -603,14 +627,14 @@ __global__ void __launch_bounds__(256) benor_event_kernel(KParams p) {
       const uint32_t to = msg & 255u, ph = (msg >> 8) & 1u, k = cur + (((msg >> 11) - cur) & 3u);
       const uint32_t x = (msg >> 9) & 3u;
       if (set_has(killed, to)) continue;               // node.ts:45
-      uint32_t *bx = &L.ibox[(to * 4u + (k & 3u)) * 2u + ph];
-      uint32_t b = *bx;
-      b += 1u << 20;                                   // len
+      const uint32_t slot = (to * 4u + (k & 3u)) * 2u + ph;
+      uint32_t b = box.get(slot);
+      b += 1u << (2u * kSh);                           // len
       if (x == 0u) b += 1u;                            // c0
-      else if (x == 1u) b += 1u << 10;                 // c1
-      *bx = b;
-      if ((b >> 20) != quorum) continue;               // node.ts:52, :88 (fires once: exactly F faulty)
-      const uint32_t c0 = b & 1023u, c1 = (b >> 10) & 1023u;
+      else if (x == 1u) b += 1u << kSh;                // c1
+      box.set(slot, b);
+      if ((b >> (2u * kSh)) != quorum) continue;       // node.ts:52, :88 (fires once: exactly F faulty)
+      const uint32_t c0 = b & kMask, c1 = (b >> kSh) & kMask;
       uint32_t body;
       if (ph == 0u) {                                  // node.ts:53-80
         const uint32_t v = c0 > c1 ? 0u : (c1 > c0 ? 1u : 2u);
@@ -635,8 +659,8 @@ __global__ void __launch_bounds__(256) benor_event_kernel(KParams p) {
         }
         L.xs[to] = nx;
         L.ks[to] = (int16_t)(k + 1u);
-        L.ibox[(to * 4u + ((k + 2u) & 3u)) * 2u + 0u] = 0u;   // recycle round k-2's slots for k+2
-        L.ibox[(to * 4u + ((k + 2u) & 3u)) * 2u + 1u] = 0u;
+        box.set((to * 4u + ((k + 2u) & 3u)) * 2u + 0u, 0u);   // recycle round k-2's slots for k+2
+        box.set((to * 4u + ((k + 2u) & 3u)) * 2u + 1u, 0u);
         L.comp[(k & 3u) * NW + (to >> 6)] |= 1ull << (to & 63u);
         while (full(L.comp + (cur & 3u) * NW, killed)) {
           if (full(decided, killed)) { halted = 1; R = cur; break; }
@@ -716,8 +740,9 @@ void plan_geometry(KParams &p) {
     p.nblocks = 1;
     p.variant = 4;
     p.wave_bytes = 0;
-    p.lds_bytes = p.hist_bytes;
-    // per-lane scratch (u32 words): pool, inbox window, comp[4] (u64), crash[64], xs[64] (i8), ks[64] (i16)
+    // N <= kMaxEventLdsN: the inbox counters live in LDS, 8N u16 per lane of the
+    // 256-lane workgroup (EvBox)
+    p.lds_bytes = p.hist_bytes + (p.N <= kMaxEventLdsN ? 256u * 8u * p.N * 2u : 0u);
     const uint32_t NW = p.N <= 64u ? 1u : 4u;
     p.ev_cap = 4u * p.N * p.N + 64u;
     // per-lane scratch (u32 words): pool, inbox window, comp[4][NW] (u64), crash[N] (u64), xs (i8), ks (i16)
@@ -835,8 +860,18 @@ static hipError_t dispatch_b(const KParams &p, int grid, hipStream_t s, std::int
 
 hipError_t launch_lockstep(const KParams &p, int grid, hipStream_t s) {
   if (p.variant == 4) {
-    if (p.N <= 64u) hipLaunchKernelGGL(benor_event_kernel<1>, dim3(grid), dim3(256), p.lds_bytes, s, p);
-    else hipLaunchKernelGGL(benor_event_kernel<4>, dim3(grid), dim3(256), p.lds_bytes, s, p);
+    if (p.N <= kMaxEventLdsN) {
+      if (p.lds_bytes > 64u * 1024u) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&benor_event_kernel<1, true>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds_bytes);
+        if (e != hipSuccess) return e;
+      }
+      hipLaunchKernelGGL((benor_event_kernel<1, true>), dim3(grid), dim3(256), p.lds_bytes, s, p);
+    } else if (p.N <= 64u) {
+      hipLaunchKernelGGL((benor_event_kernel<1, false>), dim3(grid), dim3(256), p.lds_bytes, s, p);
+    } else {
+      hipLaunchKernelGGL((benor_event_kernel<4, false>), dim3(grid), dim3(256), p.lds_bytes, s, p);
+    }
     return hipGetLastError();
   }
   if (p.variant == 6) return dispatch_lane(p, grid, s, std::make_integer_sequence<int, (int)kMaxLaneM>{});

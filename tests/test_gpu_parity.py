@@ -372,6 +372,9 @@ def test_event_mode_golden(oracle_vectors):
 @pytest.mark.parametrize("N,F,cc,cw,trials", [(10, 4, 0, 0, 200_000), (10, 4, 1, 150, 200_000),
                                               (20, 6, 2, 600, 20_000), (64, 21, 4, 10_000, 500),
                                               (3, 1, 1, 6, 50_000), (1, 0, 0, 0, 1000),
+                                              # inbox counters in LDS up to N = 31 (5-bit fields), then scratch
+                                              (16, 5, 1, 300, 20_000), (31, 10, 3, 2_000, 5_000),
+                                              (32, 10, 2, 2_000, 3_000), (29, 0, 2, 1_500, 5_000),
                                               # N > 64 (r02): 4-word node bitsets, 8-bit node ids
                                               (65, 20, 2, 9_000, 300), (128, 42, 3, 40_000, 200),
                                               (256, 85, 5, 150_000, 20), (200, 0, 1, 80_000, 20)])
@@ -385,7 +388,7 @@ def test_event_mode_matches_oracle(N, F, cc, cw, trials):
 
 
 def test_event_mode_without_stop_equals_lockstep_kernel():
-    for N, F in [(10, 4), (64, 21), (33, 0), (128, 42), (100, 0)]:
+    for N, F in [(10, 4), (64, 21), (33, 0), (128, 42), (100, 0), (31, 10), (17, 0)]:
         fl = first_f(N, F)
         a = benor.TrialsPlan(N, F, fl, seed=8, k_max=16, mode=EV).run(0, 50_000)
         b = benor.TrialsPlan(N, F, fl, seed=8, k_max=16).run(0, 50_000)
