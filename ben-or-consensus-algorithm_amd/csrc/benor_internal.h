@@ -25,6 +25,10 @@ constexpr uint32_t kMaxLaneM = 64;         // m <= 64: lane kernel, one trial pe
 constexpr uint32_t kMaxMfmaM = 1024;       // matrix-core kernel (benor_mfma.h): W <= 16, operands in registers;
                                            // beyond, the big-network form (runtime W, proposals in LDS) to BO_MAX_N
 constexpr uint32_t kMaxEventN = 256;       // event level: node ids in 8 bits of a message
+// Workgroups of `lds` dynamic LDS bytes that fit one CU's 160 KB: allocation
+// is in 512-byte granules (a 23216-byte group fits 6 per CU, not 7: the 7th
+// waits, and a grid sized for 7 per CU ran 1.45x longer).
+constexpr uint32_t lds_groups_per_cu(uint32_t lds) { return lds ? (160u * 1024u) / ((lds + 511u) & ~511u) : 64u; }
 constexpr uint32_t kMaxEventLdsN = 31;     // event level: inbox counters in LDS (5-bit fields) up to here
 constexpr uint64_t kMaxTrialsPerLaunch = 1ull << 31;   // trial offsets within a launch fit 32 bits
 constexpr uint32_t kParamBytes = 32;       // LDS parameter block after the histogram (W kernel)

@@ -925,7 +925,7 @@ int lockstep_grid(const KParams &p, int device) {
   // the matrix-core kernel uses no wave slices (its big-network form: proposal planes)
   const uint32_t lds = mfma ? (p.W > 16u ? mfma_big_lds_bytes(p, bw) : p.hist_bytes) : p.lds_bytes;
   if (lds > 0) {
-    const uint64_t lds_fit = (160u * 1024u) / lds;
+    const uint64_t lds_fit = lds_groups_per_cu(lds);
     if (lds_fit < per_cu) per_cu = lds_fit ? lds_fit : 1;
   }
   // Lane kernel: a short launch spread over every wave slot (~2 trials per

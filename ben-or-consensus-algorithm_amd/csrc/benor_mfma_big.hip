@@ -38,15 +38,24 @@ constexpr uint32_t kBigMaxW = kMaxW;   // 64 chunks at N = 4096
 // (12 or 16: -3..-20 % on N=2048..4096 shapes; profiles/r02_big_zero_start_ab.jsonl).
 #define BENOR_BIG_REG_WAVES 8
 #endif
-#ifndef BENOR_BIG_NT
-#define BENOR_BIG_NT 4                  // receiver tiles per expanded operand
-#endif
 
 // Words per lane of a wave's x plane: the W x1 words rounded up to whole
 // Philox blocks per lane half (4 words each); the slice adds the KP <= W
 // proposal words (+1: a tile block may fill word KP when KP is odd).
 __host__ __device__ constexpr uint32_t big_plane_words(uint32_t W) { return 4u * ((((W + 1u) >> 1) + 1u) >> 1); }
-__host__ __device__ constexpr uint32_t big_slice_words(uint32_t W) { return big_plane_words(W) + W + 1u; }
+// The R-phase writes NT/2 proposal words per block of NT tiles, so up to
+// ceil(MT/NT) * NT/2 <= W + NT/2 - 1 words (MT = ceil(m/32) <= 2W).
+__host__ __device__ constexpr uint32_t big_slice_words(uint32_t W, uint32_t NT) {
+  return big_plane_words(W) + W + NT / 2u - 1u;
+}
+// Receiver tiles per expanded operand: 8 from W = 28 on (more independent
+// accumulator chains and half the expansion VALU and LDS reads per product,
+// at 2 waves per SIMD), else 4 (3 waves per SIMD by registers).  Measured
+// (profiles/r02_big_nt_ab.jsonl): NT = 8 +20 % at N=4096 F=0 (W=64), +12 % at
+// N=2048 F=0 (W=32), +6 % at N=4096 F=2000 (W=33), -2 % at N=4096 F=1365
+// (W=43), -8 % at W=21..22.
+constexpr uint32_t kBigNt8MinW = 28;
+__host__ __device__ constexpr uint32_t big_nt(uint32_t W) { return W >= kBigNt8MinW ? 8u : 4u; }
 
 template <int KIND, int NT, int BW>
 __global__ void __launch_bounds__(64 * BW) benor_mfma_big_kernel(KParams p) {
@@ -67,7 +76,7 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_big_kernel(KParams p) {
   // The wave's LDS slice: X [plane_words][64] x1 bits, then P [W][64]
   // proposal bits.  Each lane reads back only its own words (its trial
   // column and half), so no barrier orders them.
-  uint32_t *X = reinterpret_cast<uint32_t *>(smem + p.hist_bytes) + (size_t)wv * big_slice_words(W) * 64u;
+  uint32_t *X = reinterpret_cast<uint32_t *>(smem + p.hist_bytes) + (size_t)wv * big_slice_words(W, NT) * 64u;
   uint32_t *PL = X + big_plane_words(W) * 64u;
   for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) lhist[i] = 0u;
   if (threadIdx.x == 0) {
@@ -260,7 +269,9 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_big_kernel(KParams p) {
   }
 }
 
-uint32_t mfma_big_lds_bytes(const KParams &p, uint32_t bw) { return p.hist_bytes + bw * big_slice_words(p.W) * 64u * 4u; }
+uint32_t mfma_big_lds_bytes(const KParams &p, uint32_t bw) {
+  return p.hist_bytes + bw * big_slice_words(p.W, big_nt(p.W)) * 64u * 4u;
+}
 
 // Waves per workgroup: the most resident waves per CU -- LDS (160 KB) against
 // the ~2 waves/SIMD its registers allow -- with ties to larger workgroups,
@@ -271,7 +282,7 @@ uint32_t mfma_big_block_waves(const KParams &p) {
   constexpr uint32_t kRegWaves = BENOR_BIG_REG_WAVES;
   uint32_t best = 4, best_waves = 0;
   for (uint32_t bw = 4; bw >= 1; bw >>= 1) {
-    uint32_t w = (160u * 1024u) / mfma_big_lds_bytes(p, bw) * bw;
+    uint32_t w = lds_groups_per_cu(mfma_big_lds_bytes(p, bw)) * bw;
     if (w > kRegWaves) w = kRegWaves;
     if (w > best_waves) {
       best_waves = w;
@@ -281,9 +292,8 @@ uint32_t mfma_big_block_waves(const KParams &p) {
   return best;
 }
 
-template <int KIND, int BW>
+template <int KIND, int NT, int BW>
 static hipError_t launch_big_kind(const KParams &p, int grid, hipStream_t s) {
-  constexpr int NT = BENOR_BIG_NT;
   const uint32_t lds = mfma_big_lds_bytes(p, BW);
   if (lds > 64u * 1024u) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&benor_mfma_big_kernel<KIND, NT, BW>),
@@ -294,19 +304,24 @@ static hipError_t launch_big_kind(const KParams &p, int grid, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int KIND>
+template <int KIND, int NT>
 static hipError_t launch_big_bw(const KParams &p, int grid, hipStream_t s) {
   const uint32_t bw = mfma_big_block_waves(p);
-  if (bw == 4u) return launch_big_kind<KIND, 4>(p, grid, s);
-  if (bw == 2u) return launch_big_kind<KIND, 2>(p, grid, s);
-  return launch_big_kind<KIND, 1>(p, grid, s);
+  if (bw == 4u) return launch_big_kind<KIND, NT, 4>(p, grid, s);
+  if (bw == 2u) return launch_big_kind<KIND, NT, 2>(p, grid, s);
+  return launch_big_kind<KIND, NT, 1>(p, grid, s);
+}
+
+template <int KIND>
+static hipError_t launch_big_nt(const KParams &p, int grid, hipStream_t s) {
+  return big_nt(p.W) == 8u ? launch_big_bw<KIND, 8>(p, grid, s) : launch_big_bw<KIND, 4>(p, grid, s);
 }
 
 hipError_t launch_mfma_big(const KParams &p, int grid, hipStream_t s) {
   if (p.W < 17u || p.W > kBigMaxW) return hipErrorInvalidValue;
-  if (p.G == 0u) return launch_big_bw<0>(p, grid, s);
-  if (p.G == 1u) return launch_big_bw<1>(p, grid, s);
-  return launch_big_bw<2>(p, grid, s);
+  if (p.G == 0u) return launch_big_nt<0>(p, grid, s);
+  if (p.G == 1u) return launch_big_nt<1>(p, grid, s);
+  return launch_big_nt<2>(p, grid, s);
 }
 
 }  // namespace benor
