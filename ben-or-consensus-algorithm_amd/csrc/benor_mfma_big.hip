@@ -45,8 +45,11 @@ constexpr uint32_t kBigMaxW = kMaxW;   // 64 chunks at N = 4096
 __host__ __device__ constexpr uint32_t big_plane_words(uint32_t W) { return 4u * ((((W + 1u) >> 1) + 1u) >> 1); }
 // The R-phase writes NT/2 proposal words per block of NT tiles, so up to
 // ceil(MT/NT) * NT/2 <= W + NT/2 - 1 words (MT = ceil(m/32) <= 2W).
-__host__ __device__ constexpr uint32_t big_slice_words(uint32_t W, uint32_t NT) {
-  return big_plane_words(W) + W + NT / 2u - 1u;
+__host__ __device__ constexpr uint32_t big_prop_words(uint32_t W, uint32_t NT) { return W + NT / 2u - 1u; }
+// REGEN (round 1 of random initial values): no x plane in LDS, each tile block
+// regenerates its x words from Philox, so the slice is the proposal words only.
+__host__ __device__ constexpr uint32_t big_slice_words(uint32_t W, uint32_t NT, bool regen) {
+  return (regen ? 0u : big_plane_words(W)) + big_prop_words(W, NT);
 }
 // Receiver tiles per expanded operand: 8 from W = 28 on (more independent
 // accumulator chains and half the expansion VALU and LDS reads per product,
@@ -57,7 +60,7 @@ __host__ __device__ constexpr uint32_t big_slice_words(uint32_t W, uint32_t NT) 
 constexpr uint32_t kBigNt8MinW = 28;
 __host__ __device__ constexpr uint32_t big_nt(uint32_t W) { return W >= kBigNt8MinW ? 8u : 4u; }
 
-template <int KIND, int NT, int BW>
+template <int KIND, int NT, int BW, bool REGEN>
 __global__ void __launch_bounds__(64 * BW) benor_mfma_big_kernel(KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t lane = threadIdx.x & 63u, h = lane >> 5;
@@ -76,8 +79,8 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_big_kernel(KParams p) {
   // The wave's LDS slice: X [plane_words][64] x1 bits, then P [W][64]
   // proposal bits.  Each lane reads back only its own words (its trial
   // column and half), so no barrier orders them.
-  uint32_t *X = reinterpret_cast<uint32_t *>(smem + p.hist_bytes) + (size_t)wv * big_slice_words(W, NT) * 64u;
-  uint32_t *PL = X + big_plane_words(W) * 64u;
+  uint32_t *X = reinterpret_cast<uint32_t *>(smem + p.hist_bytes) + (size_t)wv * big_slice_words(W, NT, REGEN) * 64u;
+  uint32_t *PL = X + (REGEN ? 0u : big_plane_words(W)) * 64u;
   for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) lhist[i] = 0u;
   if (threadIdx.x == 0) {
     keys[0] = (uint32_t)p.seed;
@@ -118,7 +121,9 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_big_kernel(KParams p) {
     const bool valid = t < trial_count;
     const uint32_t toff = cont ? (valid ? p.trial_list[t] : 0u) : t;   // the trial's offset in the launch
     // ---- /start (node.ts:167-188): x1 words 2c + h of this lane's trial, c < W
-    if (KIND != 0 && cont != 0u) {             // continuation: the coins of round cont-1
+    if (REGEN) {
+      // x words are regenerated per tile block in the R-phase
+    } else if (KIND != 0 && cont != 0u) {      // continuation: the coins of round cont-1
       const uint64_t trial = lds_u64(keys + 2) + toff;
       for (uint32_t c = 0; c < W; ++c) {
         const uint2 kk = lds_keys(keys);
@@ -147,7 +152,7 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_big_kernel(KParams p) {
         X[c * 64u + lane] = h ? q.w : q.z;
       }
     }
-    X[(W - 1u) * 64u + lane] &= last_mask;
+    if (!REGEN) X[(W - 1u) * 64u + lane] &= last_mask;
 
     // ---- R-phase (node.ts:46-82): NT receiver tiles on each expanded x
     // chunk; proposals to LDS as sign bits (1 = proposal 0).
@@ -159,12 +164,41 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_big_kernel(KParams p) {
       mf_v16f acc[NT];
 #pragma unroll
       for (int u = 0; u < NT; ++u) acc[u] = mf_v16f{};
-      for (uint32_t c = 0; c < W; ++c) {
-        const mf_v4i b = expand_votes(X[c * 64u + lane]);
+      if constexpr (REGEN) {
+        // x1 words of chunks 4j .. 4j+3 from Philox block 2j + h, the lane
+        // halves trading two words (as the /start code of the LDS form)
+        const uint64_t trial = lds_u64(keys + 2) + t;
+        const uint32_t NJ = (((W + 1u) >> 1) + 1u) >> 1;
+        for (uint32_t j = 0; j < NJ; ++j) {
+          const uint2 kk = lds_keys(keys);
+          const uint4 r = philox4x32_10(kk.x, kk.y,
+                                        make_uint4((uint32_t)trial, (uint32_t)(trial >> 32), 2u * j + h, kStreamInit << 24));
+          const uint32_t keep_a = h ? r.y : r.x, keep_b = h ? r.w : r.z;
+          const uint32_t give_a = h ? r.x : r.y, give_b = h ? r.z : r.w;
+          const uint32_t recv_a = (uint32_t)__shfl_xor((int)give_a, 32);
+          const uint32_t recv_b = (uint32_t)__shfl_xor((int)give_b, 32);
+          const uint32_t xw[4] = {h ? recv_a : keep_a, h ? recv_b : keep_b, h ? keep_a : recv_a, h ? keep_b : recv_b};
 #pragma unroll
-        for (int u = 0; u < NT; ++u) {
-          asm volatile("" : "+v"(ones));       // opaque per tile: no two tiles' products merge
-          acc[u] = mfma_count<4>(ones, b, acc[u]);
+          for (uint32_t q = 0; q < 4u; ++q) {
+            const uint32_t c = 4u * j + q;
+            if (c < W) {
+              const mf_v4i b = expand_votes(c == W - 1u ? xw[q] & last_mask : xw[q]);
+#pragma unroll
+              for (int u = 0; u < NT; ++u) {
+                asm volatile("" : "+v"(ones));
+                acc[u] = mfma_count<4>(ones, b, acc[u]);
+              }
+            }
+          }
+        }
+      } else {
+        for (uint32_t c = 0; c < W; ++c) {
+          const mf_v4i b = expand_votes(X[c * 64u + lane]);
+#pragma unroll
+          for (int u = 0; u < NT; ++u) {
+            asm volatile("" : "+v"(ones));     // opaque per tile: no two tiles' products merge
+            acc[u] = mfma_count<4>(ones, b, acc[u]);
+          }
         }
       }
 #pragma unroll
@@ -269,8 +303,18 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_big_kernel(KParams p) {
   }
 }
 
+// Round 1 of random initial values regenerates its x words from Philox (no x
+// plane in LDS) when the LDS form's slices would hold the CU under 2 waves per
+// SIMD (from W ~ 39): +12 % at N=4096 F=1365 (W=43, 6 -> 8 waves per CU), +8 %
+// at N=4096 F=0 (W=64, 4 -> 8); where the LDS form already fits 8 waves the
+// extra Philox VALU costs 4-10 % (profiles/r02_big_regen_ab.jsonl).
+static bool big_regen(const KParams &p) {
+  if (p.init_mode != BO_INIT_RANDOM || p.cont_round != 0u) return false;
+  return lds_groups_per_cu(p.hist_bytes + big_slice_words(p.W, big_nt(p.W), false) * 64u * 4u) < 8u;
+}
+
 uint32_t mfma_big_lds_bytes(const KParams &p, uint32_t bw) {
-  return p.hist_bytes + bw * big_slice_words(p.W, big_nt(p.W)) * 64u * 4u;
+  return p.hist_bytes + bw * big_slice_words(p.W, big_nt(p.W), big_regen(p)) * 64u * 4u;
 }
 
 // Waves per workgroup: the most resident waves per CU -- LDS (160 KB) against
@@ -292,16 +336,21 @@ uint32_t mfma_big_block_waves(const KParams &p) {
   return best;
 }
 
-template <int KIND, int NT, int BW>
-static hipError_t launch_big_kind(const KParams &p, int grid, hipStream_t s) {
+template <int KIND, int NT, int BW, bool REGEN>
+static hipError_t launch_big_regen(const KParams &p, int grid, hipStream_t s) {
   const uint32_t lds = mfma_big_lds_bytes(p, BW);
   if (lds > 64u * 1024u) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&benor_mfma_big_kernel<KIND, NT, BW>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&benor_mfma_big_kernel<KIND, NT, BW, REGEN>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((benor_mfma_big_kernel<KIND, NT, BW>), dim3(grid), dim3(64 * BW), lds, s, p);
+  hipLaunchKernelGGL((benor_mfma_big_kernel<KIND, NT, BW, REGEN>), dim3(grid), dim3(64 * BW), lds, s, p);
   return hipGetLastError();
+}
+
+template <int KIND, int NT, int BW>
+static hipError_t launch_big_kind(const KParams &p, int grid, hipStream_t s) {
+  return big_regen(p) ? launch_big_regen<KIND, NT, BW, true>(p, grid, s) : launch_big_regen<KIND, NT, BW, false>(p, grid, s);
 }
 
 template <int KIND, int NT>
