@@ -538,8 +538,82 @@ int bo_run_trials(const bo_trials_cfg *cfg, uint64_t trial_begin, uint64_t trial
   return rc;
 }
 
+// One trial with per-node state in lockstep mode (the network API's
+// /start, consensus.ts:3-8): every device operand -- live ids, initial planes,
+// node states, histogram, round count -- goes into one per-thread device buffer
+// that persists between calls, with one upload and one read-back.  A network of
+// the reference's size is then a few tens of microseconds, not the ten
+// allocations and frees of a plan.
+namespace {
+struct StateScratch {
+  int device = -1;
+  size_t bytes = 0;
+  unsigned char *d = nullptr;
+  std::vector<unsigned char> h;
+  // no destructor: freeing device memory while the process exits can race the
+  // HIP runtime's own teardown; the buffer is a few KB and the process owns it
+};
+thread_local StateScratch t_scratch;
+
+int run_states_lockstep(const bo_trials_cfg *cfg, uint64_t trial, bo_node_state *nodes_out, uint32_t *rounds_out) {
+  std::vector<uint32_t> live;
+  std::vector<uint4> plane;
+  benor::KParams kp;
+  int rc = plan_host(cfg, live, plane, kp);
+  if (rc) return rc;
+  int dev = 0;
+  rc = check_device(&dev);
+  if (rc) return rc;
+  const uint32_t N = cfg->N, H = bo_hist_len(cfg->k_max), m = kp.m;
+  // layout: states [N] | hist [H] u64 | rounds u32 (+pad) | live [m] u32 | init [W] uint4
+  const size_t o_st = 0, o_h = (sizeof(bo_node_state) * N + 15u) & ~size_t(15);
+  const size_t o_r = o_h + sizeof(uint64_t) * H, o_live = (o_r + 16u + 15u) & ~size_t(15);
+  const size_t o_init = (o_live + sizeof(uint32_t) * m + 15u) & ~size_t(15);
+  const size_t bytes = o_init + sizeof(uint4) * plane.size();
+  StateScratch &sc = t_scratch;
+  if (sc.device != dev || sc.bytes < bytes) {
+    if (sc.d) (void)hipFree(sc.d);
+    sc.d = nullptr;
+    sc.bytes = 0;
+    HIP_TRY(hipMalloc(&sc.d, bytes));
+    sc.bytes = bytes;
+    sc.device = dev;
+  }
+  sc.h.assign(bytes, 0);
+  // host-side initial states (node.ts:21-26); live entries are overwritten by the kernel
+  bo_node_state *st = reinterpret_cast<bo_node_state *>(sc.h.data() + o_st);
+  for (uint32_t i = 0; i < N; ++i) {
+    const bool f = cfg->faulty[i] != 0;
+    st[i].killed = f ? 1 : 0;
+    st[i].x = f ? -1 : (cfg->init_mode == BO_INIT_FIXED ? cfg->init[i] : -1);
+    st[i].decided = f ? -1 : 0;
+    st[i].pad = 0;
+    st[i].k = f ? -1 : 0;
+  }
+  if (m) std::memcpy(sc.h.data() + o_live, live.data(), sizeof(uint32_t) * m);
+  if (!plane.empty()) std::memcpy(sc.h.data() + o_init, plane.data(), sizeof(uint4) * plane.size());
+  HIP_TRY(hipMemcpy(sc.d, sc.h.data(), bytes, hipMemcpyHostToDevice));
+  bo_plan pl;                      // on the stack: its device tables are views into the scratch buffer
+  pl.kp = kp;
+  pl.cfg = *cfg;
+  pl.device = dev;
+  pl.live_ids = live;
+  pl.kp.live_ids = reinterpret_cast<uint32_t *>(sc.d + o_live);
+  pl.kp.init_plane = reinterpret_cast<uint4 *>(sc.d + o_init);
+  rc = plan_launch_impl(&pl, trial, 1, reinterpret_cast<uint64_t *>(sc.d + o_h),
+                        reinterpret_cast<bo_node_state *>(sc.d + o_st), reinterpret_cast<uint32_t *>(sc.d + o_r),
+                        nullptr);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpy(sc.h.data(), sc.d, o_r + sizeof(uint32_t), hipMemcpyDeviceToHost));
+  std::memcpy(nodes_out, sc.h.data() + o_st, sizeof(bo_node_state) * N);
+  if (rounds_out) std::memcpy(rounds_out, sc.h.data() + o_r, sizeof(uint32_t));
+  return BO_OK;
+}
+}  // namespace
+
 int bo_run_trial_states(const bo_trials_cfg *cfg, uint64_t trial, bo_node_state *nodes_out, uint32_t *rounds_out) {
   if (!cfg || !nodes_out) return fail(BO_ERR_INVALID_ARGUMENT, "NULL argument");
+  if (cfg->mode == BO_MODE_LOCKSTEP) return run_states_lockstep(cfg, trial, nodes_out, rounds_out);
   bo_plan *pl = nullptr;
   int rc = bo_plan_create(cfg, &pl);
   if (rc) return rc;
