@@ -14,6 +14,8 @@ analytic law by chi-square.
 """
 import itertools
 
+import os
+
 import numpy as np
 import pytest
 
@@ -241,6 +243,25 @@ def test_full_size_sharding_invariance_and_law():
     ref = oracle.run_trials(N, F, first_f(N, F), seed=0x243F6A8885A308D3, trial_begin=1_999_000,
                             trial_count=1000, k_max=k)
     np.testing.assert_array_equal(plan.run(1_999_000, 1000), ref.hist)
+
+
+@pytest.mark.parametrize("N,F,T", [(10, 4, 1_000_000), (5, 1, 300_000), (64, 21, 500_000), (10, 5, 200_000),
+                                   (256, 0, 2_000_000), (2048, 0, 100_000)])
+def test_histogram_independent_of_grid(N, F, T):
+    """The grid a launch gets (workgroups per CU: the lane kernel's short-launch
+    rule, LDS fit, the matrix-core continuation passes) only decides which wave
+    runs which trial ids: BENOR_BLOCKS_PER_CU = 1 or 3 gives the histogram of
+    the default grid, bit for bit."""
+    fl = first_f(N, F)
+    base = benor.TrialsPlan(N, F, fl, seed=4242, k_max=16).run(11, T)
+    for bpc in ("1", "3"):
+        os.environ["BENOR_BLOCKS_PER_CU"] = bpc
+        try:
+            got = benor.TrialsPlan(N, F, fl, seed=4242, k_max=16).run(11, T)
+        finally:
+            os.environ.pop("BENOR_BLOCKS_PER_CU", None)
+        np.testing.assert_array_equal(got, base)
+    assert base[:-1].sum() == T
 
 
 def test_launch_split_past_2_31_trials():
