@@ -62,12 +62,16 @@ EXPORTED_SYMBOLS = (
     "bo_plan_create", "bo_plan_launch", "bo_plan_run", "bo_plan_popc_words_per_node_round",
     "bo_plan_live_nodes", "bo_plan_destroy", "bo_run_trials", "bo_run_trial_states",
     "bo_popc_peak", "bo_last_error", "bo_abi_version", "bo_kernel_version", "bo_plan_kernel", "bo_kernel_for",
-    "bo_mfma_peak",
+    "bo_mfma_peak", "bo_consensus_start_sched",
 )
 
 
 class Error(Exception):
     """The reference's `new Error(message)` (launchNodes.ts:11,13)."""
+
+
+class AlreadyStartedError(RuntimeError):
+    """libbenor error 8: a second start on one network (its inboxes persist, node.ts:29-30)."""
 
 
 class NodeStateC(ctypes.Structure):
@@ -104,6 +108,8 @@ def lib() -> ctypes.CDLL:
     L.bo_network_create.argtypes = [ctypes.c_uint32, ctypes.c_uint32, P(ctypes.c_int8), ctypes.c_uint32,
                                     P(ctypes.c_uint8), ctypes.c_uint32, P(ctypes.c_void_p)]
     L.bo_consensus_start.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32]
+    L.bo_consensus_start_sched.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, P(ctypes.c_uint32),
+                                           ctypes.c_uint32]
     L.bo_consensus_stop.argtypes = [ctypes.c_void_p]
     L.bo_node_stop.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
     L.bo_get_state.argtypes = [ctypes.c_void_p, ctypes.c_uint32, P(NodeStateC)]
@@ -149,6 +155,8 @@ def _check(rc: int) -> None:
         msg = last_error()
         if rc in (BO_ERR_ARRAYS_DONT_MATCH, BO_ERR_FAULTY_COUNT):
             raise Error(msg)
+        if rc == BO_ERR_ALREADY_STARTED:
+            raise AlreadyStartedError(f"libbenor error {rc}: {msg}")
         raise RuntimeError(f"libbenor error {rc}: {msg}")
 
 
@@ -205,10 +213,20 @@ class Network:
             _lib.bo_network_destroy(h)
             self._h = None
 
-    def start(self, seed: int | None = None, k_max: int = DEFAULT_K_MAX) -> None:
+    def start(self, seed: int | None = None, k_max: int = DEFAULT_K_MAX, stop_after=None) -> None:
+        """stop_after: GET /stop requests that land during the run -- {node: deliveries} or a
+        length-N sequence (None = not stopped); deliveries = POST /message handled network-wide
+        before the stop (bo_consensus_start_sched: the event-level kernel, N <= 256)."""
         if seed is None:
             seed = secrets.randbits(64)        # the reference's coin is Math.random()
-        _check(lib().bo_consensus_start(self._h, seed, k_max))
+        if not stop_after:
+            _check(lib().bo_consensus_start(self._h, seed, k_max))
+            return
+        sched = [None] * self.N
+        for i, v in (stop_after.items() if isinstance(stop_after, dict) else enumerate(stop_after)):
+            sched[i] = v
+        arr = _crash_array(self.N, sched)
+        _check(lib().bo_consensus_start_sched(self._h, seed, k_max, arr, self.N))
 
     def stop(self) -> None:
         _check(lib().bo_consensus_stop(self._h))
@@ -247,12 +265,21 @@ def _net(N: int) -> Network:
     return _current
 
 
-def startConsensus(N: int, seed: int | None = None, k_max: int = DEFAULT_K_MAX) -> None:
+def startConsensus(N: int, seed: int | None = None, k_max: int = DEFAULT_K_MAX, stop_after=None,
+                   strict: bool = False) -> None:
     """src/nodes/consensus.ts:3-8: GET /start on every node, then the round
-    loop (node.ts:43-163) on the GPU until every live node decided or k_max."""
+    loop (node.ts:43-163) on the GPU until every live node decided or k_max.
+    stop_after: mid-run GET /stop schedule (Network.start).  A second start on
+    a network resolves as the reference's does (every GET /start answers 200)
+    but runs nothing: its inboxes persist (node.ts:29-30), so no fresh
+    consensus can follow; strict=True raises Error instead."""
     if N == 0:
         return
-    _net(N).start(seed, k_max)
+    try:
+        _net(N).start(seed, k_max, stop_after)
+    except AlreadyStartedError:
+        if strict:
+            raise
 
 
 def stopConsensus(N: int) -> None:

@@ -4,6 +4,7 @@
     python -m benor.cli trials --N 1024 --F 341 --trials 1000000          # one batch, JSON summary
     python -m benor.cli sweep --N 64,128,...,4096 --steps 32 --trials 2**30 --out sweep.csv
                                                                           # C5 phase diagram
+    python -m benor.cli sweep --cells 4096:0,4096:1984 --per-cell 4793490  # two cells of it
 
 `start` re-states src/start.ts:6-43: same default scenario (N = 10, nodes
 0-3 faulty, every initial value 1), same checks ("Lengths don't match",
@@ -103,10 +104,15 @@ def cmd_sweep(a) -> int:
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group(backend)
-    Ns = _ints(a.N)
-    phis = [i * 0.5 / a.steps for i in range(a.steps)]
-    cells = [(N, int(phi * N)) for N in Ns for phi in phis]
-    per_cell = max(1, _int(str(a.trials)) // len(cells))
+    if a.cells:
+        # selected cells of a full sweep, re-run at that sweep's per-cell budget (--per-cell):
+        # a cell's rows depend only on (N, F, seed, per-cell trials, k_max)
+        cells = [tuple(_int(x) for x in c.split(":")) for c in a.cells.split(",")]
+    else:
+        Ns = _ints(a.N)
+        phis = [i * 0.5 / a.steps for i in range(a.steps)]
+        cells = [(N, int(phi * N)) for N in Ns for phi in phis]
+    per_cell = _int(str(a.per_cell)) if a.per_cell else max(1, _int(str(a.trials)) // len(cells))
     t0 = time.perf_counter()
     stream = torch.cuda.current_stream()
     # Every cell's plan first, then all launches back to back into one [cells, H]
@@ -158,6 +164,8 @@ def main(argv=None) -> int:
     w.add_argument("--trials", default="2**30")
     w.add_argument("--seed", type=int, default=0x243F6A8885A308D3)
     w.add_argument("--k-max", type=int, default=32)
+    w.add_argument("--cells", default=None, help="N:F,N:F,... instead of the N x phi grid")
+    w.add_argument("--per-cell", default=None, help="trials per cell (default: --trials / cells)")
     w.add_argument("--out", default=None)
     w.add_argument("--progress", action="store_true")
     a = ap.parse_args(argv)

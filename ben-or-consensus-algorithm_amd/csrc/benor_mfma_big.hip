@@ -270,8 +270,12 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_big_kernel(KParams p) {
       const uint32_t dcols = (uint32_t)bd | (uint32_t)(bd >> 32);
       halt &= ~dcols;
       if (dcols) {
-        if (lane < 32u && ((dcols >> lane) & 1u))
-          seg[n_def + (uint32_t)__builtin_popcount(dcols & ((1u << lane) - 1u))] = toff;
+        if (lane < 32u && ((dcols >> lane) & 1u)) {
+          // the host sizes a segment for a wave's most groups per launch
+          // (plan_launch_impl); the bound only guards the buffer
+          const uint32_t idx = n_def + (uint32_t)__builtin_popcount(dcols & ((1u << lane) - 1u));
+          if (idx < p.defer_seg_cap) seg[idx] = toff;
+        }
         n_def += (uint32_t)__builtin_popcount(dcols);
       }
     }

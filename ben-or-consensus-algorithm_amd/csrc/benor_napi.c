@@ -6,9 +6,11 @@
  *   networkCreate(N, F, initialValues, faultyList) -> external handle
  *       launchNodes.ts:4-44 (throws Error("Arrays don't match") /
  *       Error("faultyList doesnt have F faulties") with the reference's text)
- *   networkStart(handle, seed:BigInt, kMax) -> Promise<void>
+ *   networkStart(handle, seed:BigInt, kMax[, stopAfter]) -> Promise<void>
  *       consensus.ts:3-8 + node.ts:167-188; runs the round loop kernel on a
- *       libuv worker thread (napi_async_work), so the event loop stays free
+ *       libuv worker thread (napi_async_work), so the event loop stays free;
+ *       stopAfter (array of N delivery counts, null/undefined = never): GET /stop
+ *       requests landing mid-run, node.ts:191-194 (bo_consensus_start_sched)
  *   networkStop(handle) / nodeStop(handle, i)       consensus.ts:10-15, node.ts:191-194
  *   getState(handle, i) -> {killed, x, decided, k}  node.ts:197-199
  *   status(handle, i) -> 500 | 200                  node.ts:33-39
@@ -140,6 +142,8 @@ typedef struct {
     bo_network *net;
     uint64_t seed;
     uint32_t k_max;
+    uint32_t *stop_after;      /* [n_stop] or NULL */
+    uint32_t n_stop;
     int rc;
     char err[512];
 } start_job;
@@ -147,7 +151,7 @@ typedef struct {
 static void start_execute(napi_env env, void *data) {
     (void)env;
     start_job *j = (start_job *)data;
-    j->rc = bo_consensus_start(j->net, j->seed, j->k_max);
+    j->rc = bo_consensus_start_sched(j->net, j->seed, j->k_max, j->stop_after, j->n_stop);
     if (j->rc) snprintf(j->err, sizeof j->err, "libbenor error %d: %s", j->rc, bo_last_error());
 }
 
@@ -165,14 +169,15 @@ static void start_complete(napi_env env, napi_status status, void *data) {
     }
     napi_delete_reference(env, j->net_ref);
     napi_delete_async_work(env, j->work);
+    free(j->stop_after);
     free(j);
 }
 
 static napi_value network_start(napi_env env, napi_callback_info info) {
-    size_t argc = 3;
-    napi_value argv[3];
+    size_t argc = 4;
+    napi_value argv[4];
     NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-    if (argc < 3) { napi_throw_type_error(env, NULL, "networkStart(handle, seed, kMax)"); return NULL; }
+    if (argc < 3) { napi_throw_type_error(env, NULL, "networkStart(handle, seed, kMax[, stopAfter])"); return NULL; }
     bo_network *net = get_net(env, argv[0]);
     if (!net) return NULL;
     start_job *j = (start_job *)calloc(1, sizeof *j);
@@ -184,6 +189,21 @@ static napi_value network_start(napi_env env, napi_callback_info info) {
     }
     int ok = 1;
     j->k_max = get_u32(env, argv[2], &ok);
+    bool is_arr = false;
+    if (argc > 3) napi_is_array(env, argv[3], &is_arr);
+    if (is_arr) {                               /* stop schedule: one entry per node */
+        uint32_t n = 0;
+        napi_get_array_length(env, argv[3], &n);
+        j->n_stop = n;
+        j->stop_after = (uint32_t *)malloc(sizeof(uint32_t) * (n ? n : 1));
+        for (uint32_t i = 0; i < n; ++i) {
+            napi_value e;
+            napi_valuetype t;
+            napi_get_element(env, argv[3], i, &e);
+            napi_typeof(env, e, &t);
+            j->stop_after[i] = (t == napi_null || t == napi_undefined) ? 0xFFFFFFFFu : get_u32(env, e, &ok);
+        }
+    }
     j->net = net;
     napi_create_reference(env, argv[0], 1, &j->net_ref);   /* keep the handle alive while running */
     napi_value promise, name;

@@ -166,12 +166,27 @@ int bo_consensus_stop(bo_network *net) {   // consensus.ts:10-15
 }
 
 int bo_consensus_start(bo_network *net, uint64_t seed, uint32_t k_max) {   // consensus.ts:3-8
+  return bo_consensus_start_sched(net, seed, k_max, nullptr, 0u);
+}
+
+// startConsensus with GET /stop requests landing during the run (node.ts:191-194
+// served while the round loop is in flight).  Without a schedule: the lockstep
+// round loop (every running node hears every running node).  With
+// one: the event-level kernel, delivery by delivery in the seeded order, each
+// scheduled /stop applied after its node's delivery count (oracle (iii)).
+int bo_consensus_start_sched(bo_network *net, uint64_t seed, uint32_t k_max, const uint32_t *stop_after,
+                             uint32_t n_stop_after) {
   if (!net) return fail(BO_ERR_INVALID_ARGUMENT, "net is NULL");
   if (k_max < 1 || k_max > BO_MAX_K) return fail(BO_ERR_INVALID_ARGUMENT, "k_max out of range");
   const uint32_t N = net->N;
+  if (stop_after && n_stop_after != N) return fail(BO_ERR_ARRAYS_DONT_MATCH, "stop schedule must have N entries");
+  bool scheduled = false;
+  for (uint32_t i = 0; stop_after && i < N; ++i) scheduled = scheduled || stop_after[i] != 0xFFFFFFFFu;
+  if (scheduled && N > benor::kMaxEventN)
+    return fail(BO_ERR_UNSUPPORTED, "a mid-run /stop schedule runs the event-level kernel: N <= 256");
   std::vector<uint8_t> crashed(N);
   std::vector<int8_t> x(N);
-  std::vector<uint32_t> active;
+  std::vector<uint32_t> active, sched(N, 0xFFFFFFFFu);
   {
     std::lock_guard<std::mutex> g(net->mu);
     // The reference's per-node inboxes (node.ts:29-30) live as long as the
@@ -188,7 +203,10 @@ int bo_consensus_start(bo_network *net, uint64_t seed, uint32_t k_max) {   // co
     for (uint32_t i = 0; i < N; ++i) {
       crashed[i] = net->st[i].killed ? 1 : 0;
       x[i] = net->st[i].killed ? 0 : net->st[i].x;
-      if (!net->st[i].killed) active.push_back(i);
+      if (!net->st[i].killed) {
+        active.push_back(i);
+        if (stop_after) sched[i] = stop_after[i];
+      }
     }
     if (active.empty()) { net->started = true; return BO_OK; }
     const int64_t quorum = (int64_t)N - (int64_t)net->F;
@@ -211,10 +229,11 @@ int bo_consensus_start(bo_network *net, uint64_t seed, uint32_t k_max) {   // co
   cfg.F = net->F;
   cfg.k_max = k_max;
   cfg.init_mode = BO_INIT_FIXED;
-  cfg.mode = BO_MODE_LOCKSTEP;
+  cfg.mode = scheduled ? BO_MODE_EVENT : BO_MODE_LOCKSTEP;
   cfg.seed = seed;
   cfg.faulty = crashed.data();
   cfg.init = x.data();
+  cfg.crash_at = scheduled ? sched.data() : nullptr;
   // Launch-time validation is already done; here the crashed set is the
   // killed set, which has exactly N - quorum = F members at this point.
   std::vector<bo_node_state> states(N);
@@ -226,12 +245,13 @@ int bo_consensus_start(bo_network *net, uint64_t seed, uint32_t k_max) {   // co
     net->started = false;          // nothing ran: the start may be retried
     return rc;
   }
-  // A GET /stop served while the kernel ran is ordered after the run: the
-  // node keeps its final x / decided / k and stays killed.
+  // A scheduled /stop is part of the run (the kernel's killed flag); one
+  // served while the kernel ran is ordered after it: the node keeps its final
+  // x / decided / k and stays killed.
   for (uint32_t i : active) {
     const int8_t killed = net->st[i].killed;
     net->st[i] = states[i];
-    net->st[i].killed = killed;
+    net->st[i].killed = (int8_t)(killed | states[i].killed);
   }
   // The reference's auto-stop (node.ts:116-145): after its P-phase a node asks
   // every node's /getState and, when every answer has `decided` truthy, sends
@@ -441,9 +461,18 @@ static int plan_launch_impl(bo_plan *pl, uint64_t trial_begin, uint64_t trial_co
     const uint64_t cap = std::min<uint64_t>(trial_count, benor::kDeferChunk);
     kp.trial_count = cap;
     const int grid = benor::lockstep_grid(kp, pl->device);
-    const uint64_t waves = (uint64_t)grid * benor::block_waves(kp);
-    const uint64_t seg_cap = ((cap + 31u) / 32u + waves - 1u) / waves * 32u;   // a wave's trials per launch, at most
-    const uint64_t words = 2u * cap + 64u + waves * seg_cap;                   // two lists, their lengths, segments
+    // Every launch of the chunk (round 1 and the continuation passes) runs on
+    // `grid` workgroups, but the big-network form may pick a different
+    // workgroup size for the continuations (no x regeneration there, so a
+    // larger LDS slice: ADVICE r02).  A wave runs at most ceil(groups / waves)
+    // 32-trial groups of a launch, so the segments are sized for the launch
+    // with the fewest waves and allocated for the one with the most.
+    benor::KParams kc0 = kp;
+    kc0.cont_round = 2u;
+    const uint64_t bw1 = benor::block_waves(kp), bw2 = benor::block_waves(kc0);
+    const uint64_t waves_min = (uint64_t)grid * std::min(bw1, bw2), waves = (uint64_t)grid * std::max(bw1, bw2);
+    const uint64_t seg_cap = ((cap + 31u) / 32u + waves_min - 1u) / waves_min * 32u;   // a wave's trials per launch, at most
+    const uint64_t words = 2u * cap + 64u + waves * seg_cap;                           // two lists, their lengths, segments
     if (pl->defer_words < words) {
       if (pl->d_defer) (void)hipFree(pl->d_defer);
       pl->d_defer = nullptr;

@@ -30,6 +30,15 @@ const BASE_NODE_PORT = 3000;   // src/config.ts:1
 async function launchNetwork(N, F, initialValues, faultyList, options = {}) {
   const basePort = options.basePort !== undefined ? options.basePort : BASE_NODE_PORT;
   const kMax = options.kMax !== undefined ? options.kMax : 64;
+  // options.stopAfter: GET /stop requests that land during the run, as delivery
+  // counts per node (array of N, null = never; bo_consensus_start_sched).  The
+  // run is one kernel, so a /stop request arriving over HTTP while it is in
+  // flight is ordered after it; a scheduled one lands mid-round.
+  let sched;
+  if (options.stopAfter !== undefined && options.stopAfter !== null) {
+    sched = new Array(N).fill(null);
+    for (const [i, v] of Object.entries(options.stopAfter)) sched[Number(i)] = v;
+  }
   const handle = addon.networkCreate(N, F, initialValues, faultyList);   // launchNodes.ts:10-13 errors
   const net = {
     handle, N, started: new Array(N).fill(false), running: null, ran: false, seed: options.seed,
@@ -49,7 +58,7 @@ async function launchNetwork(N, F, initialValues, faultyList, options = {}) {
     if (seed === undefined) {
       seed = (BigInt(Math.floor(Math.random() * 2 ** 32)) << 32n) | BigInt(Math.floor(Math.random() * 2 ** 32));
     }
-    net.running = addon.networkStart(handle, BigInt(seed), kMax).then(() => {
+    net.running = addon.networkStart(handle, BigInt(seed), kMax, sched).then(() => {
       net.ran = true;
       net.running = null;
     });

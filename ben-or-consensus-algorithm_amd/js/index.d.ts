@@ -35,6 +35,12 @@ export interface StartOptions {
   seed?: bigint | number;
   /** Round cap (default 64). */
   kMax?: number;
+  /** GET /stop requests landing mid-run (node.ts:191-194): per node, the number of
+   * POST /message deliveries (network-wide, seeded order) after which it is stopped;
+   * an array of N entries (null = never) or {nodeId: deliveries}.  Event-level kernel, N <= 256. */
+  stopAfter?: (number | null)[] | { [nodeId: number]: number };
+  /** Reject a second start on one network (libbenor error 8) instead of resolving as a no-op. */
+  strict?: boolean;
 }
 
 export declare function startConsensus(N: number, options?: StartOptions): Promise<void>;

@@ -49,13 +49,28 @@ function randomSeed() {
 // Resolves once the round loop has run to completion (all live nodes decided,
 // or kMax rounds).  The reference resolves before consensus finishes and the
 // callers poll getNodesState; polling here sees the final states at once.
-// A second start on the same network rejects: the reference's round inboxes
-// outlive a run (node.ts:29-30), so it would not be a fresh consensus.
+// options.stopAfter: GET /stop requests that land while consensus runs
+// (node.ts:191-194) -- an array of N delivery counts or an object
+// {nodeId: deliveries}; a node is stopped after that many POST /message have
+// been handled network-wide (seeded delivery order, the event-level kernel,
+// N <= 256).
+// A second start on the same network resolves, as the reference's GET /start
+// answers 200, but runs nothing: its round inboxes outlive a run (node.ts:29-30),
+// so no fresh consensus can follow (options.strict: reject with libbenor error 8).
 async function startConsensus(N, options = {}) {
   if (N === 0) return;
   const seed = options.seed !== undefined ? BigInt(options.seed) : randomSeed();
   const kMax = options.kMax !== undefined ? options.kMax : DEFAULT_K_MAX;
-  await addon.networkStart(net(N).handle, seed, kMax);
+  let sched;
+  if (options.stopAfter !== undefined && options.stopAfter !== null) {
+    sched = new Array(N).fill(null);
+    for (const [i, v] of Object.entries(options.stopAfter)) sched[Number(i)] = v;
+  }
+  try {
+    await addon.networkStart(net(N).handle, seed, kMax, sched);
+  } catch (e) {
+    if (options.strict || !/libbenor error 8:/.test(e.message)) throw e;
+  }
 }
 
 async function stopConsensus(N) {

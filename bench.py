@@ -341,6 +341,17 @@ def main():
         merge_histogram(step_hist)              # RCCL merge of the outcome histograms
         hist.add_(step_hist)
 
+    # Clock ramp before the warm-up steps: ~0.3 s of the matrix-core (or
+    # popcount) peak probe, whose figure is reported as roofline.peak_probe.
+    # Without it the first bench launches run ~13 % slower while the clocks
+    # rise, and a kernel trace of this command averages them in
+    # (profiles/r03-v0_summary.md).
+    mfma = plan.kernel == benor.BO_KERNEL_MFMA
+    peak_measured = None
+    if not args.no_peak_probe:
+        t_ramp = time.perf_counter()
+        while time.perf_counter() - t_ramp < 0.3:
+            peak_measured = 2 * benor.mfma_peak(10) if mfma else benor.popc_peak(10)
     for s in range(args.warmup):
         step(s)
     torch.cuda.synchronize()
@@ -373,11 +384,7 @@ def main():
     my_trials = rank_range(args.scaling, args.warmup, rank, world, T)[1]
     per_launch_nr = live_nr * my_trials / total_trials
     avg_kernel_s = float(np.mean(kern_ms)) * 1e-3
-    mfma = plan.kernel == benor.BO_KERNEL_MFMA
     achieved = per_launch_nr * words_per_nr / avg_kernel_s
-    peak_measured = None
-    if not args.no_peak_probe:
-        peak_measured = 2 * benor.mfma_peak(10) if mfma else benor.popc_peak(10)
     kver = benor.kernel_version()
     traffic = None
     tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")

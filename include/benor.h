@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define BENOR_ABI_VERSION 4
+#define BENOR_ABI_VERSION 5
 
 /* Return codes.  The first two are the reference's two launch errors. */
 enum {
@@ -100,6 +100,20 @@ int bo_network_create(uint32_t N, uint32_t F,
  * after it: the node keeps its final state and is killed. */
 int bo_consensus_start(bo_network *net, uint64_t seed, uint32_t k_max);
 
+/* startConsensus(N) with GET /stop requests that land while consensus runs
+ * (node.ts:191-194 served mid-round; from then on the node drops every
+ * message, node.ts:45).  stop_after[i] (n_stop_after == N entries) = number
+ * of POST /message deliveries, network-wide, after which node i is stopped;
+ * UINT32_MAX = not stopped.  Deliveries follow BO_MODE_EVENT's seeded order
+ * (trial 0 of `seed`), so a schedule is reproducible.  With every entry
+ * UINT32_MAX (or stop_after NULL) this is bo_consensus_start; otherwise the
+ * run is message-granular on the event-level kernel (N <= 256, else
+ * BO_ERR_UNSUPPORTED) and the per-node states are its final ones, scheduled
+ * stops included (killed, x / decided / k as of the stop).  The auto-stop and
+ * one-start rules of bo_consensus_start apply. */
+int bo_consensus_start_sched(bo_network *net, uint64_t seed, uint32_t k_max,
+                             const uint32_t *stop_after, uint32_t n_stop_after);
+
 /* stopConsensus(N)  (consensus.ts:10-15) -> GET /stop on every node (node.ts:191-194). */
 int bo_consensus_stop(bo_network *net);
 
@@ -153,7 +167,11 @@ int bo_plan_create(const bo_trials_cfg *cfg, bo_plan **out);
 
 /* Run global trial ids [trial_begin, trial_begin + trial_count) and ADD their
  * outcomes into hist_dev (device pointer, bo_hist_len(k_max) uint64).
- * Asynchronous on `stream` (hipStream_t or NULL). */
+ * Asynchronous on `stream` (hipStream_t or NULL).  A plan owns per-plan
+ * device scratch (the matrix-core kernels' deferred-trial lists, the event
+ * mode's message pools), so launches of ONE plan must be issued from one host
+ * thread at a time and ordered on one stream (or separated by a
+ * synchronisation); concurrent launches need one plan each. */
 int bo_plan_launch(bo_plan *plan, uint64_t trial_begin, uint64_t trial_count,
                    uint64_t *hist_dev, void *stream);
 

@@ -27,6 +27,8 @@ def tie_prob(m: int, p: float = 0.5) -> float:
     if m % 2:
         return 0.0
     h = m // 2
+    if p == 0.5:
+        return comb(m, h) / (1 << m)          # exact big-integer ratio: no overflow at m in the thousands
     return comb(m, h) * (p ** h) * ((1 - p) ** h)
 
 

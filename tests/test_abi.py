@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol():
     L = benor.lib()
     for s in header_symbols():
         assert hasattr(L, s)
-    assert L.bo_abi_version() == 4
+    assert L.bo_abi_version() == 5
     assert L.bo_hist_len(64) == 65 * 3 + 1
 
 
@@ -88,7 +88,7 @@ def test_reference_accepts_what_it_accepts():
     assert benor.getNodesState(2)[0]["x"] is None
 
 
-def test_second_start_refused_without_gpu_work():
+def test_second_start_without_gpu_work():
     """A start that stalls (a node stopped first: fewer than N-F senders,
     node.ts:52) needs no device; a second start is refused either way --
     the reference's inboxes persist across /start (node.ts:29-30)."""
@@ -96,8 +96,10 @@ def test_second_start_refused_without_gpu_work():
     nodes[0]._net.stop_node(0)
     benor.startConsensus(5, seed=3)
     assert [s["k"] for s in benor.getNodesState(5)] == [0, 1, 1, 1, None]
+    benor.startConsensus(5, seed=3)                     # resolves, runs nothing (the reference answers 200)
+    assert [s["k"] for s in benor.getNodesState(5)] == [0, 1, 1, 1, None]
     with pytest.raises(RuntimeError, match="libbenor error 8: consensus already started"):
-        benor.startConsensus(5, seed=3)
+        benor.startConsensus(5, seed=3, strict=True)
 
 
 def test_network_create_null_arrays():

@@ -152,17 +152,19 @@ def test_stopped_nodes_stall():
     assert all(s["k"] == 1 and s["decided"] is False for s in st[1:4])
 
 
-def test_second_start_is_refused():
+def test_second_start_is_a_no_op():
     """The reference's round inboxes (node.ts:29-30) outlive a run, so a second
     GET /start re-triggers every round-1 tally (node.ts:47-52) instead of
-    running a fresh consensus: the network API refuses it and keeps the
-    first run's states."""
+    running a fresh consensus.  startConsensus resolves as the reference's does
+    (every /start answers 200) and runs nothing: the first run's states stay;
+    the C ABI (and strict=True) reports BO_ERR_ALREADY_STARTED."""
     benor.launchNetwork(6, 2, [0, 0, 1, 1, 0, 1], [True, False, False, False, False, True])
     benor.startConsensus(6, seed=1)
     a = benor.getNodesState(6)
-    with pytest.raises(RuntimeError, match="already started"):
-        benor.startConsensus(6, seed=1)
+    benor.startConsensus(6, seed=2)
     assert benor.getNodesState(6) == a and all(s["decided"] for s in a[1:5])
+    with pytest.raises(benor.AlreadyStartedError, match="already started"):
+        benor.startConsensus(6, seed=1, strict=True)
 
 
 def test_stop_during_run_is_kept():

@@ -211,6 +211,37 @@ def test_mfma_deferral_fixed_init_matches_oracle(N, F, q):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("k_max", [1, 2, 3])
+@pytest.mark.parametrize("N,F", [(256, 0), (1000, 333), (300, 140), (2048, 0), (3000, 1400)])
+def test_mfma_deferral_small_kmax_matches_oracle(N, F, k_max):
+    """k_max 1..3 against the continuation passes: the host runs
+    matrix-core rounds 2 .. min(3, k_max - 1) and leaves the rest to the
+    popcount kernel, whose trials then reach k_max undecided.  KIND 1 and 2,
+    small- and big-network forms."""
+    seed = 0xC0FFEE ^ (N << 8) ^ k_max
+    p = plan(N, F, seed=seed, k_max=k_max)
+    assert p.kernel == benor.BO_KERNEL_MFMA
+    begin, T = (1 << 33) + 3 * N, 3000 + N % 71
+    got = p.run(begin, T)
+    ref = oracle.run_trials(N, F, first_f(N, F), seed=seed, trial_begin=begin, trial_count=T, k_max=k_max)
+    np.testing.assert_array_equal(got, ref.hist)
+
+
+@pytest.mark.gpu
+def test_mfma_deferral_two_chunks_matches_oracle():
+    """One launch just above kDeferChunk (2^22) trials at a non-zero trial_begin:
+    the second deferral chunk starts at trial_begin + 2^22."""
+    N, F, seed = 100, 0, 99
+    T, begin = (1 << 22) + 1001, (1 << 32) + 12345
+    p = plan(N, F, seed=seed, k_max=8)
+    assert p.kernel == benor.BO_KERNEL_MFMA
+    got = p.run(begin, T)
+    ref = oracle.run_trials(N, F, first_f(N, F), seed=seed, trial_begin=begin, trial_count=T, k_max=8,
+                            threads=min(16, os.cpu_count() or 1))
+    np.testing.assert_array_equal(got, ref.hist)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("N,F,T", [(128, 0, 9_000_001), (1024, 0, 1_000_003), (600, 250, 2_000_001), (257, 127, 5_000_000)])
 def test_mfma_deferral_equals_popcount_kernel(N, F, T):
     """Over several deferral chunks (kDeferChunk = 2^22 trials): the same

@@ -69,7 +69,7 @@ def main():
         print(json.dumps({"N": N, "F": F, "f": f, "mode": ["lockstep", "random", "event"][mode], "trials": trials,
                           "mean_rounds": rounds / trials, "ms": round(ms, 3), "node_rounds_per_s": rate,
                           "popc_frac": rate * words / PEAK,
-                          "agreement_violations": int(hist[-1]),
+                          "agreement_violations": int(hist[-1]), "kernel_version": benor.kernel_version(),
                           # event level: each live node-round is 2 broadcasts of N messages
                           "messages_per_s": rate * 2 * N if mode == 2 else None}), flush=True)
 
