@@ -342,16 +342,29 @@ def main():
         hist.add_(step_hist)
 
     # Clock ramp before the warm-up steps: ~0.3 s of the matrix-core (or
-    # popcount) peak probe, whose figure is reported as roofline.peak_probe.
-    # Without it the first bench launches run ~13 % slower while the clocks
-    # rise, and a kernel trace of this command averages them in
-    # (profiles/r03-v0_summary.md).
+    # popcount) peak probe, whose figure is reported as roofline.peak_probe,
+    # then ~0.2 s of a neighbouring shape's kernel (F - 1: the same kernel
+    # family and instruction mix under another template instance, so a kernel
+    # trace keeps it apart from the bench kernel).  Without the ramp the first
+    # two bench launches run 6-15 % slower while clocks and power settle, and a
+    # kernel trace of this command averages them in (profiles/r03-v0_summary.md,
+    # profiles/r03-v1_summary.md).
     mfma = plan.kernel == benor.BO_KERNEL_MFMA
     peak_measured = None
     if not args.no_peak_probe:
         t_ramp = time.perf_counter()
         while time.perf_counter() - t_ramp < 0.3:
             peak_measured = 2 * benor.mfma_peak(10) if mfma else benor.popc_peak(10)
+        if F > 0:
+            ramp = benor.TrialsPlan(N, F - 1, [i < F - 1 for i in range(N)], seed=args.seed ^ 0x5A5A, k_max=k_max)
+            ramp_hist = torch.zeros(ramp.hist_len, dtype=torch.int64, device="cuda")
+            t_ramp = time.perf_counter()
+            r = 0
+            while time.perf_counter() - t_ramp < 0.2:
+                ramp.launch(r * T, T, ramp_hist.data_ptr(), stream.cuda_stream)
+                torch.cuda.synchronize()
+                r += 1
+            del ramp, ramp_hist
     for s in range(args.warmup):
         step(s)
     torch.cuda.synchronize()
