@@ -46,9 +46,10 @@ BO_KERNEL_RANDOM = 2
 BO_KERNEL_EVENT = 4
 BO_KERNEL_LANE = 6
 BO_KERNEL_MFMA = 7
+BO_KERNEL_MFMA_SMALL = 8
 KERNEL_NAMES = {BO_KERNEL_NONE: "none", BO_KERNEL_BLOCKED: "blocked popcount", BO_KERNEL_W: "W popcount",
                 BO_KERNEL_RANDOM: "random delivery", BO_KERNEL_EVENT: "event level", BO_KERNEL_LANE: "lane",
-                BO_KERNEL_MFMA: "matrix core (e2m1 MFMA)"}
+                BO_KERNEL_MFMA: "matrix core (e2m1 MFMA)", BO_KERNEL_MFMA_SMALL: "packed matrix core (e2m1 MFMA, m <= 32)"}
 BO_MAX_N = 4096
 BO_MAX_K = 1024
 

@@ -22,6 +22,8 @@ constexpr int kWavesPerBlock = 4;          // 256-thread workgroups, one trial p
 constexpr uint32_t kMaxW = BO_MAX_N / 64;  // u64 words per bit plane at N = 4096
 constexpr int kMaxWSpecialised = 32;       // m <= 2048: fully unrolled W-specialised kernel
 constexpr uint32_t kMaxLaneM = 64;         // m <= 64: lane kernel, one trial per lane (benor_lane.h)
+constexpr uint32_t kMaxSmallMfmaM = 32;    // 2 <= m <= 32: packed matrix-core kernel, 64 * min(32 / m, 8)
+                                           // trials per wave iteration (benor_mfma_small.h)
 constexpr uint32_t kMaxMfmaM = 1024;       // matrix-core kernel (benor_mfma.h): W <= 16, operands in registers;
                                            // beyond, the big-network form (runtime W, proposals in LDS) to BO_MAX_N
 constexpr uint32_t kMaxEventN = 256;       // event level: node ids in 8 bits of a message
@@ -41,6 +43,8 @@ struct KParams {
   uint32_t nblocks;         // ceil(W / G)
   uint32_t variant;         // 7: matrix-core lockstep, round 1 (benor_mfma.h; the W kernel serves its state
                             //    launches and the trials it defers),
+                            // 8: packed matrix-core lockstep (2 <= m <= 32, benor_mfma_small.h; the lane kernel
+                            //    serves its state launches),
                             // 6: lane lockstep (m <= 64), 1: W-specialised lockstep (W <= kMaxWSpecialised = 32),
                             // 0: blocked lockstep, 2: random delivery, 4: event level
   uint32_t base_variant;    // variant 7: the popcount kernel (1 W, 0 blocked) that serves the state
@@ -107,6 +111,13 @@ hipError_t launch_b(const KParams &p, int grid_blocks, hipStream_t stream);
 // Lane kernel (benor_lane.h), m = 1..kMaxLaneM, instantiated in benor_lane_*.hip.
 template <int MM>
 hipError_t launch_lane_m(const KParams &p, int grid_blocks, hipStream_t stream);
+
+// Packed matrix-core kernel (benor_mfma_small.h), m = 2..32, benor_mfma_small_02_32.hip.
+template <int MM>
+hipError_t launch_mfma_small_m(const KParams &p, int grid_blocks, hipStream_t stream);
+constexpr uint32_t small_slots(uint32_t m) { return (32u / m) < 8u ? (32u / m) : 8u; }
+// LDS words per wave: round-2 and round-3 lists (2 batches each), lane-path queue
+constexpr uint32_t small_wave_words(uint32_t m) { return 2u * 2u * 64u * small_slots(m) + 64u + 64u * small_slots(m); }
 
 // Matrix-core kernel (benor_mfma.h), W = 2..16, instantiated in benor_mfma_*.hip;
 // W = 17..64 (m <= 4096): the big-network form, benor_mfma_big.hip.

@@ -777,6 +777,17 @@ void plan_geometry(KParams &p) {
     p.variant = 6;
     p.wave_bytes = 128u * 8u + 128u * 16u;          // init-word ring, coin-block ring
     p.lds_bytes = p.hist_bytes + kWavesPerBlock * p.wave_bytes;
+    // Packed matrix-core kernel (benor_mfma_small.h): 2 <= m <= 32, every
+    // trial can decide (m > F) and no "?" initial value (every vote count is
+    // m).  The lane kernel planned above serves the state launches (network
+    // API); the packed kernel re-runs its rare leftovers itself.
+    const char *no_mfma = getenv("BENOR_NO_MFMA");
+    if (p.m >= 2u && p.m <= kMaxSmallMfmaM && p.m > p.F && p.init_q == 0u && !(no_mfma && no_mfma[0] == '1')) {
+      p.base_variant = p.variant;
+      p.base_G = p.G;
+      p.variant = 8;
+      p.lds_bytes = p.hist_bytes + kWavesPerBlock * small_wave_words(p.m) * 4u;
+    }
     return;
   }
   const uint32_t nph = (W + 1u) / 2u, tb = 64u / nph;   // init ring: tb trials per Philox pass
@@ -844,6 +855,13 @@ static hipError_t dispatch_lane(const KParams &p, int grid, hipStream_t s, std::
 }
 
 template <int... Is>
+static hipError_t dispatch_mfma_small(const KParams &p, int grid, hipStream_t s, std::integer_sequence<int, Is...>) {
+  hipError_t e = hipErrorInvalidValue;
+  (void)((p.m == (uint32_t)(Is + 2) ? (e = launch_mfma_small_m<Is + 2>(p, grid, s), true) : false) || ...);
+  return e;
+}
+
+template <int... Is>
 static hipError_t dispatch_mfma(const KParams &p, int grid, hipStream_t s, std::integer_sequence<int, Is...>) {
   hipError_t e = hipErrorInvalidValue;
   (void)((p.W == (uint32_t)(Is + 2) ? (e = launch_mfma<Is + 2>(p, grid, s), true) : false) || ...);
@@ -875,6 +893,15 @@ hipError_t launch_lockstep(const KParams &p, int grid, hipStream_t s) {
     return hipGetLastError();
   }
   if (p.variant == 6) return dispatch_lane(p, grid, s, std::make_integer_sequence<int, (int)kMaxLaneM>{});
+  if (p.variant == 8 && !p.node_out && !p.rounds_out)
+    return dispatch_mfma_small(p, grid, s, std::make_integer_sequence<int, (int)kMaxSmallMfmaM - 1>{});   // m = 2..32
+  if (p.variant == 8) {                      // state launch of a packed shape: the lane kernel
+    KParams q = p;
+    q.variant = p.base_variant;
+    q.G = p.base_G;
+    q.lds_bytes = q.hist_bytes + kWavesPerBlock * q.wave_bytes;
+    return launch_lockstep(q, grid, s);
+  }
   if (p.variant == 2) {
     if (p.lds_bytes > 64u * 1024u) {
       hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&benor_random_kernel),
@@ -914,6 +941,34 @@ int lockstep_grid(const KParams &p, int device) {
     uint64_t grid = p.ev_lanes / 256u;
     if (blocks_needed < grid) grid = blocks_needed;
     return (int)(grid < 1 ? 1 : grid);
+  }
+  if (p.variant == 8) {
+    if (p.node_out || p.rounds_out) {        // state launch: the lane kernel
+      KParams q = p;
+      q.variant = p.base_variant;
+      q.G = p.base_G;
+      q.lds_bytes = q.hist_bytes + kWavesPerBlock * q.wave_bytes;
+      return lockstep_grid(q, device);
+    }
+    // Packed matrix-core kernel: a wave runs 64 * S trials per iteration and
+    // drains its round-2/3 lists and lane-path queue at the end, so each wave
+    // takes ~3 batches of fresh trials (fewer, longer-lived waves amortise the
+    // drain), at most what LDS admits per CU and 2 workgroups per CU.
+    const uint64_t batch = 64u * small_slots(p.m);
+    const uint64_t groups = (p.trial_count + batch - 1u) / batch;
+    uint64_t per_cu = groups / ((uint64_t)cus * kWavesPerBlock * 3u);
+    uint64_t cap = lds_groups_per_cu(p.lds_bytes);
+    if (cap > 2u) cap = 2u;
+    if (per_cu > cap) per_cu = cap;
+    if (per_cu < 1u) per_cu = 1u;
+    if (const char *ev = getenv("BENOR_BLOCKS_PER_CU")) {   // tuning knob
+      const uint64_t v = strtoull(ev, nullptr, 10);
+      if (v >= 1u && v <= lds_groups_per_cu(p.lds_bytes)) per_cu = v;
+    }
+    uint64_t grid = (uint64_t)cus * per_cu;
+    const uint64_t need = (groups + kWavesPerBlock - 1u) / kWavesPerBlock;
+    if (need < grid) grid = need;
+    return (int)(grid < 1u ? 1u : grid);
   }
   // 32 waves per CU when registers and LDS allow it.
   const bool mfma = p.variant == 7 && !p.node_out && !p.rounds_out;

@@ -198,11 +198,14 @@ enum {
   BO_KERNEL_RANDOM = 2,
   BO_KERNEL_EVENT = 4,
   BO_KERNEL_LANE = 6,
-  BO_KERNEL_MFMA = 7
+  BO_KERNEL_MFMA = 7,
+  BO_KERNEL_MFMA_SMALL = 8 /* packed matrix-core kernel: 2 <= m <= 32, m > F, no "?" initial value;
+                              64 * min(32/m, 8) trials per wave iteration, block-diagonal e2m1 products */
 };
 
 /* The kernel family bo_plan_launch runs for this plan.  (The per-node-state
- * launch behind the network API runs the W kernel for an MFMA shape.) */
+ * launch behind the network API runs the W kernel for an MFMA shape and the
+ * lane kernel for an MFMA_SMALL shape.) */
 int bo_plan_kernel(const bo_plan *plan);
 
 /* The same choice for a configuration, made on the host (no device needed):

@@ -65,7 +65,8 @@ def test_kernel_choice():
     assert K.kernel_for(1537, 512) == K.BO_KERNEL_MFMA            # m = 1025: the big-network form
     assert K.kernel_for(4096, 1365) == K.BO_KERNEL_MFMA           # m = 2731
     assert K.kernel_for(4096, 2048) == K.BO_KERNEL_W              # m = F: never decides
-    assert K.kernel_for(10, 4) == K.BO_KERNEL_LANE                # m <= 64
+    assert K.kernel_for(10, 4) == K.BO_KERNEL_MFMA_SMALL          # m <= 32, m > F: packed matrix-core kernel
+    assert K.kernel_for(64, 21) == K.BO_KERNEL_LANE               # 32 < m <= 64
     assert K.kernel_for(96, 31) == K.BO_KERNEL_MFMA               # m = 65
     assert K.kernel_for(1024, 341, mode=K.BO_MODE_RANDOM_DELIVERY) == K.BO_KERNEL_RANDOM
     assert K.kernel_for(10, 4, mode=K.BO_MODE_EVENT) == K.BO_KERNEL_EVENT

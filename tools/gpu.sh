@@ -10,7 +10,8 @@
 # says which files were copied into profiles/ from which step.
 #
 #   smoke           __graft_entry__.smoke()
-#   tests           pytest -m gpu (PYTEST_ARGS, default the whole GPU suite)
+#   tests           pytest -m gpu (PYTEST_ARGS: test paths / options, default the whole GPU suite)
+#   probe           tools/mfma_fp4_layout_probe (e2m1 MFMA K pairing)
 #   bench           python bench.py (BENCH_ARGS, default the driver's --steps 20 --warmup 5)
 #   trace           rocprofv3 --kernel-trace --stats of the same bench command
 #   pmc:<shape>     PMC passes (PMC_GROUPS, '|'-separated, one rocprofv3 run each) over one
@@ -53,9 +54,12 @@ for step in "$@"; do
       timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
       chk $? smoke; tail -1 "$OUT/smoke.log";;
     tests)
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread \
-        ${PYTEST_ARGS:-} > "$OUT/tests.log" 2>&1
+      timeout -k 10 900 python -u -m pytest ${PYTEST_ARGS:-tests} -m gpu -x -v --timeout 200 --timeout-method thread \
+        > "$OUT/tests.log" 2>&1
       rc=$?; tail -3 "$OUT/tests.log"; chk $rc tests;;
+    probe)
+      timeout -k 10 60 "$R/tools/mfma_fp4_layout_probe" > "$OUT/fp4_probe.txt" 2>&1
+      rc=$?; tail -3 "$OUT/fp4_probe.txt"; chk $rc probe;;
     bench)
       timeout -k 10 400 python -u bench.py $BENCH_ARGS > "$OUT/bench.log" 2>&1
       rc=$?; tail -c 600 "$OUT/bench.log"; echo; chk $rc bench;;
