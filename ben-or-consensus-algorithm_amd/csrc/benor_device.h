@@ -63,6 +63,27 @@ __device__ __forceinline__ uint4 philox4x32_10(uint32_t k0, uint32_t k1, uint4 c
   return c;
 }
 
+// Philox4x32-10 of K counters at once, round by round, so that the K
+// independent dependency chains interleave in the instruction stream (one
+// wave computing several blocks is otherwise latency-bound on the products).
+template <int K>
+__device__ __forceinline__ void philox4x32_10_multi(uint32_t k0, uint32_t k1, uint4 (&c)[K]) {
+  k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)k0);
+  k1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)k1);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      const uint64_t p0 = mul_wide(c[i].x, 0xD2511F53u);
+      const uint64_t p1 = mul_wide(c[i].z, 0xCD9E8D57u);
+      c[i] = make_uint4(xor3_key((uint32_t)(p1 >> 32), c[i].y, k0), (uint32_t)p1,
+                        xor3_key((uint32_t)(p0 >> 32), c[i].w, k1), (uint32_t)p0);
+    }
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+
 // One receiver's tally step: acc + popcount(word).  Opaque on purpose (see
 // the header comment): the per-receiver count must execute per receiver.
 __device__ __forceinline__ uint32_t tally(uint32_t word, uint32_t acc) {

@@ -116,8 +116,6 @@ hipError_t launch_lane_m(const KParams &p, int grid_blocks, hipStream_t stream);
 template <int MM>
 hipError_t launch_mfma_small_m(const KParams &p, int grid_blocks, hipStream_t stream);
 constexpr uint32_t small_slots(uint32_t m) { return (32u / m) < 8u ? (32u / m) : 8u; }
-// LDS words per wave: round-2 and round-3 lists (2 batches each), lane-path queue
-constexpr uint32_t small_wave_words(uint32_t m) { return 2u * 2u * 64u * small_slots(m) + 64u + 64u * small_slots(m); }
 
 // Matrix-core kernel (benor_mfma.h), W = 2..16, instantiated in benor_mfma_*.hip;
 // W = 17..64 (m <= 4096): the big-network form, benor_mfma_big.hip.

@@ -786,7 +786,7 @@ void plan_geometry(KParams &p) {
       p.base_variant = p.variant;
       p.base_G = p.G;
       p.variant = 8;
-      p.lds_bytes = p.hist_bytes + kWavesPerBlock * small_wave_words(p.m) * 4u;
+      p.lds_bytes = p.hist_bytes;                   // the histogram and the parameter block only
     }
     return;
   }

@@ -20,7 +20,7 @@
 // Positions.  Lane (t, h), VGPR v (0..3), nibble n (0..7) is K position
 // beta = 4n + 3 - v of half h; slot s owns beta in [s m, s m + m) (node c of
 // the slot at s m + c).  x words (bit beta) expand to B nibbles with a shift
-// and a mask per VGPR; sign nibbles compress back with three bit-field inserts.
+// and a mask per VGPR; nibble codes compress back with shifts and masks.
 // The accumulator register j of tile T is row (j & 3) + 8 (j >> 2) + 4 h of
 // the tile (cdna_hip_programming.md section 3); packed by
 // v_cvt_scalef32_pk_fp4_f32 it becomes nibble j & 7 of VGPR 2T + (j >> 3) --
@@ -31,10 +31,10 @@
 //   R-phase: acc = A_T . Bx (A scale 2^3), Bx = +1 for x = 1, -1 for x = 0
 //     senders: 8 (c1 - c0); the fp4 conversion saturates it to the proposal
 //     +6 (p1), -6 (p0) or 0 ("?", a tie) -- node.ts:63-69.
-//   P-phase (node.ts:88-113): with Bp the proposals, |Bp| and -Bp,
-//     U = A.Bp + A.|Bp| - (12m - 6) = 12 n1 - 12m + 6 > 0  iff  n1 = m,
-//     V = A.(-Bp) + A.|Bp| - (12m - 6) = 12 n0 - 12m + 6 > 0  iff  n0 = m,
-//     W = 4 - A.|Bp| = 4 - 6 (n0 + n1) > 0  iff  every vote is "?".
+//   P-phase (node.ts:88-113): from the proposals, three 0/1 operands -- the
+//     votes that are not 1, not 0, not "?" -- counted per receiver (scale
+//     2^3, C = -0.5): the result is negative iff that count is 0, i.e. the
+//     inbox is all 1 (n1 = m), all 0 (n0 = m) or all "?" (n0 = n1 = 0).
 //   In lockstep every receiver's inbox is the whole slot (node.ts:45,171), so
 //   it is unanimous: all 1 -> every receiver decides 1 (n1 = m > F,
 //   node.ts:102-105), all 0 -> decides 0, all "?" -> every receiver flips its
@@ -42,25 +42,24 @@
 //   checked; a slot whose receivers do not all fall in one of the three cases
 //   (impossible in lockstep) is re-run by the lane path below, as is a trial
 //   that ties kSmallMaxRound times.
-// A slot that decided is counted in bin 3r + v.  A tied slot's next x plane
-// is exactly its coins of round r (every node took its coin), a pure function
-// of (seed, trial, r): it is queued, as a trial offset, on the wave's round
-// r + 1 list in LDS, and runs there with x = coin_word(r) (the continuation
-// idea of benor_mfma.h, here inside one persistent launch).  A wave takes a
-// full batch from the deepest full list first, then fresh round-1 trials, and
-// drains the partial lists at the end.
-//
-// Lane path: a trial is re-run from round 1 with the lane kernel's per-lane
-// round logic (benor_lane.h, KIND 0), one trial per lane, 64 queued trials at
-// a time (q(m)^3 of the trials: ~3 % at m = 6).
+// Slots.  Each slot holds one trial across its rounds: a slot that decided
+// is counted in bin 3r + v and takes the lane's next trial; a tied slot's next
+// x plane is exactly its coins of round r (every node took its coin), a pure
+// function of (seed, trial, r), so it simply runs round r + 1 with
+// x = coin_word(r); after a tie in round k_max the slot reads its final x (the
+// round-k_max coins) and is counted undecided.  Every slot draws one Philox
+// block per round (its initial values or its coins), the S blocks of a lane
+// computed together so that their dependency chains interleave.  A wave owns
+// a contiguous range of trials and lane l takes offsets l, l + 64, ... of it
+// whenever a slot frees up: no lists, no cross-lane traffic.  A slot whose
+// receivers are not unanimous (impossible in lockstep) re-runs its trial with
+// the lane kernel's per-lane round logic (benor_lane.h).
 #pragma once
 
 #include "benor_lane.h"
 #include "benor_mfma.h"
 
 namespace benor {
-
-constexpr uint32_t kSmallMaxRound = 3;   // rounds on the matrix cores; a later tie -> lane path
 
 // small_slots / small_wave_words: benor_internal.h
 
@@ -71,27 +70,30 @@ __device__ __forceinline__ mf_v4i small_expand(uint32_t w) {
                 (int)((w << 1) & 0x22222222u)};
 }
 
-// Sign bits (bit 3 of every nibble) of a fragment -> position bits
-// (bit 4n + 3 - v <- bit 3 of VGPR v nibble n).
-__device__ __forceinline__ uint32_t small_compress(uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3) {
-  const uint32_t t01 = (v0 & 0x88888888u) | ((v1 >> 1) & 0x44444444u);
-  const uint32_t t23 = (v2 & 0x88888888u) | ((v3 >> 1) & 0x44444444u);
+// Bit 2 of every nibble of a fragment -> position bits (bit 4n + 3 - v <- bit 2
+// of VGPR v nibble n): for the P-phase codes 0x0 (count 0) / 0x7 (count > 0).
+__device__ __forceinline__ uint32_t small_compress_b2(uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3) {
+  const uint32_t t01 = ((v0 << 1) & 0x88888888u) | (v1 & 0x44444444u);
+  const uint32_t t23 = ((v2 << 1) & 0x88888888u) | (v3 & 0x44444444u);
   return t01 | (t23 >> 2);
 }
 
 // Eight f32 results -> eight e2m1 nibbles (benor_mfma.h pack_fp4_8).
 __device__ __forceinline__ uint32_t small_pack(const mf_v16f &acc, int base) { return pack_fp4_8(acc, base); }
 
-// One trial from round 1 with the lane kernel's per-lane logic (benor_lane.h,
-// KIND 0: counts by each receiver's own v_bcnt, coins node.ts:111, k_max).
-// Returns the histogram bin; bit 31 flags an agreement violation.
+// One trial with the lane kernel's per-lane logic (benor_lane.h, KIND 0:
+// counts by each receiver's own v_bcnt, coins node.ts:111, k_max), from the
+// state after round r0: x plane x1, nobody decided (r0 = 0: /start), coin block
+// cw of round group cg (0: none).  Returns the histogram bin; bit 31 flags an
+// agreement violation.
 template <int MM>
-__device__ uint32_t small_lane_trial(uint32_t k0, uint32_t k1, uint64_t tr, uint32_t x1, uint32_t F, uint32_t k_max) {
+__device__ uint32_t small_lane_trial(uint32_t k0, uint32_t k1, uint64_t tr, uint32_t x1, uint32_t F, uint32_t k_max,
+                                     uint32_t r0, uint4 cw, uint32_t cg) {
   constexpr uint32_t live = MM == 32 ? ~0u : ((1u << MM) - 1u);
   const uint32_t tlo = (uint32_t)tr, thi = (uint32_t)(tr >> 32);
   constexpr uint32_t M = MM, hiT = M >> 1, loT = (M + 1u) >> 1;
-  uint32_t dec = 0u, r = 0u, cg = 0u;
-  uint4 cw = make_uint4(0u, 0u, 0u, 0u);
+  uint32_t dec = 0u, r = r0;
+  if (r >= k_max) return x1 == live ? 1u : (x1 == 0u ? 0u : 2u);   // undecided after k_max rounds
   for (;;) {
     ++r;
     uint32_t p0 = 0u, np1 = 0u;
@@ -104,9 +106,7 @@ __device__ uint32_t small_lane_trial(uint32_t k0, uint32_t k1, uint64_t tr, uint
     const uint32_t p1 = ~np1 & live;
     const uint32_t g1 = ((r - 1u) >> 2) + 1u;
     if (2u * (uint32_t)__builtin_popcount(x1) == M && cg != g1) {   // a tie: coins needed (node.ts:110-111)
-      uint32_t kk0 = k0, kk1 = k1;
-      asm volatile("" : "+s"(kk0), "+s"(kk1));
-      cw = coin_block(kk0, kk1, tlo, thi, 0u, r);
+      cw = coin_block<false>(k0, k1, tlo, thi, 0u, r);     // mul_lo/hi Philox on this divergent path
       cg = g1;
     }
     const uint32_t cwr = coin_word(cw, r);
@@ -132,9 +132,9 @@ __device__ uint32_t small_lane_trial(uint32_t k0, uint32_t k1, uint64_t tr, uint
 template <int MM>
 __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
   constexpr uint32_t S = small_slots(MM);
-  constexpr uint32_t BATCH = 64u * S;
   constexpr uint32_t LIVE = MM == 32 ? ~0u : ((1u << MM) - 1u);
   constexpr uint32_t USED = S * MM;                              // position bits in use per lane half
+  constexpr uint32_t EMPTY = 0xFFFFFFFFu;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -142,8 +142,6 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
   asm volatile("" : "+s"(hist_len), "+s"(trial_count));
   uint32_t *lhist = reinterpret_cast<uint32_t *>(smem);
   uint32_t *keys = reinterpret_cast<uint32_t *>(smem + p.hist_bytes - kParamBytes);
-  uint32_t *wbase = reinterpret_cast<uint32_t *>(smem + p.hist_bytes) + wv * small_wave_words(MM);
-  uint32_t *list2 = wbase, *list3 = wbase + 2u * BATCH, *lq = wbase + 4u * BATCH;   // lq: lane-path queue
   for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) lhist[i] = 0u;
   if (threadIdx.x == 0) {
     keys[0] = (uint32_t)p.seed;
@@ -156,7 +154,6 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
   const bool random_init = p.init_mode == BO_INIT_RANDOM;
   const uint32_t fixed1 = random_init ? 0u : (p.init_plane[0].z & LIVE);
   const uint32_t F = p.F, k_max = p.k_max;
-  const uint32_t R = k_max < kSmallMaxRound ? k_max : kSmallMaxRound;   // last matrix-core round
 
   // Block-diagonal A of the two tiles (see the header): lane (row rho, K half hk).
   mf_v4i A0, A1;
@@ -184,61 +181,69 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
       else A1 = a;
     }
   }
-  // Valid position bits and their -1 nibbles' base (every used position +-1).
   const uint32_t used_mask = USED == 32u ? ~0u : ((1u << USED) - 1u);
-  mf_v16f cbig, zero;
+  const mf_v4i Eu = small_expand(used_mask);
+  mf_v16f zero;                                           // the inline constant 0 as every C
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    cbig[j] = -(12.0f * (float)MM - 6.0f);
-    zero[j] = 0.0f;
-  }
-  mf_v16f four;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) four[j] = 4.0f;
+  for (int j = 0; j < 16; ++j) zero[j] = 0.0f;
+  constexpr uint32_t H = [] {                             // top bit of every slot field
+    uint32_t h = 0u;
+    for (uint32_t s = 0; s < S; ++s) h |= 1u << (s * MM + MM - 1u);
+    return h;
+  }();
+  constexpr uint32_t L = (USED == 32u ? ~0u : ((1u << USED) - 1u)) & ~H;
 
+  // This wave's trials: a contiguous range; lane l takes offsets
+  // base + l + 64 i, i = 0, 1, ..., one whenever one of its slots is free.
   const uint32_t waves_total = gridDim.x * kWavesPerBlock;
   const uint32_t wave_id = blockIdx.x * kWavesPerBlock + wv;
-  const uint32_t ngroups = (trial_count + BATCH - 1u) / BATCH;
-  uint32_t g = wave_id, len2 = 0u, len3 = 0u, lql = 0u;          // wave-uniform
-  uint32_t h0[3] = {0u, 0u, 0u}, h1[3] = {0u, 0u, 0u};             // decided 0 / 1 in round 1..3 (wave totals)
+  const uint32_t per_wave = (trial_count + waves_total - 1u) / waves_total;
+  const uint32_t wbegin = wave_id * per_wave < trial_count ? wave_id * per_wave : trial_count;
+  const uint32_t wend = wbegin + per_wave < trial_count ? wbegin + per_wave : trial_count;
+  uint32_t next = wbegin + lane;                          // this lane's next fresh trial offset
+  uint32_t toff[S], rnd[S];
+#pragma unroll
+  for (uint32_t s = 0; s < S; ++s) {
+    toff[s] = EMPTY;
+    rnd[s] = 0u;
+  }
 
   for (;;) {
-    // ---- pick the work: the deepest full list, fresh round-1 trials, then the partial lists
-    uint32_t r, n;
-    const uint32_t *src = nullptr;
-    if (R >= 3u && len3 >= BATCH) { r = 3u; n = BATCH; src = list3 + (len3 - n); len3 -= n; }
-    else if (R >= 2u && len2 >= BATCH) { r = 2u; n = BATCH; src = list2 + (len2 - n); len2 -= n; }
-    else if (g < ngroups) { r = 1u; n = trial_count - g * BATCH; n = n < BATCH ? n : BATCH; }
-    else if (len2) { r = 2u; n = len2; src = list2; len2 = 0u; }
-    else if (len3) { r = 3u; n = len3; src = list3; len3 = 0u; }
-    else break;
-    r = (uint32_t)__builtin_amdgcn_readfirstlane((int)r);
-    n = (uint32_t)__builtin_amdgcn_readfirstlane((int)n);
-
-    // ---- this lane's S trials and their x words (round 1: /start, node.ts:167-188;
-    // round r > 1: the coins of round r - 1 after a tie, node.ts:110-111)
-    uint32_t toff[S];
-    uint32_t w = 0u;
-    const uint2 kk = lds_keys(keys);
-    const uint64_t tb = lds_u64(keys + 2);
+    // ---- refill free slots from the lane's own trials (/start, node.ts:167-188)
+    bool any = false;
 #pragma unroll
     for (uint32_t s = 0; s < S; ++s) {
-      const uint32_t e = s * 64u + lane;
-      const bool valid = e < n;
-      toff[s] = valid ? (src ? src[e] : g * BATCH + e) : 0xFFFFFFFFu;
-      uint32_t x = 0u;
-      if (valid) {
-        const uint64_t tr = tb + toff[s];
-        if (r == 1u) {
-          x = random_init ? philox4x32_10(kk.x, kk.y, make_uint4((uint32_t)tr, (uint32_t)(tr >> 32), 0u, kStreamInit << 24)).x
-                          : fixed1;
-        } else {
-          x = coin_word(coin_block(kk.x, kk.y, (uint32_t)tr, (uint32_t)(tr >> 32), 0u, r - 1u), r - 1u);
-        }
-      }
-      w |= (x & LIVE) << (s * MM);
+      const bool take = toff[s] == EMPTY && next < wend;
+      toff[s] = take ? next : toff[s];
+      rnd[s] = take ? 1u : rnd[s];
+      next += take ? 64u : 0u;
+      any |= toff[s] != EMPTY;
     }
-    if (r == 1u) g += waves_total;
+    if (!__any(any)) break;
+
+    // ---- x words: round 1 the initial values, round r > 1 the coins of round
+    // r - 1 after a tie (node.ts:110-111); a slot past k_max reads the coins of
+    // round k_max, its final x.  One Philox block per slot, the S chains advanced
+    // together (philox4x32_10_multi).
+    const uint2 kk = lds_keys(keys);
+    const uint64_t tb = lds_u64(keys + 2);
+    uint4 blk[S];
+#pragma unroll
+    for (uint32_t s = 0; s < S; ++s) {
+      const uint64_t tr = tb + (toff[s] == EMPTY ? 0u : toff[s]);
+      const uint32_t c3 = rnd[s] <= 1u ? (kStreamInit << 24) : (((rnd[s] - 2u) >> 2) | (kStreamCoin << 24));
+      blk[s] = make_uint4((uint32_t)tr, (uint32_t)(tr >> 32), 0u, c3);
+    }
+    philox4x32_10_multi<S>(kk.x, kk.y, blk);
+    uint32_t xs[S];
+    uint32_t w = 0u;
+#pragma unroll
+    for (uint32_t s = 0; s < S; ++s) {
+      const uint32_t ws = (rnd[s] - 2u) & 3u;
+      const uint32_t coin = ws == 0u ? blk[s].x : ws == 1u ? blk[s].y : ws == 2u ? blk[s].z : blk[s].w;
+      xs[s] = (rnd[s] <= 1u ? (random_init ? blk[s].x : fixed1) : coin) & LIVE;
+      w |= (toff[s] == EMPTY ? 0u : xs[s]) << (s * MM);
+    }
     // B: +1.0 (0x2) where x = 1, -1.0 (0xA) where x = 0, 0 on unused positions
     const mf_v4i Ez = small_expand(used_mask & ~w);
     const mf_v4i Ex = small_expand(w);
@@ -253,106 +258,73 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
       const mf_v16f r1 = mfma_count<3>(A1, bx, zero);
       bp = mf_v4i{(int)small_pack(r0, 0), (int)small_pack(r0, 8), (int)small_pack(r1, 0), (int)small_pack(r1, 8)};
     }
-    mf_v4i babs, bneg, bnabs;
+    // P-phase operands: 1.0 on the used positions whose vote is NOT 1 / NOT 0 /
+    // NOT "?" (proposal nibbles: +6 = 0111, -6 = 1111, "?" = 0000).
+    mf_v4i bn1, bn0, bnq;
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-      babs[v] = bp[v] & 0x77777777;                   // |proposal|: 6 unless "?"
-      bneg[v] = bp[v] ^ (int)0x88888888u;             // -proposal
-      bnabs[v] = bp[v] | (int)0x88888888u;            // -|proposal|
+      const uint32_t b = (uint32_t)bp[v], b2 = b >> 2;    // bit 1 of a nibble <- its sign bit
+      bn1[v] = (int)((b2 | ~b) & (uint32_t)Eu[v]);        // p0 or "?": sign set or bit 1 clear
+      bn0[v] = (int)(~b2 & (uint32_t)Eu[v]);              // p1 or "?": sign clear
+      bnq[v] = (int)(b & 0x22222222u);                    // p0 or p1: bit 1 set
     }
-    // ---- P-phase per tile: U (all 1), V (all 0), W (all "?") sign nibbles
+    // ---- P-phase per tile: a receiver row counts the votes of its slot that
+    // are not 1 (n0 + n?), not 0 (n1 + n?), not "?" (n0 + n1), scaled by 2^3:
+    // the packed code is 0 exactly when the count is 0 (else >= 8 saturates
+    // to 6.0 = 0111), i.e. the receiver's inbox is all 1 / all 0 / all "?"
+    // (node.ts:92-98).
     uint32_t un[4], vn[4], wn[4];
 #pragma unroll
     for (int T = 0; T < 2; ++T) {
       const mf_v4i A = T == 0 ? A0 : A1;
-      const mf_v16f tp = mfma_count(A, babs, cbig);   // 6 (n0 + n1) - (12m - 6)
-      const mf_v16f u = mfma_count(A, bp, tp);        // 12 n1 - 12m + 6
-      const mf_v16f vv = mfma_count(A, bneg, tp);     // 12 n0 - 12m + 6
-      const mf_v16f ww = mfma_count(A, bnabs, four);  // 4 - 6 (n0 + n1)
+      const mf_v16f u = mfma_count<3>(A, bn1, zero);
       un[2 * T] = small_pack(u, 0);
       un[2 * T + 1] = small_pack(u, 8);
+      const mf_v16f vv = mfma_count<3>(A, bn0, zero);
       vn[2 * T] = small_pack(vv, 0);
       vn[2 * T + 1] = small_pack(vv, 8);
+      const mf_v16f ww = mfma_count<3>(A, bnq, zero);
       wn[2 * T] = small_pack(ww, 0);
       wn[2 * T + 1] = small_pack(ww, 8);
-      __builtin_amdgcn_sched_barrier(0);
     }
-    // position bits: set where NOT all 1 / NOT all 0 / NOT all "?"
-    const uint32_t wu = small_compress(un[0], un[1], un[2], un[3]);
-    const uint32_t wvv = small_compress(vn[0], vn[1], vn[2], vn[3]);
-    const uint32_t ww = small_compress(wn[0], wn[1], wn[2], wn[3]);
+    // position bits: set where the inbox is NOT all 1 / NOT all 0 / NOT all "?";
+    // then per slot field: its top bit after (((x & L) + L) | x) & H says "some
+    // receiver of the slot is not"
+    const uint32_t wu = small_compress_b2(un[0], un[1], un[2], un[3]);
+    const uint32_t wvv = small_compress_b2(vn[0], vn[1], vn[2], vn[3]);
+    const uint32_t ww = small_compress_b2(wn[0], wn[1], wn[2], wn[3]);
+    const uint32_t d1 = ~((((wu & L) + L) | wu) & H);     // every receiver decided 1 (node.ts:102-105)
+    const uint32_t d0 = ~((((wvv & L) + L) | wvv) & H);   // every receiver decided 0 (node.ts:99-101)
+    const uint32_t tq = ~((((ww & L) + L) | ww) & H);     // every receiver flipped its coin (node.ts:110-111)
 
-    // ---- per slot: decided (bins 3r + v), tied (next round's list), else the lane path
-    const bool last = r >= R;
-    uint32_t *next = r == 1u ? list2 : list3;
-    uint32_t c1 = 0u, c0 = 0u;
+    // ---- per slot: halted (bin 3r + v; node.ts:116-145 auto-stop), tied (next
+    // round, x = these coins), past k_max (undecided: bin v of its final x)
 #pragma unroll
     for (uint32_t s = 0; s < S; ++s) {
-      const uint32_t fm = LIVE << (s * MM);
-      const bool valid = toff[s] != 0xFFFFFFFFu;
-      const bool all1 = (wu & fm) == 0u, all0 = (wvv & fm) == 0u, tie = (ww & fm) == 0u;
-      c1 += (valid && all1) ? 1u : 0u;
-      c0 += (valid && all0) ? 1u : 0u;
-      const bool to_next = valid && tie && !last && !all1 && !all0;
-      const bool to_lane = valid && !all1 && !all0 && !to_next;
-      const uint64_t bn = ballot(to_next), bl = ballot(to_lane);
-      if (to_next) {
-        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bn >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bn, 0u));
-        next[(r == 1u ? len2 : len3) + rank] = toff[s];
+      const uint32_t top = s * MM + MM - 1u;
+      const bool act = toff[s] != EMPTY;
+      const bool fin = act && rnd[s] > k_max;
+      const bool h1 = act && !fin && ((d1 >> top) & 1u), h0 = act && !fin && ((d0 >> top) & 1u);
+      const bool tie = act && !fin && !h1 && !h0 && ((tq >> top) & 1u);
+      const bool odd = act && !fin && !h1 && !h0 && !tie;   // receivers not unanimous: impossible in lockstep
+      if (fin || h1 || h0) {
+        const uint32_t v = xs[s] == LIVE ? 1u : (xs[s] == 0u ? 0u : 2u);
+        atomicAdd(&lhist[fin ? v : 3u * rnd[s] + (h1 ? 1u : 0u)], 1u);
       }
-      if (to_lane) {
-        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0u));
-        lq[lql + rank] = toff[s];
+      if (odd) {                                          // re-run it with the lane kernel's logic
+        const uint2 k2 = lds_keys(keys);
+        const uint64_t tr = lds_u64(keys + 2) + toff[s];
+        uint32_t x = fixed1;
+        if (random_init)
+          x = philox4x32_10<false>(k2.x, k2.y, make_uint4((uint32_t)tr, (uint32_t)(tr >> 32), 0u, kStreamInit << 24)).x &
+              LIVE;
+        const uint32_t bin = small_lane_trial<MM>(k2.x, k2.y, tr, x, F, k_max, 0u, make_uint4(0u, 0u, 0u, 0u), 0u);
+        atomicAdd(&lhist[bin & 0x7FFFFFFFu], 1u);
+        if (bin >> 31) atomicAdd(&lhist[hist_len - 1u], 1u);
       }
-      if (r == 1u) len2 += (uint32_t)__builtin_popcountll(bn);
-      else len3 += (uint32_t)__builtin_popcountll(bn);
-      lql += (uint32_t)__builtin_popcountll(bl);
+      rnd[s] += tie ? 1u : 0u;
+      toff[s] = (fin || h1 || h0 || odd) ? EMPTY : toff[s];
     }
-    // wave totals of the decided counts: bit-sliced ballots (c <= S <= 8)
-    uint32_t t1 = 0u, t0 = 0u;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      t1 += (uint32_t)__builtin_popcountll(ballot((c1 >> b) & 1u)) << b;
-      t0 += (uint32_t)__builtin_popcountll(ballot((c0 >> b) & 1u)) << b;
-    }
-    if (r == 1u) { h1[0] += t1; h0[0] += t0; }
-    else if (r == 2u) { h1[1] += t1; h0[1] += t0; }
-    else { h1[2] += t1; h0[2] += t0; }
-
-    // ---- lane path, 64 queued trials at a time (every lane busy)
-    while (lql >= 64u) {
-      lql -= 64u;
-      const uint32_t t = lq[lql + lane];
-      const uint64_t tr = lds_u64(keys + 2) + t;
-      const uint2 k2 = lds_keys(keys);
-      uint32_t x = fixed1;
-      if (random_init) x = philox4x32_10(k2.x, k2.y, make_uint4((uint32_t)tr, (uint32_t)(tr >> 32), 0u, kStreamInit << 24)).x & LIVE;
-      const uint32_t bin = small_lane_trial<MM>(k2.x, k2.y, tr, x, F, k_max);
-      atomicAdd(&lhist[bin & 0x7FFFFFFFu], 1u);
-      if (bin >> 31) atomicAdd(&lhist[hist_len - 1u], 1u);
-    }
-  }
-  // ---- the rest of the lane-path queue
-  if (lane < lql) {
-    const uint32_t t = lq[lane];
-    const uint64_t tr = lds_u64(keys + 2) + t;
-    const uint2 k2 = lds_keys(keys);
-    uint32_t x = fixed1;
-    if (random_init) x = philox4x32_10(k2.x, k2.y, make_uint4((uint32_t)tr, (uint32_t)(tr >> 32), 0u, kStreamInit << 24)).x & LIVE;
-    const uint32_t bin = small_lane_trial<MM>(k2.x, k2.y, tr, x, F, k_max);
-    atomicAdd(&lhist[bin & 0x7FFFFFFFu], 1u);
-    if (bin >> 31) atomicAdd(&lhist[hist_len - 1u], 1u);
-  }
-  // outcome bins 3r + v of the matrix-core rounds (lane l < 9 adds one of them)
-  {
-    const uint32_t rr = lane / 2u + 1u;
-    uint32_t c = 0u;
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      if (lane == 2u * q) c = h0[q];
-      if (lane == 2u * q + 1u) c = h1[q];
-    }
-    if (lane < 6u && c) atomicAdd(&lhist[3u * rr + (lane & 1u)], c);
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) {
