@@ -933,6 +933,16 @@ uint32_t block_waves(const KParams &p) {
   return (p.variant == 7 && p.W > 16u && !p.node_out && !p.rounds_out) ? mfma_big_block_waves(p) : (uint32_t)kWavesPerBlock;
 }
 
+// Two refills' worth (64 S trials each) per chunk: a wave asks the counter
+// about once per two iterations.  BENOR_SMALL_CHUNK=<refills> overrides
+// (0: every wave runs one contiguous share, no counter).
+uint32_t small_chunk_trials(const KParams &p) {
+  uint32_t refills = 2u;
+  if (const char *ev = getenv("BENOR_SMALL_CHUNK")) refills = (uint32_t)strtoul(ev, nullptr, 10);
+  if (refills > 64u) refills = 64u;
+  return refills * 64u * small_slots(p.m);
+}
+
 int lockstep_grid(const KParams &p, int device) {
   int cus = 256;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
@@ -950,15 +960,15 @@ int lockstep_grid(const KParams &p, int device) {
       q.lds_bytes = q.hist_bytes + kWavesPerBlock * q.wave_bytes;
       return lockstep_grid(q, device);
     }
-    // Packed matrix-core kernel: a wave runs 64 * S trials per iteration and
-    // drains its round-2/3 lists and lane-path queue at the end, so each wave
-    // takes ~3 batches of fresh trials (fewer, longer-lived waves amortise the
-    // drain), at most what LDS admits per CU and 2 workgroups per CU.
+    // Packed matrix-core kernel: a wave owns a contiguous range of trials and
+    // runs 64 * S slots per iteration until its last trial halts, so each wave
+    // takes ~3 iterations' worth of fresh trials (its lanes' tails average
+    // out), at most 2 workgroups per CU.
     const uint64_t batch = 64u * small_slots(p.m);
     const uint64_t groups = (p.trial_count + batch - 1u) / batch;
     uint64_t per_cu = groups / ((uint64_t)cus * kWavesPerBlock * 3u);
     uint64_t cap = lds_groups_per_cu(p.lds_bytes);
-    if (cap > 2u) cap = 2u;
+    if (cap > 4u) cap = 4u;
     if (per_cu > cap) per_cu = cap;
     if (per_cu < 1u) per_cu = 1u;
     if (const char *ev = getenv("BENOR_BLOCKS_PER_CU")) {   // tuning knob

@@ -40,8 +40,7 @@
 //   node.ts:102-105), all 0 -> decides 0, all "?" -> every receiver flips its
 //   coin (node.ts:110-111) and nobody decides.  Each receiver's sign bits are
 //   checked; a slot whose receivers do not all fall in one of the three cases
-//   (impossible in lockstep) is re-run by the lane path below, as is a trial
-//   that ties kSmallMaxRound times.
+//   (impossible in lockstep) is re-run with the lane kernel's logic.
 // Slots.  Each slot holds one trial across its rounds: a slot that decided
 // is counted in bin 3r + v and takes the lane's next trial; a tied slot's next
 // x plane is exactly its coins of round r (every node took its coin), a pure
@@ -61,7 +60,7 @@
 
 namespace benor {
 
-// small_slots / small_wave_words: benor_internal.h
+// small_slots: benor_internal.h
 
 // 32 position bits -> B fragment, e2m1 1.0 (0b0010) where the bit is set:
 // VGPR v nibble n <- bit 4n + 3 - v.
@@ -70,12 +69,28 @@ __device__ __forceinline__ mf_v4i small_expand(uint32_t w) {
                 (int)((w << 1) & 0x22222222u)};
 }
 
-// Bit 2 of every nibble of a fragment -> position bits (bit 4n + 3 - v <- bit 2
-// of VGPR v nibble n): for the P-phase codes 0x0 (count 0) / 0x7 (count > 0).
-__device__ __forceinline__ uint32_t small_compress_b2(uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3) {
-  const uint32_t t01 = ((v0 << 1) & 0x88888888u) | (v1 & 0x44444444u);
-  const uint32_t t23 = ((v2 << 1) & 0x88888888u) | (v3 & 0x44444444u);
-  return t01 | (t23 >> 2);
+// (a & m) | (b & ~m) as one v_bfi_b32.  The asm keeps LLVM from turning a
+// 0 / ~0 mask back into a select (v_cndmask_b32 with a VCC or SGPR operand,
+// ~24 cycles per wave instruction on gfx950: profiles/r03-v7_valu_probe.txt).
+__device__ __forceinline__ uint32_t bsel(uint32_t m, uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+  return r;
+}
+
+// ORs the f32 bits of tile T's accumulator rows into their slots' words:
+// register j is receiver position 4 (j & 7) + 3 - (2T + (j >> 3)) (the
+// position its packed nibble would take), slot position / MM.
+template <int MM>
+__device__ __forceinline__ void small_or_rows(const mf_v16f &acc, int T, uint32_t (&o)[small_slots(MM)]) {
+  constexpr uint32_t USED = small_slots(MM) * MM;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const uint32_t beta = 4u * (uint32_t)(j & 7) + 3u - (2u * (uint32_t)T + (uint32_t)(j >> 3));
+    if (beta < USED) o[beta / MM] |= __float_as_uint(acc[j]);
+  }
+#pragma unroll
+  for (uint32_t s = 0; s < small_slots(MM); ++s) asm volatile("" : "+v"(o[s]));   // reduce now, free acc
 }
 
 // Eight f32 results -> eight e2m1 nibbles (benor_mfma.h pack_fp4_8).
@@ -129,6 +144,33 @@ __device__ uint32_t small_lane_trial(uint32_t k0, uint32_t k1, uint64_t tr, uint
   }
 }
 
+// Adds one lane's packed halt counters (8-bit fields: rounds 1-4) into the
+// LDS histogram (bins 3r + v) and clears them.
+__device__ __forceinline__ void small_flush_counts(uint32_t *lhist, uint32_t &cnt0, uint32_t &cnt1) {
+#pragma unroll
+  for (uint32_t f = 0; f < 4; ++f) {
+    const uint32_t a0 = (cnt0 >> (8u * f)) & 255u, a1 = (cnt1 >> (8u * f)) & 255u;
+    if (a0) atomicAdd(&lhist[3u * (f + 1u)], a0);
+    if (a1) atomicAdd(&lhist[3u * (f + 1u) + 1u], a1);
+  }
+  cnt0 = cnt1 = 0u;
+}
+
+// BENOR_SMALL_TIMING (tools/small_phase_probe.hip only): lane 0 of every wave
+// adds the shader-clock cycles of each phase to p.rounds_out[0..7].
+#ifdef BENOR_SMALL_TIMING
+#define SMALL_T(i)                                                         \
+  do {                                                                     \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();                      \
+    tph[i] += t_ - tlast;                                                  \
+    tlast = t_;                                                            \
+  } while (0)
+#else
+#define SMALL_T(i) \
+  do {             \
+  } while (0)
+#endif
+
 template <int MM>
 __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
   constexpr uint32_t S = small_slots(MM);
@@ -153,6 +195,7 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
 
   const bool random_init = p.init_mode == BO_INIT_RANDOM;
   const uint32_t fixed1 = random_init ? 0u : (p.init_plane[0].z & LIVE);
+  const uint32_t rmask = random_init ? ~0u : 0u;         // round-1 x: the Philox word, or the fixed plane
   const uint32_t F = p.F, k_max = p.k_max;
 
   // Block-diagonal A of the two tiles (see the header): lane (row rho, K half hk).
@@ -186,40 +229,82 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
   mf_v16f zero;                                           // the inline constant 0 as every C
 #pragma unroll
   for (int j = 0; j < 16; ++j) zero[j] = 0.0f;
-  constexpr uint32_t H = [] {                             // top bit of every slot field
-    uint32_t h = 0u;
-    for (uint32_t s = 0; s < S; ++s) h |= 1u << (s * MM + MM - 1u);
-    return h;
-  }();
-  constexpr uint32_t L = (USED == 32u ? ~0u : ((1u << USED) - 1u)) & ~H;
 
-  // This wave's trials: a contiguous range; lane l takes offsets
-  // base + l + 64 i, i = 0, 1, ..., one whenever one of its slots is free.
+  // Trials reach the lanes through a wave pool [pool, pend): at every refill
+  // the lanes with a free slot take the next pool offsets in lane order
+  // (ballot + mbcnt), so a wave's lanes drain one shared pool and none sits
+  // idle while another still has trials.  With p.work the pool is a chunk of
+  // work_chunk trials taken from the launch-wide counter, the next chunk's
+  // ticket requested one chunk ahead; without it, the wave's share of the launch.
   const uint32_t waves_total = gridDim.x * kWavesPerBlock;
   const uint32_t wave_id = blockIdx.x * kWavesPerBlock + wv;
-  const uint32_t per_wave = (trial_count + waves_total - 1u) / waves_total;
-  const uint32_t wbegin = wave_id * per_wave < trial_count ? wave_id * per_wave : trial_count;
-  const uint32_t wend = wbegin + per_wave < trial_count ? wbegin + per_wave : trial_count;
-  uint32_t next = wbegin + lane;                          // this lane's next fresh trial offset
+  const bool dyn = p.work != nullptr;
+  uint32_t pool, pend, nxt_v = 0u;
+  bool drained;                                           // no chunk left to take
+  if (dyn) {
+    uint32_t chunk = p.work_chunk;
+    asm volatile("" : "+s"(chunk));
+    uint32_t t0 = 0u;
+    if (lane == 0u) t0 = atomicAdd(p.work, chunk);
+    if (lane == 0u) nxt_v = atomicAdd(p.work, chunk);
+    pool = (uint32_t)__builtin_amdgcn_readfirstlane((int)t0);
+    drained = pool >= trial_count;
+    pend = drained ? pool : (pool + chunk < trial_count ? pool + chunk : trial_count);
+  } else {
+    const uint32_t per_wave = (trial_count + waves_total - 1u) / waves_total;
+    pool = wave_id * per_wave < trial_count ? wave_id * per_wave : trial_count;
+    pend = pool + per_wave < trial_count ? pool + per_wave : trial_count;
+    drained = true;
+  }
   uint32_t toff[S], rnd[S];
 #pragma unroll
   for (uint32_t s = 0; s < S; ++s) {
     toff[s] = EMPTY;
     rnd[s] = 0u;
   }
+  uint32_t cnt0 = 0u, cnt1 = 0u, since_flush = 0u;        // packed halts of rounds 1-4, v = 0 / 1
+#ifdef BENOR_SMALL_TIMING
+  uint64_t tph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast = __builtin_amdgcn_s_memtime();
+  const uint64_t tstart = tlast;
+  uint32_t iters = 0;
+#endif
 
   for (;;) {
-    // ---- refill free slots from the lane's own trials (/start, node.ts:167-188)
-    bool any = false;
+    // ---- refill free slots from the pool (/start, node.ts:167-188).
+    // Selects are bit masks (v_bfi), not v_cndmask: on gfx950 a VCC-operand
+    // v_cndmask_b32 issues at ~24 cycles per wave instruction
+    // (profiles/r03-v7_valu_probe.txt).  Offsets are < 2^31: EMPTY's bit 31 tags it.
+    uint32_t any = 0u;
 #pragma unroll
     for (uint32_t s = 0; s < S; ++s) {
-      const bool take = toff[s] == EMPTY && next < wend;
-      toff[s] = take ? next : toff[s];
-      rnd[s] = take ? 1u : rnd[s];
-      next += take ? 64u : 0u;
-      any |= toff[s] != EMPTY;
+      const uint32_t fr = toff[s] >> 31;                  // free slot
+      const uint64_t bal = __ballot(fr != 0u);
+      const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+      const uint32_t avail = pend - pool;
+      const uint32_t tm = 0u - (fr & ((rank - avail) >> 31));
+      toff[s] = bsel(tm, pool + rank, toff[s]);
+      rnd[s] = bsel(tm, 1u, rnd[s]);
+      any |= ~toff[s];
+      const uint32_t k = (uint32_t)__popcll(bal);
+      pool += k < avail ? k : avail;
+      if (pool == pend && !drained) {                     // next chunk (its ticket is back by now)
+        const uint32_t nb = (uint32_t)__builtin_amdgcn_readfirstlane((int)nxt_v);
+        uint32_t chunk = p.work_chunk;
+        asm volatile("" : "+s"(chunk));
+        if (nb >= trial_count) {
+          drained = true;
+        } else {
+          pool = nb;
+          pend = nb + chunk < trial_count ? nb + chunk : trial_count;
+          if (lane == 0u) nxt_v = atomicAdd(p.work, chunk);
+        }
+      }
     }
-    if (!__any(any)) break;
+    if (!__any((any >> 31) != 0u)) break;                 // every slot free and the pool drained
+#ifdef BENOR_SMALL_TIMING
+    ++iters;
+#endif
+    SMALL_T(0);
 
     // ---- x words: round 1 the initial values, round r > 1 the coins of round
     // r - 1 after a tie (node.ts:110-111); a slot past k_max reads the coins of
@@ -228,21 +313,29 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
     const uint2 kk = lds_keys(keys);
     const uint64_t tb = lds_u64(keys + 2);
     uint4 blk[S];
+    uint32_t fmask[S];                                    // all ones where the slot runs round 1
 #pragma unroll
     for (uint32_t s = 0; s < S; ++s) {
-      const uint64_t tr = tb + (toff[s] == EMPTY ? 0u : toff[s]);
-      const uint32_t c3 = rnd[s] <= 1u ? (kStreamInit << 24) : (((rnd[s] - 2u) >> 2) | (kStreamCoin << 24));
+      const uint64_t tr = tb + (toff[s] & 0x7FFFFFFFu);
+      fmask[s] = 0u - ((rnd[s] - 2u) >> 31);
+      const uint32_t c3 = bsel(fmask[s], kStreamInit << 24, ((rnd[s] - 2u) >> 2) | (kStreamCoin << 24));
       blk[s] = make_uint4((uint32_t)tr, (uint32_t)(tr >> 32), 0u, c3);
     }
     philox4x32_10_multi<S>(kk.x, kk.y, blk);
+    SMALL_T(1);
     uint32_t xs[S];
     uint32_t w = 0u;
 #pragma unroll
     for (uint32_t s = 0; s < S; ++s) {
-      const uint32_t ws = (rnd[s] - 2u) & 3u;
-      const uint32_t coin = ws == 0u ? blk[s].x : ws == 1u ? blk[s].y : ws == 2u ? blk[s].z : blk[s].w;
-      xs[s] = (rnd[s] <= 1u ? (random_init ? blk[s].x : fixed1) : coin) & LIVE;
-      w |= (toff[s] == EMPTY ? 0u : xs[s]) << (s * MM);
+      const uint32_t ws = rnd[s] - 2u;                    // coin word (r - 2) & 3 of the block
+      const uint32_t m0 = (uint32_t)__builtin_amdgcn_sbfe((int)ws, 0, 1), m1 = (uint32_t)__builtin_amdgcn_sbfe((int)ws, 1, 1);
+      const uint32_t lo = bsel(m0, blk[s].y, blk[s].x), hi = bsel(m0, blk[s].w, blk[s].z);
+      const uint32_t coin = bsel(m1, hi, lo);
+      const uint32_t init = bsel(rmask, blk[s].x, fixed1);
+      xs[s] = bsel(fmask[s], init, coin) & LIVE;
+      uint32_t keep = (toff[s] >> 31) - 1u;               // ~0 unless the slot is EMPTY
+      asm("" : "+v"(keep));                               // a mask, not a select
+      w |= (xs[s] & keep) << (s * MM);
     }
     // B: +1.0 (0x2) where x = 1, -1.0 (0xA) where x = 0, 0 on unused positions
     const mf_v4i Ez = small_expand(used_mask & ~w);
@@ -258,6 +351,7 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
       const mf_v16f r1 = mfma_count<3>(A1, bx, zero);
       bp = mf_v4i{(int)small_pack(r0, 0), (int)small_pack(r0, 8), (int)small_pack(r1, 0), (int)small_pack(r1, 8)};
     }
+    SMALL_T(2);
     // P-phase operands: 1.0 on the used positions whose vote is NOT 1 / NOT 0 /
     // NOT "?" (proposal nibbles: +6 = 0111, -6 = 1111, "?" = 0000).
     mf_v4i bn1, bn0, bnq;
@@ -269,47 +363,49 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
       bnq[v] = (int)(b & 0x22222222u);                    // p0 or p1: bit 1 set
     }
     // ---- P-phase per tile: a receiver row counts the votes of its slot that
-    // are not 1 (n0 + n?), not 0 (n1 + n?), not "?" (n0 + n1), scaled by 2^3:
-    // the packed code is 0 exactly when the count is 0 (else >= 8 saturates
-    // to 6.0 = 0111), i.e. the receiver's inbox is all 1 / all 0 / all "?"
-    // (node.ts:92-98).
-    uint32_t un[4], vn[4], wn[4];
+    // are not 1 (n0 + n?), not 0 (n1 + n?), not "?" (n0 + n1).  A count is
+    // >= 0, so its f32 is +0.0 exactly when the receiver's inbox is all 1 /
+    // all 0 / all "?" (node.ts:92-98), and the OR of the f32 bits of a slot's
+    // rows is 0 iff every receiver of the slot saw that.
+    uint32_t o1[S], o0[S], oq[S];                         // nonzero: some receiver's count is not 0
+#pragma unroll
+    for (uint32_t s = 0; s < S; ++s) o1[s] = o0[s] = oq[s] = 0u;
 #pragma unroll
     for (int T = 0; T < 2; ++T) {
       const mf_v4i A = T == 0 ? A0 : A1;
-      const mf_v16f u = mfma_count<3>(A, bn1, zero);
-      un[2 * T] = small_pack(u, 0);
-      un[2 * T + 1] = small_pack(u, 8);
-      const mf_v16f vv = mfma_count<3>(A, bn0, zero);
-      vn[2 * T] = small_pack(vv, 0);
-      vn[2 * T + 1] = small_pack(vv, 8);
-      const mf_v16f ww = mfma_count<3>(A, bnq, zero);
-      wn[2 * T] = small_pack(ww, 0);
-      wn[2 * T + 1] = small_pack(ww, 8);
+      // one product live at a time (the scheduler would otherwise issue all six first)
+      small_or_rows<MM>(mfma_count<3>(A, bn1, zero), T, o1);
+      __builtin_amdgcn_sched_barrier(0);
+      small_or_rows<MM>(mfma_count<3>(A, bn0, zero), T, o0);
+      __builtin_amdgcn_sched_barrier(0);
+      small_or_rows<MM>(mfma_count<3>(A, bnq, zero), T, oq);
+      __builtin_amdgcn_sched_barrier(0);
     }
-    // position bits: set where the inbox is NOT all 1 / NOT all 0 / NOT all "?";
-    // then per slot field: its top bit after (((x & L) + L) | x) & H says "some
-    // receiver of the slot is not"
-    const uint32_t wu = small_compress_b2(un[0], un[1], un[2], un[3]);
-    const uint32_t wvv = small_compress_b2(vn[0], vn[1], vn[2], vn[3]);
-    const uint32_t ww = small_compress_b2(wn[0], wn[1], wn[2], wn[3]);
-    const uint32_t d1 = ~((((wu & L) + L) | wu) & H);     // every receiver decided 1 (node.ts:102-105)
-    const uint32_t d0 = ~((((wvv & L) + L) | wvv) & H);   // every receiver decided 0 (node.ts:99-101)
-    const uint32_t tq = ~((((ww & L) + L) | ww) & H);     // every receiver flipped its coin (node.ts:110-111)
+    SMALL_T(3);
 
     // ---- per slot: halted (bin 3r + v; node.ts:116-145 auto-stop), tied (next
-    // round, x = these coins), past k_max (undecided: bin v of its final x)
+    // round, x = these coins), past k_max (undecided: bin v of its final x).
+    // Halts of rounds 1-4 go to two packed per-lane counters (8-bit fields,
+    // flushed every 31 iterations); later rounds and k_max to LDS atomics.
 #pragma unroll
     for (uint32_t s = 0; s < S; ++s) {
-      const uint32_t top = s * MM + MM - 1u;
-      const bool act = toff[s] != EMPTY;
-      const bool fin = act && rnd[s] > k_max;
-      const bool h1 = act && !fin && ((d1 >> top) & 1u), h0 = act && !fin && ((d0 >> top) & 1u);
-      const bool tie = act && !fin && !h1 && !h0 && ((tq >> top) & 1u);
-      const bool odd = act && !fin && !h1 && !h0 && !tie;   // receivers not unanimous: impossible in lockstep
-      if (fin || h1 || h0) {
+      const uint32_t act = (toff[s] >> 31) ^ 1u;
+      const uint32_t fin = act & ((k_max - rnd[s]) >> 31);
+      const uint32_t run = act & (fin ^ 1u);
+      // every receiver decided 1 (node.ts:102-105) / decided 0 (node.ts:99-101) /
+      // flipped its coin (node.ts:110-111): the slot's row OR is 0
+      // (the ORs are < 2^31: 0 - o has bit 31 set iff o != 0)
+      const uint32_t n1 = (0u - o1[s]) >> 31, n0 = (0u - o0[s]) >> 31, nq = (0u - oq[s]) >> 31;
+      const uint32_t h1 = run & (n1 ^ 1u), h0 = run & n1 & (n0 ^ 1u);
+      const uint32_t tie = run & n1 & n0 & (nq ^ 1u);
+      const uint32_t odd = run & n1 & n0 & nq;            // receivers not unanimous: impossible in lockstep
+      const uint32_t early = (rnd[s] - 5u) >> 31;          // round <= 4
+      const uint32_t sh = ((rnd[s] - 1u) & 3u) << 3;
+      cnt1 += (h1 & early) << sh;
+      cnt0 += (h0 & early) << sh;
+      if ((((h1 | h0) & (early ^ 1u)) | fin) != 0u) {
         const uint32_t v = xs[s] == LIVE ? 1u : (xs[s] == 0u ? 0u : 2u);
-        atomicAdd(&lhist[fin ? v : 3u * rnd[s] + (h1 ? 1u : 0u)], 1u);
+        atomicAdd(&lhist[fin ? v : 3u * rnd[s] + h1], 1u);
       }
       if (odd) {                                          // re-run it with the lane kernel's logic
         const uint2 k2 = lds_keys(keys);
@@ -322,8 +418,36 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
         atomicAdd(&lhist[bin & 0x7FFFFFFFu], 1u);
         if (bin >> 31) atomicAdd(&lhist[hist_len - 1u], 1u);
       }
-      rnd[s] += tie ? 1u : 0u;
-      toff[s] = (fin || h1 || h0 || odd) ? EMPTY : toff[s];
+      rnd[s] += tie;
+      toff[s] |= 0u - (h1 | h0 | fin | odd);             // -> EMPTY
+    }
+    if (++since_flush == 31u) {
+      small_flush_counts(lhist, cnt0, cnt1);
+      since_flush = 0u;
+    }
+    SMALL_T(4);
+  }
+  small_flush_counts(lhist, cnt0, cnt1);
+#ifdef BENOR_SMALL_TIMING
+  if (lane == 0) {
+    unsigned long long *o = reinterpret_cast<unsigned long long *>(p.rounds_out);
+    for (int i = 0; i < 5; ++i) atomicAdd(&o[i], (unsigned long long)tph[i]);
+    atomicAdd(&o[6], (unsigned long long)iters);
+    atomicAdd(&o[7], 1ull);
+    o[8 + 3 * wave_id] = tstart;                          // per wave: start, end, iterations
+    o[9 + 3 * wave_id] = __builtin_amdgcn_s_memtime();
+    o[10 + 3 * wave_id] = iters;
+  }
+#endif
+  if (dyn) {                                              // the last wave out resets the counter
+    const uint32_t last = (uint32_t)__builtin_amdgcn_readfirstlane((int)nxt_v);   // its prefetch is back
+    asm volatile("" ::"s"(last));
+  }
+  if (dyn && lane == 0u) {
+    __threadfence();
+    if (atomicAdd(p.work + 1, 1u) == waves_total - 1u) {
+      atomicExch(p.work, 0u);
+      atomicExch(p.work + 1, 0u);
     }
   }
   __syncthreads();

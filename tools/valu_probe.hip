@@ -6,7 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 
-template <int OP>
+template <int OP, int CH = 8>
 __global__ void __launch_bounds__(256) probe(unsigned *sink, int iters, unsigned seed) {
   unsigned a[8];
   unsigned long long c[8];
@@ -19,7 +19,7 @@ __global__ void __launch_bounds__(256) probe(unsigned *sink, int iters, unsigned
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
+      for (int i = 0; i < CH; ++i) {
         if (OP == 0) asm volatile("v_bcnt_u32_b32 %0, %1, %0" : "+v"(a[i]) : "v"(x));
         if (OP == 1) asm volatile("v_add_u32 %0, %1, %0" : "+v"(a[i]) : "v"(x));
         if (OP == 2) asm volatile("v_and_b32 %0, %1, %0" : "+v"(a[i]) : "v"(x));
@@ -39,6 +39,15 @@ __global__ void __launch_bounds__(256) probe(unsigned *sink, int iters, unsigned
         if (OP == 12) asm volatile("v_mul_lo_u32 %0, %1, %0" : "+v"(a[i]) : "v"(x));
         if (OP == 13) asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(c[i]) : "v"(x), "v"(a[i]) : "vcc");
         if (OP == 14) asm volatile("v_bitop3_b32 %0, %1, %0, %2 bitop3:0x96" : "+v"(a[i]) : "v"(x), "s"(seed));
+        if (OP == 15) asm volatile("v_cvt_scalef32_pk_fp4_f32 %0, %1, %1, %2" : "+v"(a[i]) : "v"(x), "v"(1.0f));
+        if (OP == 16) asm volatile("v_perm_b32 %0, %1, %0, %2" : "+v"(a[i]) : "v"(x), "s"(0x0C0C0B09u));
+        if (OP == 17) asm volatile("v_bfe_u32 %0, %0, 3, 1" : "+v"(a[i]));
+        if (OP == 18) asm volatile("v_lshlrev_b32 %0, 1, %0" : "+v"(a[i]));
+        if (OP == 19) asm volatile("v_and_or_b32 %0, %0, %1, %1" : "+v"(a[i]) : "v"(x));
+        if (OP == 20) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a[i]) : "v"(x));
+        if (OP == 21) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(a[i]) : "v"(x), "s"((unsigned long long)seed * 0x100000001ull));
+        if (OP == 22) asm volatile("v_bfi_b32 %0, %1, %0, %1" : "+v"(a[i]) : "v"(x));
+        if (OP == 23) asm volatile("v_bfe_i32 %0, %0, 3, 1" : "+v"(a[i]));
       }
     }
   }
@@ -48,29 +57,36 @@ __global__ void __launch_bounds__(256) probe(unsigned *sink, int iters, unsigned
   if (s == 0x12345678u) sink[blockIdx.x] = s;
 }
 
-template <int OP>
-void run(const char *name, int cus, int blocks_per_cu) {
+template <int OP, int CH = 8>
+void run(const char *name, int cus, int blocks_per_cu, int threads = 256) {
   unsigned *sink;
   (void)hipMalloc(&sink, sizeof(unsigned) * cus * 64);
   const int grid = cus * blocks_per_cu, iters = 4096;
-  hipLaunchKernelGGL(probe<OP>, dim3(grid), dim3(256), 0, 0, sink, iters, 1u);
+  hipLaunchKernelGGL((probe<OP, CH>), dim3(grid), dim3(threads), 0, 0, sink, iters, 1u);
   (void)hipDeviceSynchronize();
   hipEvent_t a, b;
   (void)hipEventCreate(&a);
   (void)hipEventCreate(&b);
   (void)hipEventRecord(a, 0);
   const int reps = 10;
-  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(probe<OP>, dim3(grid), dim3(256), 0, 0, sink, iters, 1u);
+  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL((probe<OP, CH>), dim3(grid), dim3(threads), 0, 0, sink, iters, 1u);
   (void)hipEventRecord(b, 0);
   (void)hipEventSynchronize(b);
   float ms = 0;
   (void)hipEventElapsedTime(&ms, a, b);
-  const double ops = (double)grid * 256 * iters * 64 * reps;
+  const double ops = (double)grid * threads * iters * 8 * CH * reps;
   const double rate = ops / (ms * 1e-3);
-  // cycles per wave64 instruction per SIMD at 2.4 GHz nominal
-  const double cyc = (double)cus * 4 * 64 * 2.4e9 / rate;
-  printf("%-24s blocks/CU=%2d  %.2f T lane-ops/s  (%.2f cyc/wave-instr/SIMD @2.4GHz)\n", name, blocks_per_cu,
-         rate / 1e12, cyc);
+  if (CH == 8) {
+    // cycles per wave64 instruction per SIMD at 2.4 GHz nominal
+    const double cyc = (double)cus * 4 * 64 * 2.4e9 / rate;
+    printf("%-24s blocks/CU=%2d  %.2f T lane-ops/s  (%.2f cyc/wave-instr/SIMD @2.4GHz)\n", name, blocks_per_cu,
+           rate / 1e12, cyc);
+  } else {
+    // one dependent chain in one wave per CU: cycles from issue to a dependent issue
+    const double per_wave = ms * 1e-3 / reps / ((double)iters * 8 * CH);
+    printf("%-24s one chain, one wave per CU: %.1f cycles per dependent instruction @2.4GHz\n", name,
+           per_wave * 2.4e9);
+  }
   (void)hipFree(sink);
 }
 
@@ -94,6 +110,22 @@ int main() {
     run<12>("v_mul_lo_u32", cus, bpc);
     run<13>("v_mad_u64_u32", cus, bpc);
     run<14>("v_bitop3_b32 (xor3)", cus, bpc);
+    run<15>("v_cvt_scalef32_pk_fp4", cus, bpc);
+    run<16>("v_perm_b32", cus, bpc);
+    run<17>("v_bfe_u32", cus, bpc);
+    run<18>("v_lshlrev_b32", cus, bpc);
+    run<19>("v_and_or_b32", cus, bpc);
+    run<20>("v_cndmask_b32 (vcc)", cus, bpc);
+    run<21>("v_cndmask_b32_e64 (s)", cus, bpc);
+    run<22>("v_bfi_b32", cus, bpc);
+    run<23>("v_bfe_i32", cus, bpc);
   }
+  // dependent-issue latency (packed small-network kernel, r03)
+  run<1, 1>("v_add_u32", cus, 1, 64);
+  run<0, 1>("v_bcnt_u32_b32", cus, 1, 64);
+  run<13, 1>("v_mad_u64_u32", cus, 1, 64);
+  run<14, 1>("v_bitop3_b32", cus, 1, 64);
+  run<15, 1>("v_cvt_scalef32_pk_fp4", cus, 1, 64);
+  run<16, 1>("v_perm_b32", cus, 1, 64);
   return 0;
 }
