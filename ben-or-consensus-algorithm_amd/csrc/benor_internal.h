@@ -91,12 +91,6 @@ struct KParams {
   // round r of the trials trial_begin + trial_list[i], i < *trial_list_len,
   // which tied in every round before r (x = their round r-1 coins); 0: round 1
   uint32_t cont_round;
-  // packed matrix-core kernel (variant 8): waves take work_chunk trials at a
-  // time from work[0]; the last wave to finish zeroes work[0] and work[1]
-  // (its finish count), so consecutive launches on one stream need no reset.
-  // nullptr: every wave runs one contiguous share of the launch.
-  uint32_t *work;
-  uint32_t work_chunk;
 };
 
 constexpr uint32_t kMfmaContRounds = 3;        // matrix-core passes up to round 3, then the popcount kernel
@@ -122,8 +116,6 @@ hipError_t launch_lane_m(const KParams &p, int grid_blocks, hipStream_t stream);
 template <int MM>
 hipError_t launch_mfma_small_m(const KParams &p, int grid_blocks, hipStream_t stream);
 constexpr uint32_t small_slots(uint32_t m) { return (32u / m) < 8u ? (32u / m) : 8u; }
-// Trials per chunk of the packed kernel's work counter (KParams::work); 0: static ranges.
-uint32_t small_chunk_trials(const KParams &p);
 
 // Matrix-core kernel (benor_mfma.h), W = 2..16, instantiated in benor_mfma_*.hip;
 // W = 17..64 (m <= 4096): the big-network form, benor_mfma_big.hip.

@@ -933,16 +933,6 @@ uint32_t block_waves(const KParams &p) {
   return (p.variant == 7 && p.W > 16u && !p.node_out && !p.rounds_out) ? mfma_big_block_waves(p) : (uint32_t)kWavesPerBlock;
 }
 
-// Two refills' worth (64 S trials each) per chunk: a wave asks the counter
-// about once per two iterations.  BENOR_SMALL_CHUNK=<refills> overrides
-// (0: every wave runs one contiguous share, no counter).
-uint32_t small_chunk_trials(const KParams &p) {
-  uint32_t refills = 2u;
-  if (const char *ev = getenv("BENOR_SMALL_CHUNK")) refills = (uint32_t)strtoul(ev, nullptr, 10);
-  if (refills > 64u) refills = 64u;
-  return refills * 64u * small_slots(p.m);
-}
-
 int lockstep_grid(const KParams &p, int device) {
   int cus = 256;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);

@@ -78,6 +78,12 @@ __device__ __forceinline__ uint32_t bsel(uint32_t m, uint32_t a, uint32_t b) {
   return r;
 }
 
+// All ones where a == b, else 0 (no compare: a VCC select is slow, see bsel).
+__device__ __forceinline__ uint32_t small_eq(uint32_t a, uint32_t b) {
+  const uint32_t d = a ^ b;
+  return ((d | (0u - d)) >> 31) - 1u;
+}
+
 // ORs the f32 bits of tile T's accumulator rows into their slots' words:
 // register j is receiver position 4 (j & 7) + 3 - (2T + (j >> 3)) (the
 // position its packed nibble would take), slot position / MM.
@@ -230,32 +236,15 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
 #pragma unroll
   for (int j = 0; j < 16; ++j) zero[j] = 0.0f;
 
-  // Trials reach the lanes through a wave pool [pool, pend): at every refill
-  // the lanes with a free slot take the next pool offsets in lane order
-  // (ballot + mbcnt), so a wave's lanes drain one shared pool and none sits
-  // idle while another still has trials.  With p.work the pool is a chunk of
-  // work_chunk trials taken from the launch-wide counter, the next chunk's
-  // ticket requested one chunk ahead; without it, the wave's share of the launch.
+  // This wave's trials: one contiguous share [pool, pend) of the launch.  At
+  // every refill the lanes with a free slot take the next offsets in lane
+  // order (ballot + mbcnt), so the wave's lanes drain one shared pool and none
+  // sits idle while another still has trials.
   const uint32_t waves_total = gridDim.x * kWavesPerBlock;
   const uint32_t wave_id = blockIdx.x * kWavesPerBlock + wv;
-  const bool dyn = p.work != nullptr;
-  uint32_t pool, pend, nxt_v = 0u;
-  bool drained;                                           // no chunk left to take
-  if (dyn) {
-    uint32_t chunk = p.work_chunk;
-    asm volatile("" : "+s"(chunk));
-    uint32_t t0 = 0u;
-    if (lane == 0u) t0 = atomicAdd(p.work, chunk);
-    if (lane == 0u) nxt_v = atomicAdd(p.work, chunk);
-    pool = (uint32_t)__builtin_amdgcn_readfirstlane((int)t0);
-    drained = pool >= trial_count;
-    pend = drained ? pool : (pool + chunk < trial_count ? pool + chunk : trial_count);
-  } else {
-    const uint32_t per_wave = (trial_count + waves_total - 1u) / waves_total;
-    pool = wave_id * per_wave < trial_count ? wave_id * per_wave : trial_count;
-    pend = pool + per_wave < trial_count ? pool + per_wave : trial_count;
-    drained = true;
-  }
+  const uint32_t per_wave = (trial_count + waves_total - 1u) / waves_total;
+  uint32_t pool = wave_id * per_wave < trial_count ? wave_id * per_wave : trial_count;
+  const uint32_t pend = pool + per_wave < trial_count ? pool + per_wave : trial_count;
   uint32_t toff[S], rnd[S];
 #pragma unroll
   for (uint32_t s = 0; s < S; ++s) {
@@ -270,34 +259,48 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
 #endif
 
   for (;;) {
-    // ---- refill free slots from the pool (/start, node.ts:167-188).
     // Selects are bit masks (v_bfi), not v_cndmask: on gfx950 a VCC-operand
     // v_cndmask_b32 issues at ~24 cycles per wave instruction
     // (profiles/r03-v7_valu_probe.txt).  Offsets are < 2^31: EMPTY's bit 31 tags it.
+    const bool tail = pool == pend;                       // wave-uniform: every trial handed out
     uint32_t any = 0u;
+    if (!tail) {
+      // ---- refill free slots from the pool (/start, node.ts:167-188)
 #pragma unroll
-    for (uint32_t s = 0; s < S; ++s) {
-      const uint32_t fr = toff[s] >> 31;                  // free slot
-      const uint64_t bal = __ballot(fr != 0u);
-      const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-      const uint32_t avail = pend - pool;
-      const uint32_t tm = 0u - (fr & ((rank - avail) >> 31));
-      toff[s] = bsel(tm, pool + rank, toff[s]);
-      rnd[s] = bsel(tm, 1u, rnd[s]);
-      any |= ~toff[s];
-      const uint32_t k = (uint32_t)__popcll(bal);
-      pool += k < avail ? k : avail;
-      if (pool == pend && !drained) {                     // next chunk (its ticket is back by now)
-        const uint32_t nb = (uint32_t)__builtin_amdgcn_readfirstlane((int)nxt_v);
-        uint32_t chunk = p.work_chunk;
-        asm volatile("" : "+s"(chunk));
-        if (nb >= trial_count) {
-          drained = true;
-        } else {
-          pool = nb;
-          pend = nb + chunk < trial_count ? nb + chunk : trial_count;
-          if (lane == 0u) nxt_v = atomicAdd(p.work, chunk);
-        }
+      for (uint32_t s = 0; s < S; ++s) {
+        const uint32_t fr = toff[s] >> 31;                // free slot
+        const uint64_t bal = __ballot(fr != 0u);
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+        const uint32_t avail = pend - pool;
+        const uint32_t tm = 0u - (fr & ((rank - avail) >> 31));
+        toff[s] = bsel(tm, pool + rank, toff[s]);
+        rnd[s] = bsel(tm, 1u, rnd[s]);
+        any |= ~toff[s];
+        const uint32_t k = (uint32_t)__popcll(bal);
+        pool += k < avail ? k : avail;
+      }
+    } else {
+      // ---- tail: a free slot runs a LATER round of the lane's first unfinished
+      // trial.  In lockstep, round r + 1 of a trial depends on round r only
+      // through "round r tied" (its x is then the round-r coins, a function of
+      // (trial, r): node.ts:110-111), so a trial's slots ("its chain") hold
+      // consecutive rounds evaluated side by side, and its first non-tied
+      // round decides.  The lane's last trials then need fewer iterations.
+      uint32_t lead = EMPTY;
+#pragma unroll
+      for (int s = (int)S - 1; s >= 0; --s) lead = bsel((toff[s] >> 31) - 1u, toff[s], lead);
+      uint32_t mx = 0u;                                   // the chain's last round
+#pragma unroll
+      for (uint32_t s = 0; s < S; ++s) mx = __builtin_elementwise_max(mx, rnd[s] & small_eq(toff[s], lead));
+      const uint32_t has = (lead >> 31) ^ 1u;
+#pragma unroll
+      for (uint32_t s = 0; s < S; ++s) {
+        const uint32_t take = (toff[s] >> 31) & has & ((mx - k_max - 1u) >> 31);   // rounds up to k_max + 1
+        const uint32_t tm = 0u - take;
+        mx += take;
+        toff[s] = bsel(tm, lead, toff[s]);
+        rnd[s] = bsel(tm, mx, rnd[s]);
+        any |= ~toff[s];
       }
     }
     if (!__any((any >> 31) != 0u)) break;                 // every slot free and the pool drained
@@ -387,17 +390,47 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
     // round, x = these coins), past k_max (undecided: bin v of its final x).
     // Halts of rounds 1-4 go to two packed per-lane counters (8-bit fields,
     // flushed every 31 iterations); later rounds and k_max to LDS atomics.
+    uint32_t act[S], out[S];                              // occupied; ended its trial (anything but a tie)
 #pragma unroll
     for (uint32_t s = 0; s < S; ++s) {
-      const uint32_t act = (toff[s] >> 31) ^ 1u;
-      const uint32_t fin = act & ((k_max - rnd[s]) >> 31);
-      const uint32_t run = act & (fin ^ 1u);
+      act[s] = (toff[s] >> 31) ^ 1u;
+      const uint32_t n1 = (0u - o1[s]) >> 31, n0 = (0u - o0[s]) >> 31, nq = (0u - oq[s]) >> 31;
+      out[s] = act[s] & (((k_max - rnd[s]) >> 31) | ((n1 & n0 & (nq ^ 1u)) ^ 1u));   // past k_max, or not a tie
+    }
+    // tail chains: a slot counts only if no earlier round of its trial ended
+    // it; a trial with no ending round advances every slot by the chain length
+    uint32_t first[S], done[S], adv[S];
+#pragma unroll
+    for (uint32_t s = 0; s < S; ++s) {
+      first[s] = out[s];
+      done[s] = out[s];
+      adv[s] = 1u;
+    }
+    if (tail) {
+#pragma unroll
+      for (uint32_t s = 0; s < S; ++s) {
+        uint32_t blocked = 0u, dn = 0u, k = 0u;
+#pragma unroll
+        for (uint32_t s2 = 0; s2 < S; ++s2) {
+          const uint32_t eq = small_eq(toff[s2], toff[s]) & 1u;
+          blocked |= eq & out[s2] & ((rnd[s2] - rnd[s]) >> 31);
+          dn |= eq & out[s2];
+          k += eq;
+        }
+        first[s] = out[s] & (blocked ^ 1u);
+        done[s] = act[s] & dn;
+        adv[s] = k;
+      }
+    }
+#pragma unroll
+    for (uint32_t s = 0; s < S; ++s) {
+      const uint32_t fin = first[s] & ((k_max - rnd[s]) >> 31);
+      const uint32_t run = first[s] & (fin ^ 1u);
       // every receiver decided 1 (node.ts:102-105) / decided 0 (node.ts:99-101) /
       // flipped its coin (node.ts:110-111): the slot's row OR is 0
       // (the ORs are < 2^31: 0 - o has bit 31 set iff o != 0)
       const uint32_t n1 = (0u - o1[s]) >> 31, n0 = (0u - o0[s]) >> 31, nq = (0u - oq[s]) >> 31;
       const uint32_t h1 = run & (n1 ^ 1u), h0 = run & n1 & (n0 ^ 1u);
-      const uint32_t tie = run & n1 & n0 & (nq ^ 1u);
       const uint32_t odd = run & n1 & n0 & nq;            // receivers not unanimous: impossible in lockstep
       const uint32_t early = (rnd[s] - 5u) >> 31;          // round <= 4
       const uint32_t sh = ((rnd[s] - 1u) & 3u) << 3;
@@ -418,8 +451,8 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
         atomicAdd(&lhist[bin & 0x7FFFFFFFu], 1u);
         if (bin >> 31) atomicAdd(&lhist[hist_len - 1u], 1u);
       }
-      rnd[s] += tie;
-      toff[s] |= 0u - (h1 | h0 | fin | odd);             // -> EMPTY
+      rnd[s] += adv[s] & (0u - (act[s] & (done[s] ^ 1u)));
+      toff[s] |= 0u - done[s];                            // -> EMPTY
     }
     if (++since_flush == 31u) {
       small_flush_counts(lhist, cnt0, cnt1);
@@ -439,17 +472,6 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
     o[10 + 3 * wave_id] = iters;
   }
 #endif
-  if (dyn) {                                              // the last wave out resets the counter
-    const uint32_t last = (uint32_t)__builtin_amdgcn_readfirstlane((int)nxt_v);   // its prefetch is back
-    asm volatile("" ::"s"(last));
-  }
-  if (dyn && lane == 0u) {
-    __threadfence();
-    if (atomicAdd(p.work + 1, 1u) == waves_total - 1u) {
-      atomicExch(p.work, 0u);
-      atomicExch(p.work + 1, 0u);
-    }
-  }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) {
     const uint32_t c = lhist[i];

@@ -86,7 +86,6 @@ struct bo_plan {
   uint32_t *d_scratch = nullptr;   // event mode
   uint32_t *d_defer = nullptr;     // matrix-core KIND > 0: deferred-trial list, its length, per-wave segments
   uint64_t defer_words = 0;
-  uint32_t *d_work = nullptr;      // packed matrix-core kernel: trial counter, finished waves
   int device = 0;
 };
 
@@ -404,12 +403,6 @@ int bo_plan_create(const bo_trials_cfg *cfg, bo_plan **out) {
       kp.crash_at = pl->d_crash;
       kp.scratch = pl->d_scratch;
     }
-    if (kp.variant == 8 && benor::small_chunk_trials(kp) != 0u) {   // the packed kernel's work counter
-      e = hipMalloc(&pl->d_work, 2 * sizeof(uint32_t));
-      if (e == hipSuccess) e = hipMemset(pl->d_work, 0, 2 * sizeof(uint32_t));
-      if (e != hipSuccess) { bo_plan_destroy(pl); return hip_fail(e, "work counter"); }
-      kp.work = pl->d_work;
-    }
   }
   *out = pl;
   return BO_OK;
@@ -423,7 +416,6 @@ void bo_plan_destroy(bo_plan *pl) {
   if (pl->d_crash) (void)hipFree(pl->d_crash);
   if (pl->d_scratch) (void)hipFree(pl->d_scratch);
   if (pl->d_defer) (void)hipFree(pl->d_defer);
-  if (pl->d_work) (void)hipFree(pl->d_work);
   delete pl;
 }
 
@@ -537,7 +529,6 @@ static int plan_launch_impl(bo_plan *pl, uint64_t trial_begin, uint64_t trial_co
     kp.trial_begin = trial_begin + done;
     kp.trial_count = n;
     const int grid = benor::lockstep_grid(kp, pl->device);
-    if (kp.work) kp.work_chunk = benor::small_chunk_trials(kp);
     HIP_TRY(benor::launch_lockstep(kp, grid, s));
     done += n;
   }

@@ -5,7 +5,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DBENOR_SMALL_TIMING -I include \
 //     -I ben-or-consensus-algorithm_amd/csrc -mllvm -amdgpu-mfma-vgpr-form \
 //     tools/small_phase_probe.hip -o tools/small_phase_probe
-//   tools/small_phase_probe [trials] [blocks_per_cu] [chunk refills, 0 = static ranges]
+//   tools/small_phase_probe [trials] [blocks_per_cu]
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -16,7 +16,6 @@ using namespace benor;
 int main(int argc, char **argv) {
   const uint64_t T = argc > 1 ? strtoull(argv[1], nullptr, 10) : 1000000ull;
   const int bpc = argc > 2 ? atoi(argv[2]) : 1;
-  const uint32_t refills = argc > 3 ? (uint32_t)atoi(argv[3]) : 0u;   // chunk in refills (0: static ranges)
   constexpr int MM = 6;
   KParams p{};
   p.N = 10;
@@ -39,13 +38,6 @@ int main(int argc, char **argv) {
   hipMemset(tim, 0, 8 * tim_words);
   p.hist = hist;
   p.rounds_out = reinterpret_cast<uint32_t *>(tim);
-  uint32_t *work = nullptr;
-  if (refills) {
-    hipMalloc(&work, 8);
-    hipMemset(work, 0, 8);
-    p.work = work;
-    p.work_chunk = refills * 64u * small_slots(MM);
-  }
   int cus = 256;
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
   const uint64_t groups = (T + 64 * small_slots(MM) - 1) / (64 * small_slots(MM));
@@ -66,7 +58,6 @@ int main(int argc, char **argv) {
   static unsigned long long t[8 + 3 * 256 * 16 * 4];
   hipMemcpy(t, tim, 8 * tim_words, hipMemcpyDeviceToHost);
   const double it = (double)t[6] / (double)t[7];
-  printf("chunk %u refills: ", refills);
   printf("trials %llu grid %llu blocks, %.1f us; waves %llu, %.2f iterations per wave\n", (unsigned long long)T,
          (unsigned long long)grid, ms * 1e3, t[7], it);
   const char *names[5] = {"refill/loop", "philox", "x -> R-phase", "P-phase", "slots"};
