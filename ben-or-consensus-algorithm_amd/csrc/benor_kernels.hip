@@ -893,9 +893,9 @@ hipError_t launch_lockstep(const KParams &p, int grid, hipStream_t s) {
     return hipGetLastError();
   }
   if (p.variant == 6) return dispatch_lane(p, grid, s, std::make_integer_sequence<int, (int)kMaxLaneM>{});
-  if (p.variant == 8 && !p.node_out && !p.rounds_out)
+  if (p.variant == 8 && !small_on_lane(p))
     return dispatch_mfma_small(p, grid, s, std::make_integer_sequence<int, (int)kMaxSmallMfmaM - 1>{});   // m = 2..32
-  if (p.variant == 8) {                      // state launch of a packed shape: the lane kernel
+  if (p.variant == 8) {                      // state launch or short launch of a packed shape: the lane kernel
     KParams q = p;
     q.variant = p.base_variant;
     q.G = p.base_G;
@@ -933,6 +933,18 @@ uint32_t block_waves(const KParams &p) {
   return (p.variant == 7 && p.W > 16u && !p.node_out && !p.rounds_out) ? mfma_big_block_waves(p) : (uint32_t)kWavesPerBlock;
 }
 
+// A packed-shape launch runs on the lane kernel when it writes per-node
+// state (network API) or is short: the packed kernel's iterations are
+// latency-bound until a wave holds several batches of trials, and the
+// geometric tail of its last trials weighs on a short launch.
+// BENOR_SMALL_MIN_TRIALS overrides the crossover.
+bool small_on_lane(const KParams &p) {
+  if (p.node_out || p.rounds_out) return true;
+  uint64_t min_trials = kSmallMinTrials;
+  if (const char *ev = getenv("BENOR_SMALL_MIN_TRIALS")) min_trials = strtoull(ev, nullptr, 10);
+  return p.trial_count < min_trials;
+}
+
 int lockstep_grid(const KParams &p, int device) {
   int cus = 256;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
@@ -943,7 +955,7 @@ int lockstep_grid(const KParams &p, int device) {
     return (int)(grid < 1 ? 1 : grid);
   }
   if (p.variant == 8) {
-    if (p.node_out || p.rounds_out) {        // state launch: the lane kernel
+    if (small_on_lane(p)) {                  // state launch or short launch: the lane kernel
       KParams q = p;
       q.variant = p.base_variant;
       q.G = p.base_G;

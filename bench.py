@@ -206,7 +206,7 @@ def other_configs(benor, torch, k_max, seed):
             decided = T - undecided
             tie_rounds = (rounds - k_max * undecided) - decided
             ops = nr * (words + 3) + tie_rounds * m * 41 / 4
-            roof = {"bound": "valu issue (tallies, compares, Philox coins)", "kernel": "lane (one trial per lane)",
+            roof = {"bound": "valu issue (tallies, compares, Philox coins)", "kernel": benor.KERNEL_NAMES[plan.kernel],
                     "unit": "T lane-ops/s", "lane_ops_per_node_round": ops / max(nr, 1),
                     "achieved": ops / (ms * 1e-3) / 1e12}
         if plan.kernel != benor.BO_KERNEL_MFMA:

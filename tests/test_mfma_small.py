@@ -20,6 +20,13 @@ import benor
 import oracle
 
 
+@pytest.fixture(autouse=True)
+def packed_for_every_launch(monkeypatch):
+    """Launches shorter than kSmallMinTrials run the lane kernel; these tests
+    pin the packed kernel itself at every trial count."""
+    monkeypatch.setenv("BENOR_SMALL_MIN_TRIALS", "0")
+
+
 def first_f(N, F):
     return [i < F for i in range(N)]
 
@@ -140,6 +147,19 @@ def test_mfma_small_equals_lane_kernel(N, F, T):
     np.testing.assert_array_equal(ha, b.run(0, T))
     cut = T // 3 + 11
     np.testing.assert_array_equal(ha, a.run(0, cut) + a.run(cut, T - cut))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T", [1_000_000, 5_000_000])
+def test_short_launch_crossover_same_histogram(monkeypatch, T):
+    """Under the default crossover a 10^6-trial launch of configs[1] runs on
+    the lane kernel and a 5*10^6 one on the packed kernel; both equal the
+    other kernel's histogram."""
+    monkeypatch.delenv("BENOR_SMALL_MIN_TRIALS")
+    p = plan(10, 4, seed=99, k_max=16)
+    h = p.run(7, T)
+    monkeypatch.setenv("BENOR_SMALL_MIN_TRIALS", "0" if T < 4_000_000 else str(1 << 40))
+    np.testing.assert_array_equal(h, p.run(7, T))
 
 
 @pytest.mark.gpu
