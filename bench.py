@@ -39,6 +39,7 @@ differs from --gpus is an error, never a silent single-GPU run.
 import argparse
 import hashlib
 import json
+import math
 import os
 import socket
 import subprocess
@@ -227,6 +228,65 @@ def other_configs(benor, torch, k_max, seed):
             out[name]["steady_state"] = {"trials": 20 * T, "kernel_ms": ms20, "node_rounds_per_s": nr20 / (ms20 * 1e-3),
                                          "roofline_frac": roof["frac"] * (nr20 / ms20) / (nr / ms)}
     return out
+
+
+def delivery_blocks(m, q):
+    """Philox4x32-10 blocks one receiver-phase of random delivery draws for its
+    q-of-m inbox (oracle_delivery_mask), and the information
+    floor log2 C(m, q) / 128.  The sampler's fix-up length is random: its mean
+    is taken from the normal approximation of the Bernoulli count."""
+    k = min(q, m - q)
+    floor = (math.lgamma(m + 1) - math.lgamma(q + 1) - math.lgamma(m - q + 1)) / math.log(2) / 128
+    if k >= 64 and 8 * k > m:                          # Bernoulli(a/16) mask + exact fix-up
+        a = min(15, max(1, -(-16 * q // m)))
+        tz = (a & -a).bit_length() - 1
+        mask_words = -(-m // 32) * (4 - tz)
+        p = a / 16
+        mu, sd = m * p - q, math.sqrt(m * p * (1 - p))
+        dist = sd * math.sqrt(2 / math.pi) * math.exp(-mu * mu / (2 * sd * sd)) + mu * math.erf(mu / (sd * math.sqrt(2)))
+        accept = (m * p) / m if mu > 0 else 1 - p
+        b = max(1, (m - 1).bit_length())
+        fields = dist / accept
+        return {"sampler": f"bernoulli a={a}/16 + fix-up", "blocks": mask_words / 4 + fields / (32 // b) / 4,
+                "floor_blocks": floor}
+    return {"sampler": "floyd", "blocks": k / 4, "floor_blocks": floor}
+
+
+def random_delivery_config(benor, torch, k_max, seed, N=1024, F=341, f=0, T=100_000):
+    """SURVEY §8f #4 at N=1024, F=341, f=0 (every receiver tallies a random
+    q = N - F of the m = N - f live senders): one warm-up and one timed launch
+    at full occupancy, and its real bound -- VALU issue of the Philox blocks
+    that draw the delivery masks (41 lane-ops per block), two
+    receiver-phases per live node-round -- beside the information floor."""
+    import numpy as np
+
+    stream = torch.cuda.current_stream()
+    plan = benor.TrialsPlan(N, F, [i < f for i in range(N)], seed=seed, k_max=k_max,
+                            mode=benor.BO_MODE_RANDOM_DELIVERY)
+    h = torch.zeros(plan.hist_len, dtype=torch.int64, device="cuda")
+    plan.launch(0, T // 10, h.data_ptr(), stream.cuda_stream)
+    torch.cuda.synchronize()
+    h.zero_()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    plan.launch(T, T, h.data_ptr(), stream.cuda_stream)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1)
+    hist = h.cpu().numpy().astype(np.uint64)
+    m = plan.live_nodes
+    nr, rounds = node_rounds(hist, m, k_max)
+    rate = nr / (ms * 1e-3)
+    d = delivery_blocks(m, N - F)
+    ops = 41 * 2 * d["blocks"]
+    return {"trials": T, "kernel_ms": ms, "node_rounds_per_s": rate, "mean_rounds": rounds / T,
+            "agreement_violations": int(hist[-1]),
+            "roofline": {"bound": "valu issue (Philox4x32-10 delivery-mask blocks)", "kernel": "random delivery",
+                         "sampler": d["sampler"], "philox_blocks_per_node_round": 2 * d["blocks"],
+                         "floor_blocks_per_node_round": 2 * d["floor_blocks"], "lane_ops_per_node_round": ops,
+                         "unit": "T lane-ops/s", "achieved": rate * ops / 1e12, "peak": SPEC_PEAK_POPC / 1e12,
+                         "frac": rate * ops / SPEC_PEAK_POPC,
+                         "floor_frac": rate * 41 * 2 * d["floor_blocks"] / SPEC_PEAK_POPC}}
 
 
 def network_latency(benor, reps=200):
@@ -449,6 +509,7 @@ def main():
     if world == 1 and not args.no_other_configs:
         out["other_configs"] = other_configs(benor, torch, k_max, args.seed)
         out["other_configs"]["C1 N=5,F=1 network API"] = network_latency(benor)
+        out["other_configs"]["C4 N=1024,F=341,f=0 random delivery"] = random_delivery_config(benor, torch, k_max, args.seed)
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(N, F, k_max, args.seed, args.cpu_seconds)
     if rank == 0:
