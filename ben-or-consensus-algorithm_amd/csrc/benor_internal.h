@@ -116,7 +116,10 @@ hipError_t launch_lane_m(const KParams &p, int grid_blocks, hipStream_t stream);
 template <int MM>
 hipError_t launch_mfma_small_m(const KParams &p, int grid_blocks, hipStream_t stream);
 constexpr uint32_t small_slots(uint32_t m) { return (32u / m) < 8u ? (32u / m) : 8u; }
-constexpr uint64_t kSmallMinTrials = 10000000;  // shorter packed-shape launches run on the lane kernel
+constexpr uint32_t kSmallMaxRound = 3;   // rounds on the matrix cores; a later tie -> the lane path
+// LDS words per wave: round-2 and round-3 lists (2 batches each), lane-path queue (a batch + 64)
+constexpr uint32_t small_wave_words(uint32_t m) { return 5u * 64u * small_slots(m) + 64u; }
+constexpr uint64_t kSmallMinTrials = 500000;    // shorter packed-shape launches run on the lane kernel
 bool small_on_lane(const KParams &p);
 
 // Matrix-core kernel (benor_mfma.h), W = 2..16, instantiated in benor_mfma_*.hip;

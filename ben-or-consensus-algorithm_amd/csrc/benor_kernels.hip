@@ -786,7 +786,7 @@ void plan_geometry(KParams &p) {
       p.base_variant = p.variant;
       p.base_G = p.G;
       p.variant = 8;
-      p.lds_bytes = p.hist_bytes;                   // the histogram and the parameter block only
+      p.lds_bytes = p.hist_bytes + kWavesPerBlock * small_wave_words(p.m) * 4u;   // histogram, round lists
     }
     return;
   }
@@ -934,9 +934,9 @@ uint32_t block_waves(const KParams &p) {
 }
 
 // A packed-shape launch runs on the lane kernel when it writes per-node
-// state (network API) or is short: the packed kernel's iterations are
-// latency-bound until a wave holds several batches of trials, and the
-// geometric tail of its last trials weighs on a short launch.
+// state (network API) or is short: below ~10^6 trials the packed kernel's
+// partial round lists at the end of each wave outweigh its per-trial gain
+// (DESIGN §4.2).
 // BENOR_SMALL_MIN_TRIALS overrides the crossover.
 bool small_on_lane(const KParams &p) {
   if (p.node_out || p.rounds_out) return true;
@@ -962,10 +962,9 @@ int lockstep_grid(const KParams &p, int device) {
       q.lds_bytes = q.hist_bytes + kWavesPerBlock * q.wave_bytes;
       return lockstep_grid(q, device);
     }
-    // Packed matrix-core kernel: a wave owns a contiguous range of trials and
-    // runs 64 * S slots per iteration until its last trial halts, so each wave
-    // takes ~3 iterations' worth of fresh trials (its lanes' tails average
-    // out), at most 2 workgroups per CU.
+    // Packed matrix-core kernel: a wave runs batches of 64 S trials (fresh
+    // round-1 batches strided over the waves, then its own round lists), so
+    // each wave gets ~3 fresh batches, at most 4 workgroups per CU.
     const uint64_t batch = 64u * small_slots(p.m);
     const uint64_t groups = (p.trial_count + batch - 1u) / batch;
     uint64_t per_cu = groups / ((uint64_t)cus * kWavesPerBlock * 3u);

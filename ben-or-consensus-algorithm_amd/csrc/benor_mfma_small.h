@@ -32,27 +32,27 @@
 //     senders: 8 (c1 - c0); the fp4 conversion saturates it to the proposal
 //     +6 (p1), -6 (p0) or 0 ("?", a tie) -- node.ts:63-69.
 //   P-phase (node.ts:88-113): from the proposals, three 0/1 operands -- the
-//     votes that are not 1, not 0, not "?" -- counted per receiver (scale
-//     2^3, C = -0.5): the result is negative iff that count is 0, i.e. the
-//     inbox is all 1 (n1 = m), all 0 (n0 = m) or all "?" (n0 = n1 = 0).
+//     votes that are not 1, not 0, not "?" -- counted per receiver (zero C):
+//     the f32 result is +0.0 iff that count is 0, i.e. the inbox is all 1
+//     (n1 = m), all 0 (n0 = m) or all "?" (n0 = n1 = 0); the OR of a slot's
+//     rows' bits tests every receiver of the slot at once.
 //   In lockstep every receiver's inbox is the whole slot (node.ts:45,171), so
 //   it is unanimous: all 1 -> every receiver decides 1 (n1 = m > F,
 //   node.ts:102-105), all 0 -> decides 0, all "?" -> every receiver flips its
-//   coin (node.ts:110-111) and nobody decides.  Each receiver's sign bits are
+//   coin (node.ts:110-111) and nobody decides.  Each receiver's row is
 //   checked; a slot whose receivers do not all fall in one of the three cases
 //   (impossible in lockstep) is re-run with the lane kernel's logic.
-// Slots.  Each slot holds one trial across its rounds: a slot that decided
-// is counted in bin 3r + v and takes the lane's next trial; a tied slot's next
-// x plane is exactly its coins of round r (every node took its coin), a pure
-// function of (seed, trial, r), so it simply runs round r + 1 with
-// x = coin_word(r); after a tie in round k_max the slot reads its final x (the
-// round-k_max coins) and is counted undecided.  Every slot draws one Philox
-// block per round (its initial values or its coins), the S blocks of a lane
-// computed together so that their dependency chains interleave.  A wave owns
-// a contiguous range of trials and lane l takes offsets l, l + 64, ... of it
-// whenever a slot frees up: no lists, no cross-lane traffic.  A slot whose
-// receivers are not unanimous (impossible in lockstep) re-runs its trial with
-// the lane kernel's per-lane round logic (benor_lane.h).
+// Rounds.  A batch is 64 S trials in the same round.  A slot that halted is
+// counted in bin 3r + v.  A tied slot's next x plane is exactly its coins of
+// round r (every node took its coin), a pure function of (seed, trial, r), so
+// its trial offset goes to the wave's round r + 1 list in LDS and runs there
+// with x = coin_word(r) (the continuation idea of benor_mfma.h, here inside one
+// launch).  A wave takes a full batch from the deepest full list first, then
+// fresh round-1 trials, and drains the partial lists at the end; a trial that
+// ties in round kSmallMaxRound (q(m)^3 of them: ~3 % at m = 6) or whose
+// receivers are not unanimous (impossible in lockstep) is re-run from round 1
+// with the lane kernel's per-lane round logic (benor_lane.h), 64 queued trials
+// at a time.
 #pragma once
 
 #include "benor_lane.h"
@@ -76,12 +76,6 @@ __device__ __forceinline__ uint32_t bsel(uint32_t m, uint32_t a, uint32_t b) {
   uint32_t r;
   asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
   return r;
-}
-
-// All ones where a == b, else 0 (no compare: a VCC select is slow, see bsel).
-__device__ __forceinline__ uint32_t small_eq(uint32_t a, uint32_t b) {
-  const uint32_t d = a ^ b;
-  return ((d | (0u - d)) >> 31) - 1u;
 }
 
 // ORs the f32 bits of tile T's accumulator rows into their slots' words:
@@ -150,36 +144,11 @@ __device__ uint32_t small_lane_trial(uint32_t k0, uint32_t k1, uint64_t tr, uint
   }
 }
 
-// Adds one lane's packed halt counters (8-bit fields: rounds 1-4) into the
-// LDS histogram (bins 3r + v) and clears them.
-__device__ __forceinline__ void small_flush_counts(uint32_t *lhist, uint32_t &cnt0, uint32_t &cnt1) {
-#pragma unroll
-  for (uint32_t f = 0; f < 4; ++f) {
-    const uint32_t a0 = (cnt0 >> (8u * f)) & 255u, a1 = (cnt1 >> (8u * f)) & 255u;
-    if (a0) atomicAdd(&lhist[3u * (f + 1u)], a0);
-    if (a1) atomicAdd(&lhist[3u * (f + 1u) + 1u], a1);
-  }
-  cnt0 = cnt1 = 0u;
-}
-
-// BENOR_SMALL_TIMING (tools/small_phase_probe.hip only): lane 0 of every wave
-// adds the shader-clock cycles of each phase to p.rounds_out[0..7].
-#ifdef BENOR_SMALL_TIMING
-#define SMALL_T(i)                                                         \
-  do {                                                                     \
-    const uint64_t t_ = __builtin_amdgcn_s_memtime();                      \
-    tph[i] += t_ - tlast;                                                  \
-    tlast = t_;                                                            \
-  } while (0)
-#else
-#define SMALL_T(i) \
-  do {             \
-  } while (0)
-#endif
 
 template <int MM>
 __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
   constexpr uint32_t S = small_slots(MM);
+  constexpr uint32_t BATCH = 64u * S;
   constexpr uint32_t LIVE = MM == 32 ? ~0u : ((1u << MM) - 1u);
   constexpr uint32_t USED = S * MM;                              // position bits in use per lane half
   constexpr uint32_t EMPTY = 0xFFFFFFFFu;
@@ -190,6 +159,11 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
   asm volatile("" : "+s"(hist_len), "+s"(trial_count));
   uint32_t *lhist = reinterpret_cast<uint32_t *>(smem);
   uint32_t *keys = reinterpret_cast<uint32_t *>(smem + p.hist_bytes - kParamBytes);
+  // The wave's LDS slice: the round-2 and round-3 lists (2 BATCH each: a list
+  // is drained once it holds a batch, and one batch adds at most BATCH) and
+  // the lane-path queue (drained 64 at a time).
+  uint32_t *list2 = reinterpret_cast<uint32_t *>(smem + p.hist_bytes) + wv * small_wave_words(MM);
+  uint32_t *list3 = list2 + 2u * BATCH, *lq = list2 + 4u * BATCH;
   for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) lhist[i] = 0u;
   if (threadIdx.x == 0) {
     keys[0] = (uint32_t)p.seed;
@@ -203,6 +177,7 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
   const uint32_t fixed1 = random_init ? 0u : (p.init_plane[0].z & LIVE);
   const uint32_t rmask = random_init ? ~0u : 0u;         // round-1 x: the Philox word, or the fixed plane
   const uint32_t F = p.F, k_max = p.k_max;
+  const uint32_t R = k_max < kSmallMaxRound ? k_max : kSmallMaxRound;   // last matrix-core round
 
   // Block-diagonal A of the two tiles (see the header): lane (row rho, K half hk).
   mf_v4i A0, A1;
@@ -236,109 +211,54 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
 #pragma unroll
   for (int j = 0; j < 16; ++j) zero[j] = 0.0f;
 
-  // This wave's trials: one contiguous share [pool, pend) of the launch.  At
-  // every refill the lanes with a free slot take the next offsets in lane
-  // order (ballot + mbcnt), so the wave's lanes drain one shared pool and none
-  // sits idle while another still has trials.
   const uint32_t waves_total = gridDim.x * kWavesPerBlock;
   const uint32_t wave_id = blockIdx.x * kWavesPerBlock + wv;
-  const uint32_t per_wave = (trial_count + waves_total - 1u) / waves_total;
-  uint32_t pool = wave_id * per_wave < trial_count ? wave_id * per_wave : trial_count;
-  const uint32_t pend = pool + per_wave < trial_count ? pool + per_wave : trial_count;
-  uint32_t toff[S], rnd[S];
-#pragma unroll
-  for (uint32_t s = 0; s < S; ++s) {
-    toff[s] = EMPTY;
-    rnd[s] = 0u;
-  }
-  uint32_t cnt0 = 0u, cnt1 = 0u, since_flush = 0u;        // packed halts of rounds 1-4, v = 0 / 1
-#ifdef BENOR_SMALL_TIMING
-  uint64_t tph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast = __builtin_amdgcn_s_memtime();
-  const uint64_t tstart = tlast;
-  uint32_t iters = 0;
-#endif
+  const uint32_t ngroups = (trial_count + BATCH - 1u) / BATCH;
+  uint32_t g = wave_id, len2 = 0u, len3 = 0u, lql = 0u;          // wave-uniform
+  uint32_t h0[3] = {0u, 0u, 0u}, h1[3] = {0u, 0u, 0u};             // halts with 0 / 1 in rounds 1..3 (wave totals)
 
   for (;;) {
-    // Selects are bit masks (v_bfi), not v_cndmask: on gfx950 a VCC-operand
-    // v_cndmask_b32 issues at ~24 cycles per wave instruction
-    // (profiles/r03-v7_valu_probe.txt).  Offsets are < 2^31: EMPTY's bit 31 tags it.
-    const bool tail = pool == pend;                       // wave-uniform: every trial handed out
-    uint32_t any = 0u;
-    if (!tail) {
-      // ---- refill free slots from the pool (/start, node.ts:167-188)
-#pragma unroll
-      for (uint32_t s = 0; s < S; ++s) {
-        const uint32_t fr = toff[s] >> 31;                // free slot
-        const uint64_t bal = __ballot(fr != 0u);
-        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-        const uint32_t avail = pend - pool;
-        const uint32_t tm = 0u - (fr & ((rank - avail) >> 31));
-        toff[s] = bsel(tm, pool + rank, toff[s]);
-        rnd[s] = bsel(tm, 1u, rnd[s]);
-        any |= ~toff[s];
-        const uint32_t k = (uint32_t)__popcll(bal);
-        pool += k < avail ? k : avail;
-      }
-    } else {
-      // ---- tail: a free slot runs a LATER round of the lane's first unfinished
-      // trial.  In lockstep, round r + 1 of a trial depends on round r only
-      // through "round r tied" (its x is then the round-r coins, a function of
-      // (trial, r): node.ts:110-111), so a trial's slots ("its chain") hold
-      // consecutive rounds evaluated side by side, and its first non-tied
-      // round decides.  The lane's last trials then need fewer iterations.
-      uint32_t lead = EMPTY;
-#pragma unroll
-      for (int s = (int)S - 1; s >= 0; --s) lead = bsel((toff[s] >> 31) - 1u, toff[s], lead);
-      uint32_t mx = 0u;                                   // the chain's last round
-#pragma unroll
-      for (uint32_t s = 0; s < S; ++s) mx = __builtin_elementwise_max(mx, rnd[s] & small_eq(toff[s], lead));
-      const uint32_t has = (lead >> 31) ^ 1u;
-#pragma unroll
-      for (uint32_t s = 0; s < S; ++s) {
-        const uint32_t take = (toff[s] >> 31) & has & ((mx - k_max - 1u) >> 31);   // rounds up to k_max + 1
-        const uint32_t tm = 0u - take;
-        mx += take;
-        toff[s] = bsel(tm, lead, toff[s]);
-        rnd[s] = bsel(tm, mx, rnd[s]);
-        any |= ~toff[s];
-      }
-    }
-    if (!__any((any >> 31) != 0u)) break;                 // every slot free and the pool drained
-#ifdef BENOR_SMALL_TIMING
-    ++iters;
-#endif
-    SMALL_T(0);
+    // ---- the next batch: the deepest full list, else fresh round-1 trials
+    // (batch g, g + waves_total, ...), else the partial lists
+    uint32_t r, n;
+    const uint32_t *src = nullptr;
+    if (R >= 3u && len3 >= BATCH) { r = 3u; n = BATCH; len3 -= n; src = list3 + len3; }
+    else if (R >= 2u && len2 >= BATCH) { r = 2u; n = BATCH; len2 -= n; src = list2 + len2; }
+    else if (g < ngroups) { r = 1u; n = trial_count - g * BATCH; n = n < BATCH ? n : BATCH; }
+    else if (len2) { r = 2u; n = len2; src = list2; len2 = 0u; }
+    else if (len3) { r = 3u; n = len3; src = list3; len3 = 0u; }
+    else break;
+    r = (uint32_t)__builtin_amdgcn_readfirstlane((int)r);
+    n = (uint32_t)__builtin_amdgcn_readfirstlane((int)n);
 
-    // ---- x words: round 1 the initial values, round r > 1 the coins of round
-    // r - 1 after a tie (node.ts:110-111); a slot past k_max reads the coins of
-    // round k_max, its final x.  One Philox block per slot, the S chains advanced
-    // together (philox4x32_10_multi).
+    // ---- slot s of this lane takes batch entry 64 s + lane; its x word is
+    // the initial values (round 1, node.ts:167-188) or, after r - 1 ties, the
+    // coins of round r - 1 (node.ts:110-111): one Philox block per slot, the S
+    // chains advanced together (philox4x32_10_multi).
     const uint2 kk = lds_keys(keys);
     const uint64_t tb = lds_u64(keys + 2);
+    uint32_t toff[S];
     uint4 blk[S];
-    uint32_t fmask[S];                                    // all ones where the slot runs round 1
+    const uint32_t c3 = r == 1u ? (kStreamInit << 24) : (((r - 2u) >> 2) | (kStreamCoin << 24));
 #pragma unroll
     for (uint32_t s = 0; s < S; ++s) {
+      const uint32_t e = s * 64u + lane;
+      const uint32_t gb = g * BATCH + e;
+      toff[s] = e < n ? (src ? src[e] : gb) : EMPTY;
       const uint64_t tr = tb + (toff[s] & 0x7FFFFFFFu);
-      fmask[s] = 0u - ((rnd[s] - 2u) >> 31);
-      const uint32_t c3 = bsel(fmask[s], kStreamInit << 24, ((rnd[s] - 2u) >> 2) | (kStreamCoin << 24));
       blk[s] = make_uint4((uint32_t)tr, (uint32_t)(tr >> 32), 0u, c3);
     }
+    if (r == 1u) g += waves_total;
     philox4x32_10_multi<S>(kk.x, kk.y, blk);
-    SMALL_T(1);
-    uint32_t xs[S];
+    const uint32_t wsel = r == 1u ? 0u : ((r - 2u) & 3u);        // wave-uniform word of the block
     uint32_t w = 0u;
 #pragma unroll
     for (uint32_t s = 0; s < S; ++s) {
-      const uint32_t ws = rnd[s] - 2u;                    // coin word (r - 2) & 3 of the block
-      const uint32_t m0 = (uint32_t)__builtin_amdgcn_sbfe((int)ws, 0, 1), m1 = (uint32_t)__builtin_amdgcn_sbfe((int)ws, 1, 1);
-      const uint32_t lo = bsel(m0, blk[s].y, blk[s].x), hi = bsel(m0, blk[s].w, blk[s].z);
-      const uint32_t coin = bsel(m1, hi, lo);
-      const uint32_t init = bsel(rmask, blk[s].x, fixed1);
-      xs[s] = bsel(fmask[s], init, coin) & LIVE;
+      uint32_t x = wsel == 0u ? blk[s].x : wsel == 1u ? blk[s].y : wsel == 2u ? blk[s].z : blk[s].w;
+      if (r == 1u) x = bsel(rmask, x, fixed1);
       uint32_t keep = (toff[s] >> 31) - 1u;               // ~0 unless the slot is EMPTY
       asm("" : "+v"(keep));                               // a mask, not a select
-      w |= (xs[s] & keep) << (s * MM);
+      w |= (x & LIVE & keep) << (s * MM);
     }
     // B: +1.0 (0x2) where x = 1, -1.0 (0xA) where x = 0, 0 on unused positions
     const mf_v4i Ez = small_expand(used_mask & ~w);
@@ -354,7 +274,6 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
       const mf_v16f r1 = mfma_count<3>(A1, bx, zero);
       bp = mf_v4i{(int)small_pack(r0, 0), (int)small_pack(r0, 8), (int)small_pack(r1, 0), (int)small_pack(r1, 8)};
     }
-    SMALL_T(2);
     // P-phase operands: 1.0 on the used positions whose vote is NOT 1 / NOT 0 /
     // NOT "?" (proposal nibbles: +6 = 0111, -6 = 1111, "?" = 0000).
     mf_v4i bn1, bn0, bnq;
@@ -384,94 +303,90 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
       small_or_rows<MM>(mfma_count<3>(A, bnq, zero), T, oq);
       __builtin_amdgcn_sched_barrier(0);
     }
-    SMALL_T(3);
 
-    // ---- per slot: halted (bin 3r + v; node.ts:116-145 auto-stop), tied (next
-    // round, x = these coins), past k_max (undecided: bin v of its final x).
-    // Halts of rounds 1-4 go to two packed per-lane counters (8-bit fields,
-    // flushed every 31 iterations); later rounds and k_max to LDS atomics.
-    uint32_t act[S], out[S];                              // occupied; ended its trial (anything but a tie)
+    // ---- per slot: every receiver decided 1 (node.ts:102-105) / decided 0
+    // (node.ts:99-101) -> halted in round r (auto-stop, node.ts:116-145); every
+    // receiver flipped its coin (node.ts:110-111) -> round r + 1's list, or the
+    // lane path after round R; receivers not unanimous (impossible in
+    // lockstep) -> the lane path.  (The ORs are < 2^31: 0 - o has bit 31 set
+    // iff o != 0.)
+    const bool last = r >= R;
+    uint32_t *dst = last ? lq : (r == 1u ? list2 : list3);
+    uint32_t dlen = last ? lql : (r == 1u ? len2 : len3);
+    uint32_t c1 = 0u, c0 = 0u, odd_any = 0u;
 #pragma unroll
     for (uint32_t s = 0; s < S; ++s) {
-      act[s] = (toff[s] >> 31) ^ 1u;
+      const uint32_t valid = (toff[s] >> 31) ^ 1u;
       const uint32_t n1 = (0u - o1[s]) >> 31, n0 = (0u - o0[s]) >> 31, nq = (0u - oq[s]) >> 31;
-      out[s] = act[s] & (((k_max - rnd[s]) >> 31) | ((n1 & n0 & (nq ^ 1u)) ^ 1u));   // past k_max, or not a tie
+      c1 += valid & (n1 ^ 1u);
+      c0 += valid & n1 & (n0 ^ 1u);
+      const uint32_t tie = valid & n1 & n0 & (nq ^ 1u);
+      odd_any |= valid & n1 & n0 & nq;
+      const uint64_t bt = ballot(tie != 0u);
+      if (tie) dst[dlen + __builtin_amdgcn_mbcnt_hi((uint32_t)(bt >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bt, 0u))] = toff[s];
+      dlen += (uint32_t)__popcll(bt);
     }
-    // tail chains: a slot counts only if no earlier round of its trial ended
-    // it; a trial with no ending round advances every slot by the chain length
-    uint32_t first[S], done[S], adv[S];
-#pragma unroll
-    for (uint32_t s = 0; s < S; ++s) {
-      first[s] = out[s];
-      done[s] = out[s];
-      adv[s] = 1u;
-    }
-    if (tail) {
+    if (last) lql = dlen;
+    else if (r == 1u) len2 = dlen;
+    else len3 = dlen;
+    if (__any(odd_any != 0u)) {                           // impossible in lockstep: queue for the lane path
 #pragma unroll
       for (uint32_t s = 0; s < S; ++s) {
-        uint32_t blocked = 0u, dn = 0u, k = 0u;
+        const uint32_t valid = (toff[s] >> 31) ^ 1u;
+        const uint32_t odd = valid & ((0u - o1[s]) >> 31) & ((0u - o0[s]) >> 31) & ((0u - oq[s]) >> 31);
+        const uint64_t bo = ballot(odd != 0u);
+        if (odd) lq[lql + __builtin_amdgcn_mbcnt_hi((uint32_t)(bo >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bo, 0u))] = toff[s];
+        lql += (uint32_t)__popcll(bo);
+      }
+    }
+    // wave totals of the halts: bit-sliced ballots (c <= S <= 8)
+    uint32_t t1 = 0u, t0 = 0u;
 #pragma unroll
-        for (uint32_t s2 = 0; s2 < S; ++s2) {
-          const uint32_t eq = small_eq(toff[s2], toff[s]) & 1u;
-          blocked |= eq & out[s2] & ((rnd[s2] - rnd[s]) >> 31);
-          dn |= eq & out[s2];
-          k += eq;
-        }
-        first[s] = out[s] & (blocked ^ 1u);
-        done[s] = act[s] & dn;
-        adv[s] = k;
-      }
+    for (uint32_t b = 0; (1u << b) <= S; ++b) {
+      t1 += (uint32_t)__popcll(ballot(((c1 >> b) & 1u) != 0u)) << b;
+      t0 += (uint32_t)__popcll(ballot(((c0 >> b) & 1u) != 0u)) << b;
     }
+    if (r == 1u) { h1[0] += t1; h0[0] += t0; }
+    else if (r == 2u) { h1[1] += t1; h0[1] += t0; }
+    else { h1[2] += t1; h0[2] += t0; }
+
+    // ---- lane path, 64 queued trials at a time (every lane busy): from round
+    // 1 with the lane kernel's per-lane logic (small_lane_trial)
+    while (lql >= 64u) {
+      lql -= 64u;
+      const uint32_t t = lq[lql + lane];
+      const uint64_t tr = lds_u64(keys + 2) + t;
+      const uint2 k2 = lds_keys(keys);
+      uint32_t x = fixed1;
+      if (random_init)
+        x = philox4x32_10<false>(k2.x, k2.y, make_uint4((uint32_t)tr, (uint32_t)(tr >> 32), 0u, kStreamInit << 24)).x & LIVE;
+      const uint32_t bin = small_lane_trial<MM>(k2.x, k2.y, tr, x, F, k_max, 0u, make_uint4(0u, 0u, 0u, 0u), 0u);
+      atomicAdd(&lhist[bin & 0x7FFFFFFFu], 1u);
+      if (bin >> 31) atomicAdd(&lhist[hist_len - 1u], 1u);
+    }
+  }
+  // ---- the rest of the lane-path queue
+  if (lane < lql) {
+    const uint32_t t = lq[lane];
+    const uint64_t tr = lds_u64(keys + 2) + t;
+    const uint2 k2 = lds_keys(keys);
+    uint32_t x = fixed1;
+    if (random_init)
+      x = philox4x32_10<false>(k2.x, k2.y, make_uint4((uint32_t)tr, (uint32_t)(tr >> 32), 0u, kStreamInit << 24)).x & LIVE;
+    const uint32_t bin = small_lane_trial<MM>(k2.x, k2.y, tr, x, F, k_max, 0u, make_uint4(0u, 0u, 0u, 0u), 0u);
+    atomicAdd(&lhist[bin & 0x7FFFFFFFu], 1u);
+    if (bin >> 31) atomicAdd(&lhist[hist_len - 1u], 1u);
+  }
+  // halts of the matrix-core rounds: lane 2q + v adds bin 3 (q + 1) + v
+  {
+    uint32_t c = 0u;
 #pragma unroll
-    for (uint32_t s = 0; s < S; ++s) {
-      const uint32_t fin = first[s] & ((k_max - rnd[s]) >> 31);
-      const uint32_t run = first[s] & (fin ^ 1u);
-      // every receiver decided 1 (node.ts:102-105) / decided 0 (node.ts:99-101) /
-      // flipped its coin (node.ts:110-111): the slot's row OR is 0
-      // (the ORs are < 2^31: 0 - o has bit 31 set iff o != 0)
-      const uint32_t n1 = (0u - o1[s]) >> 31, n0 = (0u - o0[s]) >> 31, nq = (0u - oq[s]) >> 31;
-      const uint32_t h1 = run & (n1 ^ 1u), h0 = run & n1 & (n0 ^ 1u);
-      const uint32_t odd = run & n1 & n0 & nq;            // receivers not unanimous: impossible in lockstep
-      const uint32_t early = (rnd[s] - 5u) >> 31;          // round <= 4
-      const uint32_t sh = ((rnd[s] - 1u) & 3u) << 3;
-      cnt1 += (h1 & early) << sh;
-      cnt0 += (h0 & early) << sh;
-      if ((((h1 | h0) & (early ^ 1u)) | fin) != 0u) {
-        const uint32_t v = xs[s] == LIVE ? 1u : (xs[s] == 0u ? 0u : 2u);
-        atomicAdd(&lhist[fin ? v : 3u * rnd[s] + h1], 1u);
-      }
-      if (odd) {                                          // re-run it with the lane kernel's logic
-        const uint2 k2 = lds_keys(keys);
-        const uint64_t tr = lds_u64(keys + 2) + toff[s];
-        uint32_t x = fixed1;
-        if (random_init)
-          x = philox4x32_10<false>(k2.x, k2.y, make_uint4((uint32_t)tr, (uint32_t)(tr >> 32), 0u, kStreamInit << 24)).x &
-              LIVE;
-        const uint32_t bin = small_lane_trial<MM>(k2.x, k2.y, tr, x, F, k_max, 0u, make_uint4(0u, 0u, 0u, 0u), 0u);
-        atomicAdd(&lhist[bin & 0x7FFFFFFFu], 1u);
-        if (bin >> 31) atomicAdd(&lhist[hist_len - 1u], 1u);
-      }
-      rnd[s] += adv[s] & (0u - (act[s] & (done[s] ^ 1u)));
-      toff[s] |= 0u - done[s];                            // -> EMPTY
+    for (uint32_t q = 0; q < 3u; ++q) {
+      if (lane == 2u * q) c = h0[q];
+      if (lane == 2u * q + 1u) c = h1[q];
     }
-    if (++since_flush == 31u) {
-      small_flush_counts(lhist, cnt0, cnt1);
-      since_flush = 0u;
-    }
-    SMALL_T(4);
+    if (lane < 6u && c) atomicAdd(&lhist[3u * (lane / 2u + 1u) + (lane & 1u)], c);
   }
-  small_flush_counts(lhist, cnt0, cnt1);
-#ifdef BENOR_SMALL_TIMING
-  if (lane == 0) {
-    unsigned long long *o = reinterpret_cast<unsigned long long *>(p.rounds_out);
-    for (int i = 0; i < 5; ++i) atomicAdd(&o[i], (unsigned long long)tph[i]);
-    atomicAdd(&o[6], (unsigned long long)iters);
-    atomicAdd(&o[7], 1ull);
-    o[8 + 3 * wave_id] = tstart;                          // per wave: start, end, iterations
-    o[9 + 3 * wave_id] = __builtin_amdgcn_s_memtime();
-    o[10 + 3 * wave_id] = iters;
-  }
-#endif
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) {
     const uint32_t c = lhist[i];

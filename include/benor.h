@@ -201,7 +201,7 @@ enum {
   BO_KERNEL_MFMA = 7,
   BO_KERNEL_MFMA_SMALL = 8 /* packed matrix-core kernel: 2 <= m <= 32, m > F, no "?" initial value;
                               64 * min(32/m, 8) trials per wave iteration, block-diagonal e2m1 products;
-                              launches of fewer than 10^7 trials run the lane kernel
+                              launches of fewer than 5 * 10^5 trials run the lane kernel
                               (BENOR_SMALL_MIN_TRIALS overrides) */
 };
 
