@@ -150,6 +150,7 @@ def launch_ranks(n, argv):
 OTHER_CONFIGS = [("C2 N=10,F=4", 10, 4, 1_000_000), ("C2 N=10,F=5 (F>N/2, no decision)", 10, 5, 1_000_000),
                  ("C3 N=256,F=85", 256, 85, 10_000_000)]
 OTHER_REPS = 10          # back-to-back launches per config, each of its T trials
+SS_REPS = 5              # back-to-back steady-state launches (20 T trials each)
 
 
 def other_configs(benor, torch, k_max, seed):
@@ -217,15 +218,19 @@ def other_configs(benor, torch, k_max, seed):
                      "trials_per_s": T / (ms * 1e-3), "mean_rounds": rounds / T, "undecided_trials": undecided,
                      "roofline": roof}
         if ms < 1.0:
-            # a launch this short is mostly ramp-up: also time 20x the trials for the steady state
+            # a launch this short is mostly ramp-up: also time 20x the trials for the
+            # steady state, SS_REPS such launches back to back (amortising the events)
             h.zero_()
             e0.record(stream)
-            plan.launch((1 + OTHER_REPS) * T, 20 * T, h.data_ptr(), stream.cuda_stream)
+            for r in range(SS_REPS):
+                plan.launch((1 + OTHER_REPS + 20 * r) * T, 20 * T, h.data_ptr(), stream.cuda_stream)
             e1.record(stream)
             torch.cuda.synchronize()
-            ms20 = e0.elapsed_time(e1)
+            ms20 = e0.elapsed_time(e1) / SS_REPS
             nr20, _ = node_rounds(h.cpu().numpy().astype(np.uint64), m, k_max)
-            out[name]["steady_state"] = {"trials": 20 * T, "kernel_ms": ms20, "node_rounds_per_s": nr20 / (ms20 * 1e-3),
+            nr20 /= SS_REPS
+            out[name]["steady_state"] = {"trials": 20 * T, "launches_timed": SS_REPS, "kernel_ms": ms20,
+                                         "node_rounds_per_s": nr20 / (ms20 * 1e-3),
                                          "roofline_frac": roof["frac"] * (nr20 / ms20) / (nr / ms)}
     return out
 
@@ -279,7 +284,7 @@ def random_delivery_config(benor, torch, k_max, seed, N=1024, F=341, f=0, T=100_
     rate = nr / (ms * 1e-3)
     d = delivery_blocks(m, N - F)
     ops = 41 * 2 * d["blocks"]
-    return {"trials": T, "kernel_ms": ms, "node_rounds_per_s": rate, "mean_rounds": rounds / T,
+    return {"trials": T, "launches_timed": 1, "kernel_ms": ms, "node_rounds_per_s": rate, "mean_rounds": rounds / T,
             "agreement_violations": int(hist[-1]),
             "roofline": {"bound": "valu issue (Philox4x32-10 delivery-mask blocks)", "kernel": "random delivery",
                          "sampler": d["sampler"], "philox_blocks_per_node_round": 2 * d["blocks"],
@@ -403,7 +408,7 @@ def main():
 
     # Clock ramp before the warm-up steps: ~0.3 s of the matrix-core (or
     # popcount) peak probe, whose figure is reported as roofline.peak_probe,
-    # then ~0.2 s of a neighbouring shape's kernel (F - 1: the same kernel
+    # then ~0.6 s of a neighbouring shape's kernel (F - 1: the same kernel
     # family and instruction mix under another template instance, so a kernel
     # trace keeps it apart from the bench kernel).  Without the ramp the first
     # two bench launches run 6-15 % slower while clocks and power settle, and a
@@ -420,14 +425,18 @@ def main():
             ramp_hist = torch.zeros(ramp.hist_len, dtype=torch.int64, device="cuda")
             t_ramp = time.perf_counter()
             r = 0
-            while time.perf_counter() - t_ramp < 0.2:
+            while time.perf_counter() - t_ramp < 0.6:     # back to back, two launches in flight
                 ramp.launch(r * T, T, ramp_hist.data_ptr(), stream.cuda_stream)
-                torch.cuda.synchronize()
+                if r:
+                    ev_ramp.synchronize()
+                ev_ramp = torch.cuda.Event()
+                ev_ramp.record(stream)
                 r += 1
-            del ramp, ramp_hist
     for s in range(args.warmup):
         step(s)
     torch.cuda.synchronize()
+    if not args.no_peak_probe and F > 0:
+        del ramp, ramp_hist                      # freed after the warm-up: no hipFree next to a bench launch
     hist.zero_()
     # kernel-only timing with HIP events on the launch stream
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]

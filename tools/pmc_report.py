@@ -172,11 +172,20 @@ def reconcile(bench, durs):
     rf = bench["roofline"]
     rows.append(f"| headline | `{short(bk)}` | {len(durs[bk][1])} | {avg:.4f} | {rf['kernel_ms']:.4f} | "
                 f"{rf['frac']:.4f} | {rf['frac'] * rf['kernel_ms'] / avg:.4f} | {rf['kernel_ms'] / avg:.3f} |")
+    # each config's kernel: the first unused benor kernel of its family
+    # (the roofline's "kernel" name) dispatched after the headline
     later = sorted((v[0], k) for k, v in durs.items()
                    if k != bk and "benor::" in k and "peak" not in k and v[0] > durs[bk][0])
-    names = [n for n, oc in bench.get("other_configs", {}).items() if "kernel_ms" in oc]
-    for name, (_, k) in zip(names, later):
-        oc = bench["other_configs"][name]
+    used = set()
+    for name, oc in bench.get("other_configs", {}).items():
+        if "kernel_ms" not in oc:
+            continue
+        fam = family_symbol(oc.get("roofline", {}).get("kernel", ""))
+        cand = [k for _, k in later if k not in used and (fam is None or fam in k)]
+        if not cand:
+            continue
+        k = cand[0]
+        used.add(k)
         reps = oc.get("launches_timed", 10)
         d = durs[k][1]
         a = statistics.mean(d[1:1 + reps])
@@ -184,12 +193,23 @@ def reconcile(bench, durs):
         rows.append(f"| {name} | `{short(k)}` | {reps} of {len(d)} (#1..#{reps}) | {a:.5f} | "
                     f"{oc['kernel_ms']:.5f} | {fr:.4f} | {fr * oc['kernel_ms'] / a:.4f} | {oc['kernel_ms'] / a:.3f} |")
         ss = oc.get("steady_state")
-        if ss and len(d) > 1 + reps:
-            a2 = d[1 + reps]
-            rows.append(f"| {name}, steady state ({ss['trials']} trials) | `{short(k)}` | 1 (#{1 + reps}) | {a2:.5f} | "
-                        f"{ss['kernel_ms']:.5f} | {ss['roofline_frac']:.4f} | {ss['roofline_frac'] * ss['kernel_ms'] / a2:.4f} | "
-                        f"{ss['kernel_ms'] / a2:.3f} |")
+        sreps = ss.get("launches_timed", 1) if ss else 0
+        if ss and len(d) >= 1 + reps + sreps:
+            a2 = statistics.mean(d[1 + reps:1 + reps + sreps])
+            rows.append(f"| {name}, steady state ({ss['trials']} trials) | `{short(k)}` | {sreps} (#{1 + reps}..#{reps + sreps}) "
+                        f"| {a2:.5f} | {ss['kernel_ms']:.5f} | {ss['roofline_frac']:.4f} | "
+                        f"{ss['roofline_frac'] * ss['kernel_ms'] / a2:.4f} | {ss['kernel_ms'] / a2:.3f} |")
     return rows
+
+
+def family_symbol(kernel_name):
+    """Kernel-symbol substring of a roofline's kernel family (benor.KERNEL_NAMES)."""
+    for fam, sym in (("packed matrix core", "benor_mfma_small_kernel"), ("random delivery", "benor_random_kernel"),
+                     ("matrix core", "benor_mfma_"), ("lane", "benor_lane_kernel"), ("W popcount", "_w_kernel"),
+                     ("blocked", "blocked_kernel"), ("event", "benor_event_kernel")):
+        if fam in kernel_name:
+            return sym
+    return None
 
 
 def short(k):
