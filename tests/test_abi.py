@@ -119,3 +119,14 @@ def test_no_silent_cpu_fallback():
         benor.startConsensus(5, seed=1)
     with pytest.raises(RuntimeError, match="libbenor error 4"):
         benor.TrialsPlan(10, 4)
+
+
+def test_library_built_from_these_sources():
+    """libbenor.so bakes the digest of the kernel sources it was built from
+    (Makefile KSHA); build() rebuilds on a mismatch and smoke() refuses one."""
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import __graft_entry__ as g
+
+    assert benor.kernel_version() == g.kernel_digest()
