@@ -246,6 +246,34 @@ __global__ void __launch_bounds__(256) benor_mfma_kernel(KParams p) {
     // counts the x plane; the packed result is its proposal.
     uint32_t bp[MT][2];
     uint32_t qz = 0u;                          // KIND > 0: a live receiver proposed "?"
+    if constexpr (SURE && W <= 4) {
+      // Few products per tile (W): the sign packing of tile i - 1 is issued
+      // among tile i's products, a few VALU per MFMA, so it runs in their
+      // shadow (two accumulators live).
+      mf_v16f racc[2];
+#pragma unroll
+      for (int i = 0; i <= MT; ++i) {
+        if (i < MT) {
+          asm volatile("" : "+v"(ones));
+          mf_v16f acc = mfma_count(ones, bx[0], cr);
+#pragma unroll
+          for (int c = 1; c < W; ++c) acc = mfma_count(ones, bx[c], acc);
+          racc[i & 1] = acc;
+        }
+        if (i > 0) {
+          bp[i - 1][0] = pack_signs8(racc[(i - 1) & 1], 0);
+          bp[i - 1][1] = pack_signs8(racc[(i - 1) & 1], 8);
+        }
+        if (i < MT && i > 0) {
+#pragma unroll
+          for (int c = 0; c < W; ++c) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, (16 + W - 1) / W, 0);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
       asm volatile("" : "+v"(ones));
@@ -283,6 +311,36 @@ __global__ void __launch_bounds__(256) benor_mfma_kernel(KParams p) {
     uint32_t any1, any0, halt = (uint32_t)ballot(valid);
     if constexpr (SURE) {
       uint32_t s_or = 0u, s_and = ~0u;        // sign bit = "not d0" = x1
+      if constexpr (W <= 4) {
+        // tile i - 1's sign fold among tile i's products, as the R-phase
+        mf_v16f pacc[2];
+#pragma unroll
+        for (int i = 0; i <= MT; ++i) {
+          if (i < MT) {
+            asm volatile("" : "+v"(ones));
+            mf_v16f acc = mfma_count(ones, pb[0], cp);
+#pragma unroll
+            for (int c = 1; c < KP; ++c) acc = mfma_count(ones, pb[c], acc);
+            pacc[i & 1] = acc;
+          }
+          if (i > 0) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+              const uint32_t u = __float_as_uint(pacc[(i - 1) & 1][j]);
+              s_or |= u;
+              s_and &= u;
+            }
+          }
+          if (i < MT && i > 0) {
+#pragma unroll
+            for (int c = 0; c < KP; ++c) {
+              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+              __builtin_amdgcn_sched_group_barrier(0x002, (16 + KP - 1) / KP, 0);
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
         asm volatile("" : "+v"(ones));

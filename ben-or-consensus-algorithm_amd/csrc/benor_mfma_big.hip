@@ -60,6 +60,24 @@ __host__ __device__ constexpr uint32_t big_slice_words(uint32_t W, uint32_t NT, 
 constexpr uint32_t kBigNt8MinW = 28;
 __host__ __device__ constexpr uint32_t big_nt(uint32_t W) { return W >= kBigNt8MinW ? 8u : 4u; }
 
+// x1 words of chunks 4j .. 4j+3 of this lane half (h) from /start Philox block
+// 2j + h: half h keeps words h and 2 + h of its block and trades the other two
+// with lane l ^ 32 (DS bpermute).
+__device__ __forceinline__ void big_x_block(const uint32_t *keys, uint64_t trial, uint32_t h, uint32_t j,
+                                            uint32_t (&xw)[4]) {
+  const uint2 kk = lds_keys(keys);
+  const uint4 r = philox4x32_10(kk.x, kk.y, make_uint4((uint32_t)trial, (uint32_t)(trial >> 32), 2u * j + h,
+                                                       kStreamInit << 24));
+  const uint32_t keep_a = h ? r.y : r.x, keep_b = h ? r.w : r.z;
+  const uint32_t give_a = h ? r.x : r.y, give_b = h ? r.z : r.w;
+  const uint32_t recv_a = (uint32_t)__shfl_xor((int)give_a, 32);
+  const uint32_t recv_b = (uint32_t)__shfl_xor((int)give_b, 32);
+  xw[0] = h ? recv_a : keep_a;
+  xw[1] = h ? recv_b : keep_b;
+  xw[2] = h ? keep_a : recv_a;
+  xw[3] = h ? keep_b : recv_b;
+}
+
 template <int KIND, int NT, int BW, bool REGEN>
 __global__ void __launch_bounds__(64 * BW) benor_mfma_big_kernel(KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -166,39 +184,62 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_big_kernel(KParams p) {
       for (int u = 0; u < NT; ++u) acc[u] = mf_v16f{};
       if constexpr (REGEN) {
         // x1 words of chunks 4j .. 4j+3 from Philox block 2j + h, the lane
-        // halves trading two words (as the /start code of the LDS form)
+        // halves trading two words (as the /start code of the LDS form).
+        // Blocks before the last hold 4 full chunks (none is chunk W - 1):
+        // block j + 1's Philox is issued among block j's 4 NT products, one
+        // MFMA and a few VALU at a time, so it runs in the products' shadow.
         const uint64_t trial = lds_u64(keys + 2) + t;
         const uint32_t NJ = (((W + 1u) >> 1) + 1u) >> 1;
-        for (uint32_t j = 0; j < NJ; ++j) {
-          const uint2 kk = lds_keys(keys);
-          const uint4 r = philox4x32_10(kk.x, kk.y,
-                                        make_uint4((uint32_t)trial, (uint32_t)(trial >> 32), 2u * j + h, kStreamInit << 24));
-          const uint32_t keep_a = h ? r.y : r.x, keep_b = h ? r.w : r.z;
-          const uint32_t give_a = h ? r.x : r.y, give_b = h ? r.z : r.w;
-          const uint32_t recv_a = (uint32_t)__shfl_xor((int)give_a, 32);
-          const uint32_t recv_b = (uint32_t)__shfl_xor((int)give_b, 32);
-          const uint32_t xw[4] = {h ? recv_a : keep_a, h ? recv_b : keep_b, h ? keep_a : recv_a, h ? keep_b : recv_b};
+        uint32_t xw[4];
+        big_x_block(keys, trial, h, 0u, xw);
+        for (uint32_t j = 0; j + 1u < NJ; ++j) {
+          uint32_t xn[4];
+          big_x_block(keys, trial, h, j + 1u, xn);
 #pragma unroll
           for (uint32_t q = 0; q < 4u; ++q) {
-            const uint32_t c = 4u * j + q;
-            if (c < W) {
-              const mf_v4i b = expand_votes(c == W - 1u ? xw[q] & last_mask : xw[q]);
+            const mf_v4i b = expand_votes(xw[q]);
 #pragma unroll
-              for (int u = 0; u < NT; ++u) {
-                asm volatile("" : "+v"(ones));
-                acc[u] = mfma_count<4>(ones, b, acc[u]);
-              }
+            for (int u = 0; u < NT; ++u) {
+              asm volatile("" : "+v"(ones));
+              acc[u] = mfma_count<4>(ones, b, acc[u]);
+            }
+          }
+#pragma unroll
+          for (int k = 0; k < 4 * NT; ++k) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);   // up to three VALU
+          }
+#pragma unroll
+          for (uint32_t q = 0; q < 4u; ++q) xw[q] = xn[q];
+        }
+        // the last block: chunks 4 (NJ - 1) .. W - 1, chunk W - 1 masked
+#pragma unroll
+        for (uint32_t q = 0; q < 4u; ++q) {
+          const uint32_t c = 4u * (NJ - 1u) + q;
+          if (c < W) {
+            const mf_v4i b = expand_votes(c == W - 1u ? xw[q] & last_mask : xw[q]);
+#pragma unroll
+            for (int u = 0; u < NT; ++u) {
+              asm volatile("" : "+v"(ones));
+              acc[u] = mfma_count<4>(ones, b, acc[u]);
             }
           }
         }
       } else {
+        // chunk c + 1's x word is read from LDS among chunk c's NT products
+        uint32_t wcur = X[lane];
         for (uint32_t c = 0; c < W; ++c) {
-          const mf_v4i b = expand_votes(X[c * 64u + lane]);
+          const uint32_t wnext = X[(c + 1u < W ? c + 1u : c) * 64u + lane];
+          const mf_v4i b = expand_votes(wcur);
 #pragma unroll
           for (int u = 0; u < NT; ++u) {
             asm volatile("" : "+v"(ones));     // opaque per tile: no two tiles' products merge
             acc[u] = mfma_count<4>(ones, b, acc[u]);
           }
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);     // the next word's read first
+#pragma unroll
+          for (int k = 0; k < NT; ++k) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          wcur = wnext;
         }
       }
 #pragma unroll
@@ -231,13 +272,19 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_big_kernel(KParams p) {
       mf_v16f acc[NT];
 #pragma unroll
       for (int u = 0; u < NT; ++u) acc[u] = mf_v16f{};
+      uint32_t wcur = PL[lane];                // chunk k + 1's word read among chunk k's products
       for (uint32_t k = 0; k < KP; ++k) {
-        const mf_v4i b = expand_votes(PL[k * 64u + lane]);
+        const uint32_t wnext = PL[(k + 1u < KP ? k + 1u : k) * 64u + lane];
+        const mf_v4i b = expand_votes(wcur);
 #pragma unroll
         for (int u = 0; u < NT; ++u) {
           asm volatile("" : "+v"(ones));
           acc[u] = KIND == 2 ? mfma_count<1>(ones, b, acc[u]) : mfma_count(ones, b, acc[u]);
         }
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+#pragma unroll
+        for (int u = 0; u < NT; ++u) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        wcur = wnext;
       }
 #pragma unroll
       for (int u = 0; u < NT; ++u) {

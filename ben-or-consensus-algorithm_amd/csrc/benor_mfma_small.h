@@ -49,10 +49,10 @@
 // with x = coin_word(r) (the continuation idea of benor_mfma.h, here inside one
 // launch).  A wave takes a full batch from the deepest full list first, then
 // fresh round-1 trials, and drains the partial lists at the end; a trial that
-// ties in round kSmallMaxRound (q(m)^3 of them: ~3 % at m = 6) or whose
-// receivers are not unanimous (impossible in lockstep) is re-run from round 1
-// with the lane kernel's per-lane round logic (benor_lane.h), 64 queued trials
-// at a time.
+// ties in round kSmallMaxRound (q(m)^3 of them: ~3 % at m = 6) continues
+// from there with the lane kernel's per-lane round logic (benor_lane.h), 64
+// queued trials at a time; one whose receivers are not unanimous (impossible
+// in lockstep) is re-run from round 1 the same way.
 #pragma once
 
 #include "benor_lane.h"
@@ -144,6 +144,31 @@ __device__ uint32_t small_lane_trial(uint32_t k0, uint32_t k1, uint64_t tr, uint
   }
 }
 
+
+// One lane-path trial, counted into the LDS histogram.  A queue entry is a
+// trial that tied in every round up to R: its state after round R is x = its
+// round-R coins and nobody decided, so the lane kernel's round logic
+// continues it from there (coin block of rounds 1-4 in hand, R <= 3); an
+// entry with bit 31 set (receivers not unanimous) starts over from round 1.
+template <int MM>
+__device__ void small_lane_path(const uint32_t *keys, uint32_t e, uint32_t fixed1, bool random_init, uint32_t F,
+                                uint32_t k_max, uint32_t R, uint32_t *lhist, uint32_t hist_len) {
+  constexpr uint32_t LIVE = MM == 32 ? ~0u : ((1u << MM) - 1u);
+  const uint64_t tr = lds_u64(keys + 2) + (e & 0x7FFFFFFFu);
+  const uint2 k2 = lds_keys(keys);
+  uint32_t bin;
+  if (e >> 31) {
+    uint32_t x = fixed1;
+    if (random_init)
+      x = philox4x32_10<false>(k2.x, k2.y, make_uint4((uint32_t)tr, (uint32_t)(tr >> 32), 0u, kStreamInit << 24)).x & LIVE;
+    bin = small_lane_trial<MM>(k2.x, k2.y, tr, x, F, k_max, 0u, make_uint4(0u, 0u, 0u, 0u), 0u);
+  } else {
+    const uint4 cw = coin_block<false>(k2.x, k2.y, (uint32_t)tr, (uint32_t)(tr >> 32), 0u, 1u);
+    bin = small_lane_trial<MM>(k2.x, k2.y, tr, coin_word(cw, R) & LIVE, F, k_max, R, cw, 1u);
+  }
+  atomicAdd(&lhist[bin & 0x7FFFFFFFu], 1u);
+  if (bin >> 31) atomicAdd(&lhist[hist_len - 1u], 1u);
+}
 
 template <int MM>
 __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
@@ -335,7 +360,8 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
         const uint32_t valid = (toff[s] >> 31) ^ 1u;
         const uint32_t odd = valid & ((0u - o1[s]) >> 31) & ((0u - o0[s]) >> 31) & ((0u - oq[s]) >> 31);
         const uint64_t bo = ballot(odd != 0u);
-        if (odd) lq[lql + __builtin_amdgcn_mbcnt_hi((uint32_t)(bo >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bo, 0u))] = toff[s];
+        if (odd)                                          // bit 31: re-run from round 1
+          lq[lql + __builtin_amdgcn_mbcnt_hi((uint32_t)(bo >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bo, 0u))] = toff[s] | 0x80000000u;
         lql += (uint32_t)__popcll(bo);
       }
     }
@@ -350,33 +376,14 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
     else if (r == 2u) { h1[1] += t1; h0[1] += t0; }
     else { h1[2] += t1; h0[2] += t0; }
 
-    // ---- lane path, 64 queued trials at a time (every lane busy): from round
-    // 1 with the lane kernel's per-lane logic (small_lane_trial)
+    // ---- lane path, 64 queued trials at a time (every lane busy)
     while (lql >= 64u) {
       lql -= 64u;
-      const uint32_t t = lq[lql + lane];
-      const uint64_t tr = lds_u64(keys + 2) + t;
-      const uint2 k2 = lds_keys(keys);
-      uint32_t x = fixed1;
-      if (random_init)
-        x = philox4x32_10<false>(k2.x, k2.y, make_uint4((uint32_t)tr, (uint32_t)(tr >> 32), 0u, kStreamInit << 24)).x & LIVE;
-      const uint32_t bin = small_lane_trial<MM>(k2.x, k2.y, tr, x, F, k_max, 0u, make_uint4(0u, 0u, 0u, 0u), 0u);
-      atomicAdd(&lhist[bin & 0x7FFFFFFFu], 1u);
-      if (bin >> 31) atomicAdd(&lhist[hist_len - 1u], 1u);
+      small_lane_path<MM>(keys, lq[lql + lane], fixed1, random_init, F, k_max, R, lhist, hist_len);
     }
   }
   // ---- the rest of the lane-path queue
-  if (lane < lql) {
-    const uint32_t t = lq[lane];
-    const uint64_t tr = lds_u64(keys + 2) + t;
-    const uint2 k2 = lds_keys(keys);
-    uint32_t x = fixed1;
-    if (random_init)
-      x = philox4x32_10<false>(k2.x, k2.y, make_uint4((uint32_t)tr, (uint32_t)(tr >> 32), 0u, kStreamInit << 24)).x & LIVE;
-    const uint32_t bin = small_lane_trial<MM>(k2.x, k2.y, tr, x, F, k_max, 0u, make_uint4(0u, 0u, 0u, 0u), 0u);
-    atomicAdd(&lhist[bin & 0x7FFFFFFFu], 1u);
-    if (bin >> 31) atomicAdd(&lhist[hist_len - 1u], 1u);
-  }
+  if (lane < lql) small_lane_path<MM>(keys, lq[lane], fixed1, random_init, F, k_max, R, lhist, hist_len);
   // halts of the matrix-core rounds: lane 2q + v adds bin 3 (q + 1) + v
   {
     uint32_t c = 0u;
