@@ -129,11 +129,21 @@ hipError_t launch_mfma(const KParams &p, int grid_blocks, hipStream_t stream);
 hipError_t launch_mfma_big(const KParams &p, int grid_blocks, hipStream_t stream);
 uint32_t mfma_big_lds_bytes(const KParams &p, uint32_t block_waves);   // dynamic LDS of one workgroup of the big form
 uint32_t mfma_big_block_waves(const KParams &p);                       // its waves per workgroup (1, 2 or 4)
+// Workgroup-cooperative big-network form (benor_mfma_coop.hip): the waves of a
+// workgroup share one 32-trial group; deferral segments are per workgroup.
+bool mfma_big_coop(const KParams &p);                                   // this big-network launch runs it
+hipError_t launch_mfma_coop(const KParams &p, int grid_blocks, hipStream_t stream);
+uint32_t mfma_coop_lds_bytes(const KParams &p);
+uint32_t mfma_coop_block_waves(const KParams &p);                      // 4 or 8
+int mfma_coop_blocks_per_cu(const KParams &p);                         // resident workgroups per CU (occupancy)
 
 // Grid size that fills the current device for this configuration, in
 // workgroups of block_waves(p) waves.
 int lockstep_grid(const KParams &p, int device);
 uint32_t block_waves(const KParams &p);
+// Owners of deferral segments in a launch of `grid` workgroups: one per wave,
+// or one per workgroup in the cooperative big-network form.
+uint64_t defer_units(const KParams &p, int grid);
 
 // Matrix-core microbenchmark: e2m1 32x32x64 multiply-adds executed per launch.
 hipError_t launch_mfma_peak(float *sink, int grid_blocks, int iters, hipStream_t stream, double *terms_per_launch);

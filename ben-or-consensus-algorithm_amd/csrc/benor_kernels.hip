@@ -930,7 +930,12 @@ hipError_t launch_lockstep(const KParams &p, int grid, hipStream_t s) {
 // workgroup size is chosen for occupancy (mfma_big_block_waves).  Every other
 // kernel: kWavesPerBlock.
 uint32_t block_waves(const KParams &p) {
+  if (mfma_big_coop(p)) return mfma_coop_block_waves(p);
   return (p.variant == 7 && p.W > 16u && !p.node_out && !p.rounds_out) ? mfma_big_block_waves(p) : (uint32_t)kWavesPerBlock;
+}
+
+uint64_t defer_units(const KParams &p, int grid) {
+  return mfma_big_coop(p) ? (uint64_t)grid : (uint64_t)grid * block_waves(p);
 }
 
 // A packed-shape launch runs on the lane kernel when it writes per-node
@@ -979,6 +984,12 @@ int lockstep_grid(const KParams &p, int device) {
     uint64_t grid = (uint64_t)cus * per_cu;
     const uint64_t need = (groups + kWavesPerBlock - 1u) / kWavesPerBlock;
     if (need < grid) grid = need;
+    return (int)(grid < 1u ? 1u : grid);
+  }
+  if (mfma_big_coop(p)) {   // cooperative big-network form: one 32-trial group per workgroup at a time
+    const uint64_t groups = (p.trial_count + 31u) / 32u;
+    uint64_t grid = (uint64_t)cus * (uint64_t)mfma_coop_blocks_per_cu(p);
+    if (groups < grid) grid = groups;
     return (int)(grid < 1u ? 1u : grid);
   }
   // 32 waves per CU when registers and LDS allow it.

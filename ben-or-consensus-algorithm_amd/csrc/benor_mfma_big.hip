@@ -27,56 +27,12 @@
 //    0 for acc > 0, 1 for acc < 0.
 // Trials with a "?" proposal (KIND 1, 2) or an undecided receiver (KIND 2)
 // are deferred to the popcount kernel exactly as in benor_mfma.h.
-#include "benor_mfma.h"
+#include "benor_mfma_big.h"
+
+#include <cstdlib>
+#include <cstring>
 
 namespace benor {
-
-constexpr uint32_t kBigMaxW = kMaxW;   // 64 chunks at N = 4096
-#ifndef BENOR_BIG_REG_WAVES
-// Waves per CU assumed for the workgroup-size choice.  The kernel takes 124-131
-// VGPRs (3 waves per SIMD), but choosing as if 2 per SIMD fit measured best
-// (12 or 16: -3..-20 % on N=2048..4096 shapes; profiles/r02_big_zero_start_ab.jsonl).
-#define BENOR_BIG_REG_WAVES 8
-#endif
-
-// Words per lane of a wave's x plane: the W x1 words rounded up to whole
-// Philox blocks per lane half (4 words each); the slice adds the KP <= W
-// proposal words (+1: a tile block may fill word KP when KP is odd).
-__host__ __device__ constexpr uint32_t big_plane_words(uint32_t W) { return 4u * ((((W + 1u) >> 1) + 1u) >> 1); }
-// The R-phase writes NT/2 proposal words per block of NT tiles, so up to
-// ceil(MT/NT) * NT/2 <= W + NT/2 - 1 words (MT = ceil(m/32) <= 2W).
-__host__ __device__ constexpr uint32_t big_prop_words(uint32_t W, uint32_t NT) { return W + NT / 2u - 1u; }
-// REGEN (round 1 of random initial values): no x plane in LDS, each tile block
-// regenerates its x words from Philox, so the slice is the proposal words only.
-__host__ __device__ constexpr uint32_t big_slice_words(uint32_t W, uint32_t NT, bool regen) {
-  return (regen ? 0u : big_plane_words(W)) + big_prop_words(W, NT);
-}
-// Receiver tiles per expanded operand: 8 from W = 28 on (more independent
-// accumulator chains and half the expansion VALU and LDS reads per product,
-// at 2 waves per SIMD), else 4 (3 waves per SIMD by registers).  Measured
-// (profiles/r02_big_nt_ab.jsonl): NT = 8 +20 % at N=4096 F=0 (W=64), +12 % at
-// N=2048 F=0 (W=32), +6 % at N=4096 F=2000 (W=33), -2 % at N=4096 F=1365
-// (W=43), -8 % at W=21..22.
-constexpr uint32_t kBigNt8MinW = 28;
-__host__ __device__ constexpr uint32_t big_nt(uint32_t W) { return W >= kBigNt8MinW ? 8u : 4u; }
-
-// x1 words of chunks 4j .. 4j+3 of this lane half (h) from /start Philox block
-// 2j + h: half h keeps words h and 2 + h of its block and trades the other two
-// with lane l ^ 32 (DS bpermute).
-__device__ __forceinline__ void big_x_block(const uint32_t *keys, uint64_t trial, uint32_t h, uint32_t j,
-                                            uint32_t (&xw)[4]) {
-  const uint2 kk = lds_keys(keys);
-  const uint4 r = philox4x32_10(kk.x, kk.y, make_uint4((uint32_t)trial, (uint32_t)(trial >> 32), 2u * j + h,
-                                                       kStreamInit << 24));
-  const uint32_t keep_a = h ? r.y : r.x, keep_b = h ? r.w : r.z;
-  const uint32_t give_a = h ? r.x : r.y, give_b = h ? r.z : r.w;
-  const uint32_t recv_a = (uint32_t)__shfl_xor((int)give_a, 32);
-  const uint32_t recv_b = (uint32_t)__shfl_xor((int)give_b, 32);
-  xw[0] = h ? recv_a : keep_a;
-  xw[1] = h ? recv_b : keep_b;
-  xw[2] = h ? keep_a : recv_a;
-  xw[3] = h ? keep_b : recv_b;
-}
 
 template <int KIND, int NT, int BW, bool REGEN>
 __global__ void __launch_bounds__(64 * BW) benor_mfma_big_kernel(KParams p) {
@@ -417,8 +373,25 @@ static hipError_t launch_big_nt(const KParams &p, int grid, hipStream_t s) {
   return big_nt(p.W) == 8u ? launch_big_bw<KIND, 8>(p, grid, s) : launch_big_bw<KIND, 4>(p, grid, s);
 }
 
+// The cooperative form (benor_mfma_coop.hip) from W = 22 on; below, the
+// per-wave form.  Measured (r03-s2b, profiles/r03-s2b_coop_ab.txt, node-rounds
+// per second, coop vs per-wave): N=4096 F=0 at 10^5 trials x1.69 (the
+// per-wave form's long group tail), 10^6 x1.17; N=4096 F=1365 (W=43) x1.06-1.10;
+// N=3000 F=1400 (W=25) x1.06; N=2048 F=682 (W=22) x1.09; N=1500 F=200 (W=21)
+// x1.01; N=2049 F=1024 (W=17, KIND 2) x0.93.  BENOR_BIG_FORM=wave / coop
+// overrides the choice.
+bool mfma_big_coop(const KParams &p) {
+  if (p.variant != 7 || p.W <= 16u || p.node_out || p.rounds_out) return false;
+  if (const char *ev = getenv("BENOR_BIG_FORM")) {
+    if (strcmp(ev, "wave") == 0) return false;
+    if (strcmp(ev, "coop") == 0) return true;
+  }
+  return p.W >= kCoopMinW;
+}
+
 hipError_t launch_mfma_big(const KParams &p, int grid, hipStream_t s) {
   if (p.W < 17u || p.W > kBigMaxW) return hipErrorInvalidValue;
+  if (mfma_big_coop(p)) return launch_mfma_coop(p, grid, s);
   if (p.G == 0u) return launch_big_nt<0>(p, grid, s);
   if (p.G == 1u) return launch_big_nt<1>(p, grid, s);
   return launch_big_nt<2>(p, grid, s);

@@ -469,8 +469,8 @@ static int plan_launch_impl(bo_plan *pl, uint64_t trial_begin, uint64_t trial_co
     // with the fewest waves and allocated for the one with the most.
     benor::KParams kc0 = kp;
     kc0.cont_round = 2u;
-    const uint64_t bw1 = benor::block_waves(kp), bw2 = benor::block_waves(kc0);
-    const uint64_t waves_min = (uint64_t)grid * std::min(bw1, bw2), waves = (uint64_t)grid * std::max(bw1, bw2);
+    const uint64_t u1 = benor::defer_units(kp, grid), u2 = benor::defer_units(kc0, grid);
+    const uint64_t waves_min = std::min(u1, u2), waves = std::max(u1, u2);
     const uint64_t seg_cap = ((cap + 31u) / 32u + waves_min - 1u) / waves_min * 32u;   // a wave's trials per launch, at most
     const uint64_t words = 2u * cap + 64u + waves * seg_cap;                           // two lists, their lengths, segments
     if (pl->defer_words < words) {

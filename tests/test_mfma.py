@@ -278,6 +278,35 @@ def test_mfma_big_matches_oracle(N, F):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("form", [("wave", None), ("coop", "4"), ("coop", "8")])
+@pytest.mark.parametrize("N,F", [(1100, 0), (2049, 1024), (2080, 1000), (3333, 1500), (4096, 1365), (4096, 0)])
+def test_mfma_big_forms_match_oracle(N, F, form):
+    """Both big-network forms -- per-wave (benor_mfma_big.hip) and
+    workgroup-cooperative with 4 or 8 waves (benor_mfma_coop.hip) -- forced by
+    environment on every KIND, round 1 and the continuation passes, against
+    the oracle (the default picks one form per W)."""
+    seed = (N * 7 + F) & 0xFFFF
+    T, begin = 700 + N % 37, (1 << 34) + F
+    keys = {"BENOR_BIG_FORM": form[0]}
+    if form[1]:
+        keys["BENOR_COOP_BW"] = form[1]
+    old = {k: os.environ.get(k) for k in keys}
+    os.environ.update(keys)
+    try:
+        p = plan(N, F, seed=seed, k_max=10)
+        assert p.kernel == benor.BO_KERNEL_MFMA
+        got = p.run(begin, T)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    ref = oracle.run_trials(N, F, first_f(N, F), seed=seed, trial_begin=begin, trial_count=T, k_max=10)
+    np.testing.assert_array_equal(got, ref.hist)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("N,F,T", [(2048, 0, 300_000), (4096, 1365, 200_001), (3000, 1400, 250_000), (1500, 200, 400_000)])
 def test_mfma_big_equals_popcount_kernels(N, F, T):
     a = plan(N, F, True, seed=17, k_max=16)
