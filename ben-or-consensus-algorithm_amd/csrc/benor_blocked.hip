@@ -289,10 +289,7 @@ __global__ void __launch_bounds__(256) benor_lockstep_blocked_kernel(KParams p) 
 
   if (hc) atomicAdd(&lhist[lane], hc);
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) {
-    const uint32_t c = lhist[i];
-    if (c) atomicAdd(&p.hist[i], (unsigned long long)c);
-  }
+  flush_hist(lhist, p);
 }
 
 template <int G>

@@ -181,6 +181,17 @@ __device__ __forceinline__ uint64_t coin_ballot(const uint32_t *keys, uint32_t t
   return coin_ballot(k.x, k.y, tlo, thi, group, round, tie);
 }
 
+// The workgroup's LDS histogram added to the launch histogram: hist itself, or
+// (p.hist_stride != 0) this workgroup's copy, blockIdx.x & 63 (benor_internal.h
+// kHistCopies).  Call after the __syncthreads that ends the counting.
+__device__ __forceinline__ void flush_hist(const uint32_t *lhist, const KParams &p) {
+  unsigned long long *dst = p.hist + (size_t)(blockIdx.x & (kHistCopies - 1u)) * p.hist_stride;
+  for (uint32_t i = threadIdx.x; i < p.hist_len; i += blockDim.x) {
+    const uint32_t c = lhist[i];
+    if (c) atomicAdd(&dst[i], (unsigned long long)c);
+  }
+}
+
 // ------------------------------------------- W-specialised kernel (m <= 1024)
 // For networks of at most 1024 live nodes (W <= 16 receiver groups) the whole
 // round is unrolled at compile time: every receiver group's tally chain is a

@@ -249,10 +249,7 @@ __global__ void __launch_bounds__(256) benor_lane_kernel(KParams p) {
   }
 
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < p.hist_len; i += blockDim.x) {
-    const uint32_t cnt = lhist[i];
-    if (cnt) atomicAdd(&p.hist[i], (unsigned long long)cnt);
-  }
+  flush_hist(lhist, p);
 }
 
 template <int MM, int KIND>

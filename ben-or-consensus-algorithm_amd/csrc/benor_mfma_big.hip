@@ -304,10 +304,7 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_big_kernel(KParams p) {
   if (hc) atomicAdd(&lhist[lane], hc);
   if (lane == 0 && f_2) atomicAdd(&lhist[hist_len - 1u], f_2);
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) {
-    const uint32_t c = lhist[i];
-    if (c) atomicAdd(&p.hist[i], (unsigned long long)c);
-  }
+  flush_hist(lhist, p);
 }
 
 // Round 1 of random initial values regenerates its x words from Philox (no x

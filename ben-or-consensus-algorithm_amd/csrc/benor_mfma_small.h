@@ -395,10 +395,7 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
     if (lane < 6u && c) atomicAdd(&lhist[3u * (lane / 2u + 1u) + (lane & 1u)], c);
   }
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) {
-    const uint32_t c = lhist[i];
-    if (c) atomicAdd(&p.hist[i], (unsigned long long)c);
-  }
+  flush_hist(lhist, p);
 }
 
 template <int MM>

@@ -334,10 +334,7 @@ __global__ void __launch_bounds__(256) benor_lockstep_w_kernel(KParams p) {
   if (hc) atomicAdd(&lhist[lane], hc);
   if (lane == 0 && f_2) atomicAdd(&lhist[hist_len - 1u], f_2);                     // disagreement counter
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) {
-    const uint32_t c = lhist[i];
-    if (c) atomicAdd(&p.hist[i], (unsigned long long)c);
-  }
+  flush_hist(lhist, p);
 }
 
 // The runtime's grid asks for 8 workgroups per CU whatever the occupancy;

@@ -20,6 +20,7 @@
 #                   ("new" = the in-tree library, X = ab/libbenor_X.so), twice, alternating
 #   abenv           as ab, one library, variants chosen by environment: AB_ENVS is a
 #                   space-separated list of name=VAR:value,VAR:value ("new=" = no variables)
+#   burstenv        as burst, once per AB_ENVS variant, twice, alternating
 #   burst           tools/burst_time.py over BURST_SHAPES (10 back-to-back launches per shape)
 #   c5              the C5 sweep (CSV compared with results/$C5_REF) and its per-N breakdown
 #   matrix          tools/perf_matrix.py over its built-in shape list
@@ -98,6 +99,17 @@ for step in "$@"; do
           env "${envs[@]}" timeout -k 10 300 python -u tools/perf_matrix.py --shapes "${AB_SHAPES:?AB_SHAPES}" 2>/dev/null \
             | sed "s/^{/{\"lib\": \"$name\", /" >> "$OUT/ab.jsonl"
           chk $? "abenv $name"
+        done
+      done;;
+    burstenv)
+      for rep in 1 2; do
+        for spec in ${AB_ENVS:?AB_ENVS}; do
+          name=${spec%%=*}; vars=${spec#*=}
+          envs=(); IFS=',' read -r -a kv <<< "$vars"
+          for x in "${kv[@]}"; do [ -n "$x" ] && envs+=("${x%%:*}=${x#*:}"); done
+          env "${envs[@]}" timeout -k 10 300 python -u tools/burst_time.py "${BURST_SHAPES:?BURST_SHAPES}" 2>/dev/null \
+            | sed "s/^{/{\"lib\": \"$name\", /" >> "$OUT/burst.jsonl"
+          chk $? "burstenv $name"
         done
       done;;
     burst)
