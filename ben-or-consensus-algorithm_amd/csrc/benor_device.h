@@ -181,14 +181,17 @@ __device__ __forceinline__ uint64_t coin_ballot(const uint32_t *keys, uint32_t t
   return coin_ballot(k.x, k.y, tlo, thi, group, round, tie);
 }
 
-// The workgroup's LDS histogram added to the launch histogram: hist itself, or
-// (p.hist_stride != 0) this workgroup's copy, blockIdx.x & 63 (benor_internal.h
-// kHistCopies).  Call after the __syncthreads that ends the counting.
+// The workgroup's LDS histogram added to the launch histogram (one global
+// atomic per non-zero bin; call after the __syncthreads that ends the
+// counting).  Global atomics on one cache line serialise across the grid, ~12
+// ns per workgroup when every workgroup flushes at once
+// (tools/atomic_flush_probe.hip, profiles/r03-s2d_atomic_flush_probe.jsonl); the
+// round-loop kernels' workgroups end at spread-out times, and 64 histogram
+// copies merged by a second kernel measured no faster for them.
 __device__ __forceinline__ void flush_hist(const uint32_t *lhist, const KParams &p) {
-  unsigned long long *dst = p.hist + (size_t)(blockIdx.x & (kHistCopies - 1u)) * p.hist_stride;
   for (uint32_t i = threadIdx.x; i < p.hist_len; i += blockDim.x) {
     const uint32_t c = lhist[i];
-    if (c) atomicAdd(&dst[i], (unsigned long long)c);
+    if (c) atomicAdd(&p.hist[i], (unsigned long long)c);
   }
 }
 

@@ -91,22 +91,8 @@ struct KParams {
   // round r of the trials trial_begin + trial_list[i], i < *trial_list_len,
   // which tied in every round before r (x = their round r-1 coins); 0: round 1
   uint32_t cont_round;
-  // histogram copies: 0 = every workgroup adds to hist[0 .. hist_len); else the
-  // launch adds to 64 copies hist_stride words apart (copy blockIdx.x & 63) and
-  // the host merges them into the caller's histogram afterwards (flush_hist)
-  uint32_t hist_stride;
 };
 
-// End-of-kernel histogram flush (flush_hist, benor_device.h): global atomics on
-// one cache line serialise across the grid, ~12 ns per workgroup
-// (tools/atomic_flush_probe.hip: 2048 workgroups 25.8 us, an empty kernel 2.6),
-// so launches of more than kDirectFlushMaxGrid workgroups add to kHistCopies
-// copies instead, merged by one small kernel (launch_hist_merge).
-constexpr uint32_t kHistCopies = 64;
-constexpr int kDirectFlushMaxGrid = 384;
-constexpr uint32_t hist_copy_stride(uint32_t hist_len) { return (hist_len + 15u) & ~15u; }   // 128-byte multiples
-hipError_t launch_hist_merge(unsigned long long *copies, uint32_t stride, uint32_t hist_len, unsigned long long *hist,
-                             hipStream_t stream);
 
 constexpr uint32_t kMfmaContRounds = 3;        // matrix-core passes up to round 3, then the popcount kernel
 
@@ -136,15 +122,6 @@ constexpr uint32_t kSmallMaxRound = 3;   // rounds on the matrix cores; a later 
 constexpr uint32_t small_wave_words(uint32_t m) { return 5u * 64u * small_slots(m) + 64u; }
 constexpr uint64_t kSmallMinTrials = 500000;    // shorter packed-shape launches run on the lane kernel
 bool small_on_lane(const KParams &p);
-// Item kernel (benor_lane_items.h): short batch launches of packed KIND-0
-// shapes with m <= kItemsMaxM, one (trial, round) per lane per item pass.
-constexpr uint32_t kItemsMaxM = 24;             // item word: x in 24 bits, round in 8
-constexpr uint32_t kItemsRing = 512;            // items per wave's LDS ring (uint2 each)
-constexpr uint64_t kItemsMaxTrials = 4000000;   // longer launches run the packed kernel
-bool small_on_items(const KParams &p);
-constexpr uint32_t items_lds_bytes(const KParams &p) { return p.hist_bytes + kWavesPerBlock * kItemsRing * 8u; }
-template <int MM>
-hipError_t launch_items_m(const KParams &p, int grid_blocks, hipStream_t stream);
 
 // Matrix-core kernel (benor_mfma.h), W = 2..16, instantiated in benor_mfma_*.hip;
 // W = 17..64 (m <= 4096): the big-network form, benor_mfma_big.hip.

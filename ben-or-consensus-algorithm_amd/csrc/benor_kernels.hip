@@ -858,13 +858,6 @@ static hipError_t dispatch_mfma_small(const KParams &p, int grid, hipStream_t s,
 }
 
 template <int... Is>
-static hipError_t dispatch_items(const KParams &p, int grid, hipStream_t s, std::integer_sequence<int, Is...>) {
-  hipError_t e = hipErrorInvalidValue;
-  (void)((p.m == (uint32_t)(Is + 2) ? (e = launch_items_m<Is + 2>(p, grid, s), true) : false) || ...);
-  return e;
-}
-
-template <int... Is>
 static hipError_t dispatch_mfma(const KParams &p, int grid, hipStream_t s, std::integer_sequence<int, Is...>) {
   hipError_t e = hipErrorInvalidValue;
   (void)((p.W == (uint32_t)(Is + 2) ? (e = launch_mfma<Is + 2>(p, grid, s), true) : false) || ...);
@@ -896,8 +889,6 @@ hipError_t launch_lockstep(const KParams &p, int grid, hipStream_t s) {
     return hipGetLastError();
   }
   if (p.variant == 6) return dispatch_lane(p, grid, s, std::make_integer_sequence<int, (int)kMaxLaneM>{});
-  if (p.variant == 8 && small_on_items(p))
-    return dispatch_items(p, grid, s, std::make_integer_sequence<int, (int)kItemsMaxM - 1>{});             // m = 2..24
   if (p.variant == 8 && !small_on_lane(p))
     return dispatch_mfma_small(p, grid, s, std::make_integer_sequence<int, (int)kMaxSmallMfmaM - 1>{});   // m = 2..32
   if (p.variant == 8) {                      // state launch or short launch of a packed shape: the lane kernel
@@ -948,24 +939,11 @@ uint64_t defer_units(const KParams &p, int grid) {
 // partial round lists at the end of each wave outweigh its per-trial gain
 // (DESIGN §4.2).
 // BENOR_SMALL_MIN_TRIALS overrides the crossover.
-// Short batch launches of packed KIND-0 shapes (m <= 24, k_max < 256) run
-// the item kernel (benor_lane_items.h); BENOR_SMALL_FORM=items / packed / lane
-// forces a form where it applies.
-bool small_on_items(const KParams &p) {
-  if (p.variant != 8 || p.node_out || p.rounds_out) return false;
-  if (p.base_G != 0u || p.m > kItemsMaxM || p.k_max > 255u || p.init_q != 0u) return false;
-  if (const char *ev = getenv("BENOR_SMALL_FORM")) {
-    if (strcmp(ev, "items") == 0) return true;
-    if (strcmp(ev, "packed") == 0 || strcmp(ev, "lane") == 0) return false;
-  }
-  return p.trial_count < kItemsMaxTrials;
-}
-
 bool small_on_lane(const KParams &p) {
   if (p.node_out || p.rounds_out) return true;
-  if (const char *ev = getenv("BENOR_SMALL_FORM")) {
+  if (const char *ev = getenv("BENOR_SMALL_FORM")) {   // A/B knob: packed / lane
     if (strcmp(ev, "lane") == 0) return true;
-    if (strcmp(ev, "packed") == 0 || strcmp(ev, "items") == 0) return false;
+    if (strcmp(ev, "packed") == 0) return false;
   }
   uint64_t min_trials = kSmallMinTrials;
   if (const char *ev = getenv("BENOR_SMALL_MIN_TRIALS")) min_trials = strtoull(ev, nullptr, 10);
@@ -980,18 +958,6 @@ int lockstep_grid(const KParams &p, int device) {
     uint64_t grid = p.ev_lanes / 256u;
     if (blocks_needed < grid) grid = blocks_needed;
     return (int)(grid < 1 ? 1 : grid);
-  }
-  if (p.variant == 8 && small_on_items(p)) {   // item kernel: up to 8 workgroups per CU, >= 1 trial per lane
-    const uint64_t need = (p.trial_count + 255u) / 256u;
-    uint64_t per_cu = lds_groups_per_cu(items_lds_bytes(p));
-    if (per_cu > 8u) per_cu = 8u;
-    if (const char *ev = getenv("BENOR_BLOCKS_PER_CU")) {   // tuning knob
-      const uint64_t v = strtoull(ev, nullptr, 10);
-      if (v >= 1u && v < per_cu) per_cu = v;
-    }
-    uint64_t grid = (uint64_t)cus * per_cu;
-    if (need < grid) grid = need;
-    return (int)(grid < 1u ? 1u : grid);
   }
   if (p.variant == 8) {
     if (small_on_lane(p)) {                  // state launch or short launch: the lane kernel
@@ -1062,39 +1028,6 @@ int lockstep_grid(const KParams &p, int device) {
   if (blocks_needed < grid) grid = blocks_needed;
   if (grid < 1) grid = 1;
   return (int)grid;
-}
-
-// Folds the kHistCopies histogram copies of a launch into the caller's
-// histogram and zeroes them for the next launch: wave w sums bins w, w + 16,
-// ... with lane c reading copy c (all loads of a wave issued before its
-// reductions).
-__global__ void __launch_bounds__(1024) hist_merge_kernel(unsigned long long *copies, uint32_t stride,
-                                                          uint32_t hist_len, unsigned long long *hist) {
-  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  constexpr uint32_t kWaves = 16, kBatch = 8;
-  for (uint32_t b0 = wv; b0 < hist_len; b0 += kWaves * kBatch) {
-    unsigned long long v[kBatch];
-#pragma unroll
-    for (uint32_t k = 0; k < kBatch; ++k) {
-      const uint32_t b = b0 + k * kWaves;
-      v[k] = b < hist_len ? copies[(size_t)lane * stride + b] : 0ull;
-    }
-#pragma unroll
-    for (uint32_t k = 0; k < kBatch; ++k) {
-      const uint32_t b = b0 + k * kWaves;
-      if (b < hist_len && v[k]) copies[(size_t)lane * stride + b] = 0ull;
-      unsigned long long t = v[k];
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o);
-      if (lane == 0 && b < hist_len && t) hist[b] += t;
-    }
-  }
-}
-
-hipError_t launch_hist_merge(unsigned long long *copies, uint32_t stride, uint32_t hist_len, unsigned long long *hist,
-                             hipStream_t s) {
-  hipLaunchKernelGGL(hist_merge_kernel, dim3(1), dim3(1024), 0, s, copies, stride, hist_len, hist);
-  return hipGetLastError();
 }
 
 hipError_t launch_popc_peak(uint32_t *sink, int grid, int iters, hipStream_t s, double *words) {

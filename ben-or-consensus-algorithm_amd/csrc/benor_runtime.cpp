@@ -86,7 +86,6 @@ struct bo_plan {
   uint32_t *d_scratch = nullptr;   // event mode
   uint32_t *d_defer = nullptr;     // matrix-core KIND > 0: deferred-trial list, its length, per-wave segments
   uint64_t defer_words = 0;
-  unsigned long long *d_hist_copies = nullptr;   // kHistCopies histogram copies of wide launches (zeroed)
   int device = 0;
 };
 
@@ -405,12 +404,6 @@ int bo_plan_create(const bo_trials_cfg *cfg, bo_plan **out) {
       kp.scratch = pl->d_scratch;
     }
   }
-  if (kp.m != 0u) {                          // histogram copies of wide launches (plan_launch_impl), zeroed
-    const size_t bytes = sizeof(unsigned long long) * benor::hist_copy_stride(kp.hist_len) * benor::kHistCopies;
-    hipError_t e = hipMalloc(&pl->d_hist_copies, bytes);
-    if (e == hipSuccess) e = hipMemset(pl->d_hist_copies, 0, bytes);
-    if (e != hipSuccess) { bo_plan_destroy(pl); return hip_fail(e, "histogram copies"); }
-  }
   *out = pl;
   return BO_OK;
 }
@@ -423,7 +416,6 @@ void bo_plan_destroy(bo_plan *pl) {
   if (pl->d_crash) (void)hipFree(pl->d_crash);
   if (pl->d_scratch) (void)hipFree(pl->d_scratch);
   if (pl->d_defer) (void)hipFree(pl->d_defer);
-  if (pl->d_hist_copies) (void)hipFree(pl->d_hist_copies);
   delete pl;
 }
 
@@ -447,49 +439,20 @@ uint64_t bo_plan_popc_words_per_node_round(const bo_plan *pl) {
   return counts * ((pl->kp.m + 31ull) / 32ull);
 }
 
-static int plan_launch_chain(bo_plan *pl, benor::KParams kp, uint64_t trial_begin, uint64_t trial_count,
-                             hipStream_t s);
-
-// Batch launches of more than kDirectFlushMaxGrid workgroups add their
-// histograms to the plan's kHistCopies copies (one cache line of atomics
-// serialises across the grid, ~12 ns per workgroup), folded into hist_dev by
-// one merge kernel after the launch chain; smaller ones add to hist_dev.
 static int plan_launch_impl(bo_plan *pl, uint64_t trial_begin, uint64_t trial_count, uint64_t *hist_dev,
                             bo_node_state *node_out, uint32_t *rounds_out, hipStream_t s) {
   if (trial_count == 0) return BO_OK;
   benor::KParams kp = pl->kp;
-  kp.hist_stride = 0u;
-  if (kp.m != 0u && !node_out && !rounds_out) {
-    benor::KParams probe = kp;
-    probe.trial_count = std::min<uint64_t>(trial_count, (kp.variant == 7 && kp.G > 0u) ? benor::kDeferChunk
-                                                                                        : benor::kMaxTrialsPerLaunch);
-    const char *ev = getenv("BENOR_HIST_DIRECT");   // A/B knob: every launch adds to hist_dev directly
-    if (pl->d_hist_copies && !(ev && ev[0] == '1') && benor::lockstep_grid(probe, pl->device) > benor::kDirectFlushMaxGrid) {
-      const uint32_t stride = benor::hist_copy_stride(kp.hist_len);
-      kp.hist_stride = stride;
-      kp.hist = pl->d_hist_copies;
-      const int rc = plan_launch_chain(pl, kp, trial_begin, trial_count, s);
-      if (rc != BO_OK) return rc;
-      HIP_TRY(benor::launch_hist_merge(pl->d_hist_copies, stride, kp.hist_len,
-                                       reinterpret_cast<unsigned long long *>(hist_dev), s));
-      return BO_OK;
-    }
+  if (kp.m == 0) {   // no live node: every trial lands in bin (0, 2)
+    hipLaunchKernelGGL(add_bin_kernel, dim3(1), dim3(64), 0, s,
+                       reinterpret_cast<unsigned long long *>(hist_dev), 2u, (unsigned long long)trial_count);
+    HIP_TRY(hipGetLastError());
+    return BO_OK;
   }
   kp.hist = reinterpret_cast<unsigned long long *>(hist_dev);
   kp.node_out = node_out;
   kp.rounds_out = rounds_out;
-  return plan_launch_chain(pl, kp, trial_begin, trial_count, s);
-}
-
-static int plan_launch_chain(bo_plan *pl, benor::KParams kp, uint64_t trial_begin, uint64_t trial_count,
-                             hipStream_t s) {
-  unsigned long long *const hist_dev = kp.hist;
-  if (kp.m == 0) {   // no live node: every trial lands in bin (0, 2)
-    hipLaunchKernelGGL(add_bin_kernel, dim3(1), dim3(64), 0, s, hist_dev, 2u, (unsigned long long)trial_count);
-    HIP_TRY(hipGetLastError());
-    return BO_OK;
-  }
-  if (kp.variant == 7 && kp.G > 0u && !kp.node_out && !kp.rounds_out) {
+  if (kp.variant == 7 && kp.G > 0u && !node_out && !rounds_out) {
     // Matrix-core round 1 with deferral (benor_mfma.h, KIND > 0): per chunk of
     // at most kDeferChunk trials, the matrix-core launch records the trials
     // that do not halt in round 1, and the W kernel runs exactly those from
