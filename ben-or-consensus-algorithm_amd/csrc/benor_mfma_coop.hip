@@ -272,8 +272,17 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_coop_kernel(KParams p) {
   flush_hist(lhist, p);
 }
 
+// Receiver tiles per block: big_nt(W) (BENOR_COOP_NT=4 / 8 overrides).
+static uint32_t coop_nt(const KParams &p) {
+  if (const char *ev = getenv("BENOR_COOP_NT")) {
+    const int v = atoi(ev);
+    if (v == 4 || v == 8) return (uint32_t)v;
+  }
+  return big_nt(p.W);
+}
+
 uint32_t mfma_coop_lds_bytes(const KParams &p) {
-  const uint32_t NT = big_nt(p.W);
+  const uint32_t NT = coop_nt(p);
   return p.hist_bytes + (big_plane_words(p.W) + big_prop_words(p.W, NT)) * 64u * 4u + 16u * 4u * 4u;
 }
 
@@ -301,7 +310,7 @@ static int coop_occupancy(const KParams &p) {
 }
 
 int mfma_coop_blocks_per_cu(const KParams &p) {
-  const bool nt8 = big_nt(p.W) == 8u, bw8 = mfma_coop_block_waves(p) == 8u;
+  const bool nt8 = coop_nt(p) == 8u, bw8 = mfma_coop_block_waves(p) == 8u;
   const uint32_t k = p.G;
   if (nt8) {
     if (bw8) return k == 0 ? coop_occupancy<0, 8, 8>(p) : k == 1 ? coop_occupancy<1, 8, 8>(p) : coop_occupancy<2, 8, 8>(p);
@@ -330,7 +339,7 @@ static hipError_t launch_coop_bw(const KParams &p, int grid, hipStream_t s) {
 
 template <int KIND>
 static hipError_t launch_coop_nt(const KParams &p, int grid, hipStream_t s) {
-  return big_nt(p.W) == 8u ? launch_coop_bw<KIND, 8>(p, grid, s) : launch_coop_bw<KIND, 4>(p, grid, s);
+  return coop_nt(p) == 8u ? launch_coop_bw<KIND, 8>(p, grid, s) : launch_coop_bw<KIND, 4>(p, grid, s);
 }
 
 hipError_t launch_mfma_coop(const KParams &p, int grid, hipStream_t s) {
