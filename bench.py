@@ -148,7 +148,12 @@ def launch_ranks(n, argv):
 # BASELINE configs[1] and [2] (one GPU): measured after the timed region and
 # reported beside the headline, not part of `value`.
 OTHER_CONFIGS = [("C2 N=10,F=4", 10, 4, 1_000_000), ("C2 N=10,F=5 (F>N/2, no decision)", 10, 5, 1_000_000),
-                 ("C3 N=256,F=85", 256, 85, 10_000_000)]
+                 ("C3 N=256,F=85", 256, 85, 10_000_000),
+                 # configs[4] (C5) cells at N = 4096 on the big-network matrix-core kernel
+                 # (workgroup-cooperative form): KIND 0 (m odd, one launch per plan launch)
+                 # and KIND 1 (m even: round 1, two continuation passes, the popcount
+                 # remainder -- the line times all of them)
+                 ("C5 cell N=4096,F=1365", 4096, 1365, 400_000), ("C5 cell N=4096,F=0", 4096, 0, 100_000)]
 OTHER_REPS = 10          # back-to-back launches per config, each of its T trials
 SS_REPS = 5              # back-to-back steady-state launches (20 T trials each)
 
@@ -217,6 +222,8 @@ def other_configs(benor, torch, k_max, seed):
         out[name] = {"trials": T, "launches_timed": OTHER_REPS, "kernel_ms": ms, "node_rounds_per_s": nr / (ms * 1e-3),
                      "trials_per_s": T / (ms * 1e-3), "mean_rounds": rounds / T, "undecided_trials": undecided,
                      "roofline": roof}
+        if plan.kernel == benor.BO_KERNEL_MFMA and not (m % 2 == 1 and m > 2 * F):   # KIND 1, 2: deferral chain
+            out[name]["kernels_per_launch"] = "matrix-core round 1 + continuation passes + popcount remainder"
         if ms < 1.0:
             # a launch this short is mostly ramp-up: also time 20x the trials for the
             # steady state, SS_REPS such launches back to back (amortising the events)

@@ -178,7 +178,7 @@ def reconcile(bench, durs):
                    if k != bk and "benor::" in k and "peak" not in k and v[0] > durs[bk][0])
     used = set()
     for name, oc in bench.get("other_configs", {}).items():
-        if "kernel_ms" not in oc:
+        if "kernel_ms" not in oc or "kernels_per_launch" in oc:   # several kernels per plan launch: no 1:1 match
             continue
         fam = family_symbol(oc.get("roofline", {}).get("kernel", ""))
         cand = [k for _, k in later if k not in used and (fam is None or fam in k)]
