@@ -31,17 +31,33 @@ XCDS = 8
 
 
 def last_dispatch(path):
-    """Counters of the last dispatch of the longest-named benor kernel in each pass
-    (perf_matrix runs a warm-up launch, then the timed one)."""
-    per, meta = {}, {}
+    """Counters of the timed launch's main kernel.  perf_matrix runs a warm-up
+    launch (a tenth of the trials, possibly on another kernel), then the timed
+    one, and a deferral shape's launch is several kernels (round 1, continuation
+    passes, popcount remainder).  Every pass replays the same dispatch sequence,
+    so the launch is chosen once, as the longest dispatch (GRBM_GUI_ACTIVE) of
+    the pass that counts it, and taken at the same position in every pass."""
+    passes = []
     for f in sorted(glob.glob(os.path.join(path, "p*", "*counter_collection.csv"))):
         rows = [r for r in csv.DictReader(open(f)) if "benor::" in r["Kernel_Name"] and "peak" not in r["Kernel_Name"]]
-        if not rows:
-            continue
-        last = max(int(r["Dispatch_Id"]) for r in rows)
+        if rows:
+            ids = sorted({int(r["Dispatch_Id"]) for r in rows})
+            passes.append((rows, ids))
+    pick = None
+    for rows, ids in passes:
+        dur = defaultdict(float)
+        for r in rows:
+            if r["Counter_Name"] == "GRBM_GUI_ACTIVE":
+                dur[int(r["Dispatch_Id"])] += float(r["Counter_Value"])
+        if dur:
+            pick = ids.index(max(dur, key=lambda i: (dur[i], i)))
+            break
+    per, meta = {}, {}
+    for rows, ids in passes:
+        want = ids[pick] if pick is not None and pick < len(ids) else ids[-1]
         agg = defaultdict(float)
         for r in rows:
-            if int(r["Dispatch_Id"]) == last:
+            if int(r["Dispatch_Id"]) == want:
                 agg[r["Counter_Name"]] += float(r["Counter_Value"])
                 meta = {k: r[k] for k in ("Kernel_Name", "Grid_Size", "Workgroup_Size", "LDS_Block_Size",
                                           "VGPR_Count", "Accum_VGPR_Count", "SGPR_Count", "Scratch_Size")}
@@ -92,7 +108,7 @@ def main(tag):
         if bench:
             lines += reconcile(bench, durs)
             lines += ["", f"- line `ms_per_step` {bench['ms_per_step']:.4f} ms; bench-kernel trace average over "
-                          f"every launch (stats CSV) {stats_avg(stats[0], bench_kernel(durs)):.4f} ms", ""]
+                          f"every launch (stats CSV) {stats_avg(stats[0], bench_kernel(durs, bench, bench['steps'])):.4f} ms", ""]
     for d in sorted(glob.glob(os.path.join(src, "pmc_*"))):
         c, meta = last_dispatch(d)
         shp = shape_of(d) or {}
@@ -147,7 +163,15 @@ def bench_args():
     return os.environ.get("BENCH_ARGS", "--steps 20 --warmup 5")
 
 
-def bench_kernel(durs):
+def bench_kernel(durs, bench=None, steps=None):
+    """The headline kernel: with the bench line, the kernel whose last `steps`
+    launches average closest to the line's kernel_ms (the clock-ramp shape run
+    before the warm-up can hold more total time); else the most total time."""
+    if bench and steps:
+        want = bench["roofline"]["kernel_ms"]
+        cand = [k for k in durs if "benor::" in k and len(durs[k][1]) >= steps]
+        if cand:
+            return min(cand, key=lambda k: abs(statistics.mean(durs[k][1][-steps:]) - want))
     return max(durs, key=lambda k: sum(durs[k][1]))
 
 
@@ -166,7 +190,7 @@ def reconcile(bench, durs):
     headline's launches, in dispatch order."""
     rows = []
     steps = bench["steps"]
-    bk = bench_kernel(durs)
+    bk = bench_kernel(durs, bench, steps)
     timed = durs[bk][1][-steps:]
     avg = statistics.mean(timed)
     rf = bench["roofline"]
