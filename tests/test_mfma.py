@@ -320,6 +320,24 @@ def test_mfma_big_equals_popcount_kernels(N, F, T):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("N,F", [(3000, 900), (4096, 1900)])
+def test_mfma_coop_two_chunks_equals_popcount_kernels(N, F):
+    """The cooperative big-network form over two deferral chunks (kDeferChunk =
+    2^22 trials) from a 64-bit trial_begin: per-workgroup deferral segments,
+    both continuation passes and the popcount remainder of each chunk give the
+    popcount kernels' histogram (KIND 1 at W = 33; KIND 2 at W = 35)."""
+    T, begin = (1 << 22) + 777, (1 << 33) + 5
+    a = plan(N, F, True, seed=41, k_max=12)
+    os.environ["BENOR_NO_MFMA_BIG"] = "1"
+    try:
+        b = benor.TrialsPlan(N, F, seed=41, k_max=12)
+    finally:
+        os.environ.pop("BENOR_NO_MFMA_BIG", None)
+    assert a.kernel == benor.BO_KERNEL_MFMA and b.kernel != benor.BO_KERNEL_MFMA
+    np.testing.assert_array_equal(a.run(begin, T), b.run(begin, T))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("N,F,q", [(2000, 600, 1), (4096, 1000, 2), (1500, 700, 3)])
 def test_mfma_big_fixed_init_matches_oracle(N, F, q):
     rng = np.random.default_rng(N + 7 * q)
