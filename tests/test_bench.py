@@ -87,6 +87,11 @@ def test_bench_single_gpu_line():
     assert oc["C2 N=10,F=4"]["undecided_trials"] == 0 and oc["C2 N=10,F=4"]["mean_rounds"] > 1.3
     assert oc["C2 N=10,F=5 (F>N/2, no decision)"]["undecided_trials"] == 1_000_000
     assert oc["C3 N=256,F=85"]["mean_rounds"] == 1.0 and oc["C3 N=256,F=85"]["node_rounds_per_s"] > 0
+    # configs[4] cells at N=4096 (cooperative big-network kernel): m odd halts in round 1;
+    # m even is a deferral chain per launch, timed as a whole
+    c5a, c5b = oc["C5 cell N=4096,F=1365"], oc["C5 cell N=4096,F=0"]
+    assert c5a["mean_rounds"] == 1.0 and "kernels_per_launch" not in c5a
+    assert c5b["kernels_per_launch"] and c5b["undecided_trials"] == 0 and 1.0 < c5b["mean_rounds"] < 1.05
     c1 = oc.pop("C1 N=5,F=1 network API")                 # configs[0]: one network, reference calls
     assert c1["reference_assertions_hold"] and 0 < c1["median_ms"] < 50
     for k, v in oc.items():
