@@ -408,12 +408,30 @@ __global__ void __launch_bounds__(256) benor_mfma_kernel(KParams p) {
     f_1 += (uint32_t)__builtin_popcount(any1);
     f_2 += (uint32_t)__builtin_popcount(any1 & any0);
   }
-  if (!SURE && n_def) {                        // this wave's deferred trials -> the compact list
-    __threadfence();
-    uint32_t base = 0u;
-    if (lane == 0) base = atomicAdd(p.defer_len, n_def);
-    base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
-    for (uint32_t i = lane; i < n_def; i += 64u) p.defer_list[base + i] = seg[i];
+  if constexpr (!SURE) {
+    // The waves' deferred trials -> the compact list, one global atomic per
+    // workgroup: atomics on one counter serialise across the grid (~12 ns
+    // each, tools/atomic_flush_probe.hip), and one per wave held KIND 1
+    // shapes back (N=256 F=0 -26 % at 8 workgroups per CU against 2;
+    // profiles/r03-s2n_mfma_blocks_per_cu_inproc.jsonl).  Parameter-block words
+    // 4..7 hold the waves' counts, then the workgroup's base.
+    uint32_t *wdef = keys + 4;
+    if (lane == 0) wdef[wv] = n_def;
+    __syncthreads();
+    uint32_t before = 0u, total = 0u;
+#pragma unroll
+    for (uint32_t w = 0; w < (uint32_t)kWavesPerBlock; ++w) {
+      const uint32_t c = wdef[w];
+      total += c;
+      before += w < wv ? c : 0u;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && total) wdef[0] = atomicAdd(p.defer_len, total);
+    __syncthreads();
+    if (n_def) {
+      const uint32_t base = wdef[0] + before;
+      for (uint32_t i = lane; i < n_def; i += 64u) p.defer_list[base + i] = seg[i];
+    }
   }
 
   // outcome bins 3R + v of the halting round R (1, or the continuation's round)

@@ -291,12 +291,26 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_big_kernel(KParams p) {
     f_1 += (uint32_t)__builtin_popcount(any1);
     f_2 += (uint32_t)__builtin_popcount(any1 & any0);
   }
-  if (KIND > 0 && n_def) {                     // this wave's deferred trials -> the compact list
-    __threadfence();
-    uint32_t base = 0u;
-    if (lane == 0) base = atomicAdd(p.defer_len, n_def);
-    base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
-    for (uint32_t i = lane; i < n_def; i += 64u) p.defer_list[base + i] = seg[i];
+  if constexpr (KIND > 0) {
+    // the waves' deferred trials -> the compact list, one global atomic per
+    // workgroup (as benor_mfma.h; parameter-block words 4..7, BW <= 4)
+    uint32_t *wdef = keys + 4;
+    if (lane == 0) wdef[wv] = n_def;
+    __syncthreads();
+    uint32_t before = 0u, total = 0u;
+#pragma unroll
+    for (uint32_t w = 0; w < (uint32_t)BW; ++w) {
+      const uint32_t c = wdef[w];
+      total += c;
+      before += w < wv ? c : 0u;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && total) wdef[0] = atomicAdd(p.defer_len, total);
+    __syncthreads();
+    if (n_def) {
+      const uint32_t base = wdef[0] + before;
+      for (uint32_t i = lane; i < n_def; i += 64u) p.defer_list[base + i] = seg[i];
+    }
   }
 
   const uint32_t rb = 3u * (cont ? cont : 1u);   // bins 3R + v of the halting round R

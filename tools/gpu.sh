@@ -20,6 +20,8 @@
 #                   ("new" = the in-tree library, X = ab/libbenor_X.so), twice, alternating
 #   abenv           as ab, one library, variants chosen by environment: AB_ENVS is a
 #                   space-separated list of name=VAR:value,VAR:value ("new=" = no variables)
+#   abin            tools/ab_inproc.py: AB_VARIANTS over AB_SHAPES ("N,F,trials;..."), interleaved
+#                   rounds in one process (median / min per variant)
 #   burstenv        as burst, once per AB_ENVS variant, twice, alternating
 #   burst           tools/burst_time.py over BURST_SHAPES (10 back-to-back launches per shape)
 #   c5              the C5 sweep (CSV compared with results/$C5_REF) and its per-N breakdown
@@ -101,6 +103,10 @@ for step in "$@"; do
           chk $? "abenv $name"
         done
       done;;
+    abin)
+      timeout -k 10 600 python -u tools/ab_inproc.py --variants "${AB_VARIANTS:?AB_VARIANTS}" --shapes "${AB_SHAPES:?AB_SHAPES}" \
+        ${AB_ARGS:-} > "$OUT/ab_inproc.jsonl" 2> "$OUT/ab_inproc.err"
+      chk $? abin; cat "$OUT/ab_inproc.jsonl";;
     burstenv)
       for rep in 1 2; do
         for spec in ${AB_ENVS:?AB_ENVS}; do
