@@ -461,18 +461,39 @@ static int plan_launch_impl(bo_plan *pl, uint64_t trial_begin, uint64_t trial_co
     const uint64_t cap = std::min<uint64_t>(trial_count, benor::kDeferChunk);
     kp.trial_count = cap;
     const int grid = benor::lockstep_grid(kp, pl->device);
-    // Every launch of the chunk (round 1 and the continuation passes) runs on
-    // `grid` workgroups, but the big-network form may pick a different
-    // workgroup size for the continuations (no x regeneration there, so a
-    // larger LDS slice: ADVICE r02).  A wave runs at most ceil(groups / waves)
-    // 32-trial groups of a launch, so the segments are sized for the launch
-    // with the fewest waves and allocated for the one with the most.
-    benor::KParams kc0 = kp;
-    kc0.cont_round = 2u;
-    const uint64_t u1 = benor::defer_units(kp, grid), u2 = benor::defer_units(kc0, grid);
-    const uint64_t waves_min = std::min(u1, u2), waves = std::max(u1, u2);
-    const uint64_t seg_cap = ((cap + 31u) / 32u + waves_min - 1u) / waves_min * 32u;   // a wave's trials per launch, at most
-    const uint64_t words = 2u * cap + 64u + waves * seg_cap;                           // two lists, their lengths, segments
+    // Continuation passes: a trial that tied in round 1 starts round 2 from its
+    // round-1 coins, so the matrix cores run rounds 2 .. kMfmaContRounds of the
+    // deferred trials too, each pass deferring its own ties; whatever is left
+    // goes to the popcount kernel, which re-runs it from round 1.
+    const uint32_t last_round = std::min<uint32_t>(benor::kMfmaContRounds, kp.k_max - 1u);
+    // KIND 1 lists hold a round's ties only (q(m) <= 10 % at m > 64), so pass r
+    // runs on grid >> 2(r - 1) workgroups: a full-size grid gives most waves a
+    // single group, and every workgroup that works pays its serialised
+    // deferral atomic and histogram flush (~12 ns each; N=256 F=0:
+    // round 2 took 31 us for ~5 us of products).  KIND 2 defers most trials,
+    // and the cooperative form's grid is already one workgroup per group.
+    const char *full_ev = getenv("BENOR_CONT_FULL_GRID");   // A/B knob: every pass on the round-1 grid
+    const bool shrink = kp.G == 1u && !benor::mfma_big_coop(kp) && !(full_ev && full_ev[0] == '1');
+    auto pass_grid = [&](uint32_t r) {
+      if (!shrink || r < 2u) return grid;
+      const int g = grid >> (2u * (r - 1u));
+      return std::max(g, std::min(grid, 64));
+    };
+    // Deferral segments: a launch of u owners (waves, or workgroups of the
+    // cooperative form) gives each at most ceil(groups / u) 32-trial groups,
+    // so its segments hold that many trials each; the region is sized for the
+    // largest u * cap over the chunk's launches (the per-launch cap is passed
+    // in KParams::defer_seg_cap).
+    const uint64_t groups = (cap + 31u) / 32u;
+    auto seg_cap_of = [&](uint64_t units) { return (groups + units - 1u) / units * 32u; };
+    uint64_t seg_words = 0;
+    for (uint32_t r = 1u; r <= std::max<uint32_t>(last_round, 1u); ++r) {
+      benor::KParams kr = kp;
+      kr.cont_round = r >= 2u ? r : 0u;
+      const uint64_t u = benor::defer_units(kr, pass_grid(r));
+      seg_words = std::max<uint64_t>(seg_words, u * seg_cap_of(u));
+    }
+    const uint64_t words = 2u * cap + 64u + seg_words;                  // two lists, three lengths, segments
     if (pl->defer_words < words) {
       if (pl->d_defer) (void)hipFree(pl->d_defer);
       pl->d_defer = nullptr;
@@ -480,44 +501,36 @@ static int plan_launch_impl(bo_plan *pl, uint64_t trial_begin, uint64_t trial_co
       HIP_TRY(hipMalloc(&pl->d_defer, sizeof(uint32_t) * words));
       pl->defer_words = words;
     }
-    uint32_t *const segs = pl->d_defer + cap + 64u;
-    // Continuation passes: a trial that tied in
-    // round 1 starts round 2 from its round-1 coins, so the matrix cores run
-    // rounds 2 .. kMfmaContRounds of the deferred trials too, each pass
-    // deferring its own ties (list ping-pong); whatever is left goes to the
-    // popcount kernel, which re-runs it from round 1.
-    const uint32_t last_round = std::min<uint32_t>(benor::kMfmaContRounds, kp.k_max - 1u);
+    uint32_t *const lens = pl->d_defer + cap;                           // pass r's output length: lens[16 (r - 1)]
+    uint32_t *const segs = lens + 64u;
+    uint32_t *const lists[2] = {pl->d_defer, segs + seg_words};         // pass r writes lists[(r - 1) & 1]
     for (uint64_t done = 0; done < trial_count;) {
       const uint64_t n = std::min<uint64_t>(trial_count - done, cap);
-      uint32_t *list = pl->d_defer, *len = pl->d_defer + cap;
-      uint32_t *list2 = segs + waves * seg_cap, *len2 = len + 32u;
-      HIP_TRY(hipMemsetAsync(len, 0, sizeof(uint32_t), s));
+      HIP_TRY(hipMemsetAsync(lens, 0, sizeof(uint32_t) * 48u, s));   // every pass's length, one fill
       kp.trial_begin = trial_begin + done;
       kp.trial_count = n;
-      kp.defer_list = list;
-      kp.defer_len = len;
       kp.defer_seg = segs;
-      kp.defer_seg_cap = (uint32_t)seg_cap;
-      kp.cont_round = 0u;
-      HIP_TRY(benor::launch_lockstep(kp, grid, s));
-      for (uint32_t r = 2u; r <= last_round; ++r) {
-        HIP_TRY(hipMemsetAsync(len2, 0, sizeof(uint32_t), s));
+      uint32_t r_last = 1u;
+      for (uint32_t r = 1u; r <= std::max<uint32_t>(last_round, 1u); ++r) {
         benor::KParams kc = kp;
-        kc.cont_round = r;
-        kc.trial_list = list;
-        kc.trial_list_len = len;
-        kc.defer_list = list2;
-        kc.defer_len = len2;
-        HIP_TRY(benor::launch_lockstep(kc, grid, s));
-        std::swap(list, list2);
-        std::swap(len, len2);
+        const int g = pass_grid(r);
+        kc.cont_round = r >= 2u ? r : 0u;
+        if (r >= 2u) {
+          kc.trial_list = lists[(r - 2u) & 1u];
+          kc.trial_list_len = lens + 16u * (r - 2u);
+        }
+        kc.defer_list = lists[(r - 1u) & 1u];
+        kc.defer_len = lens + 16u * (r - 1u);
+        kc.defer_seg_cap = (uint32_t)seg_cap_of(benor::defer_units(kc, g));
+        HIP_TRY(benor::launch_lockstep(kc, g, s));
+        r_last = r;
       }
       benor::KParams kw = kp;
       kw.variant = kp.base_variant;              // W kernel (W <= 32) or blocked kernel
       kw.G = kp.base_G;
       kw.defer_list = kw.defer_len = kw.defer_seg = nullptr;
-      kw.trial_list = list;
-      kw.trial_list_len = len;
+      kw.trial_list = lists[(r_last - 1u) & 1u];
+      kw.trial_list_len = lens + 16u * (r_last - 1u);
       HIP_TRY(benor::launch_lockstep(kw, benor::lockstep_grid(kw, pl->device), s));
       done += n;
     }
