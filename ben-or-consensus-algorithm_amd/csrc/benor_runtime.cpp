@@ -466,14 +466,17 @@ static int plan_launch_impl(bo_plan *pl, uint64_t trial_begin, uint64_t trial_co
     // deferred trials too, each pass deferring its own ties; whatever is left
     // goes to the popcount kernel, which re-runs it from round 1.
     const uint32_t last_round = std::min<uint32_t>(benor::kMfmaContRounds, kp.k_max - 1u);
-    // KIND 1 lists hold a round's ties only (q(m) <= 10 % at m > 64), so pass r
-    // runs on grid >> 2(r - 1) workgroups: a full-size grid gives most waves a
-    // single group, and every workgroup that works pays its serialised
+    // A pass's list holds the previous round's ties only: in lockstep every
+    // receiver hears the whole x plane, so a round without an R-phase tie
+    // makes every receiver propose and then decide the majority (m > F, KIND 1
+    // and 2 alike), and random starts tie with q(m) <= 10 % at m > 64.  So pass
+    // r runs on grid >> 2(r - 1) workgroups: a full-size grid gives most waves
+    // a single group, and every workgroup that works pays its serialised
     // deferral atomic and histogram flush (~12 ns each; N=256 F=0:
-    // round 2 took 31 us for ~5 us of products).  KIND 2 defers most trials,
-    // and the cooperative form's grid is already one workgroup per group.
+    // round 2 took 31 us for ~5 us of products).  The cooperative form's grid
+    // is already one workgroup per group.
     const char *full_ev = getenv("BENOR_CONT_FULL_GRID");   // A/B knob: every pass on the round-1 grid
-    const bool shrink = kp.G == 1u && !benor::mfma_big_coop(kp) && !(full_ev && full_ev[0] == '1');
+    const bool shrink = !benor::mfma_big_coop(kp) && !(full_ev && full_ev[0] == '1');
     auto pass_grid = [&](uint32_t r) {
       if (!shrink || r < 2u) return grid;
       const int g = grid >> (2u * (r - 1u));
