@@ -25,6 +25,7 @@
 #   burstenv        as burst, once per AB_ENVS variant, twice, alternating
 #   burst           tools/burst_time.py over BURST_SHAPES (10 back-to-back launches per shape)
 #   c5              the C5 sweep (CSV compared with results/$C5_REF) and its per-N breakdown
+#   c5phases        tools/c5_phases.py: the C5 sweep's wall time split (plans / queue / drain / read-back), twice
 #   matrix          tools/perf_matrix.py over its built-in shape list
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R" || exit 1
@@ -133,6 +134,9 @@ for step in "$@"; do
           --out "$C5/n$N.csv" 2> "$C5/n$N.json")
         chk $? "c5 N=$N"
       done;;
+    c5phases)
+      timeout -k 10 120 python -u tools/c5_phases.py > "$OUT/c5_phases.jsonl" 2> "$OUT/c5_phases.err"
+      chk $? c5phases; cat "$OUT/c5_phases.jsonl";;
     matrix)
       timeout -k 10 400 python -u tools/perf_matrix.py > "$OUT/perf_matrix.jsonl" 2>&1
       chk $? matrix;;
