@@ -113,18 +113,30 @@ def cmd_sweep(a) -> int:
         phis = [i * 0.5 / a.steps for i in range(a.steps)]
         cells = [(N, int(phi * N)) for N in Ns for phi in phis]
     per_cell = _int(str(a.per_cell)) if a.per_cell else max(1, _int(str(a.trials)) // len(cells))
+    # The device context comes up before the clock starts (~0.08 s on a fresh
+    # process): "seconds" times the sweep -- plans, launches, merge, read-back.
+    torch.zeros(1, device="cuda")
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     stream = torch.cuda.current_stream()
     # Every cell's plan first, then all launches back to back into one [cells, H]
-    # histogram buffer, then ONE all-reduce over ranks and one read-back.
+    # histogram buffer, then ONE all-reduce over ranks and one read-back.  Cells go
+    # round-robin over --streams streams: each plan owns its buffers, so cells are
+    # independent, and one cell's short passes (deferred-trial rounds, the last
+    # groups of a launch) overlap the next cell's launches instead of idling CUs.
     plans = [benor.TrialsPlan(N, F, seed=a.seed ^ (N << 20) ^ F, k_max=a.k_max) for (N, F) in cells]
     H = plans[0].hist_len
     hists = torch.zeros((len(cells), H), dtype=torch.int64, device="cuda")
+    streams = [stream] + [torch.cuda.Stream() for _ in range(max(1, a.streams) - 1)]
+    for s in streams[1:]:
+        s.wait_stream(stream)                      # the zeroed histograms
     b, n = strong_range(0, per_cell, rank, world)
     for ci, plan in enumerate(plans):
-        plan.launch(b, n, hists[ci].data_ptr(), stream.cuda_stream)
+        plan.launch(b, n, hists[ci].data_ptr(), streams[ci % len(streams)].cuda_stream)
         if rank == 0 and a.progress:
             print(f"[{ci + 1}/{len(cells)}] N={cells[ci][0]} F={cells[ci][1]} queued", file=sys.stderr, flush=True)
+    for s in streams[1:]:
+        stream.wait_stream(s)
     merge_histogram(hists)
     allh = hists.cpu().numpy().astype(np.uint64)
     rows = [summarize(allh[ci], N, F, a.k_max) for ci, (N, F) in enumerate(cells)]
@@ -166,6 +178,7 @@ def main(argv=None) -> int:
     w.add_argument("--k-max", type=int, default=32)
     w.add_argument("--cells", default=None, help="N:F,N:F,... instead of the N x phi grid")
     w.add_argument("--per-cell", default=None, help="trials per cell (default: --trials / cells)")
+    w.add_argument("--streams", type=int, default=4, help="HIP streams the cells are spread over")
     w.add_argument("--out", default=None)
     w.add_argument("--progress", action="store_true")
     a = ap.parse_args(argv)

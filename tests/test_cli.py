@@ -79,3 +79,20 @@ def test_sweep_two_ranks_equals_one(tmp_path):
     assert one.read_bytes() == two.read_bytes()
     rows = list(csv.DictReader(open(one)))
     assert len(rows) == 9 and all(int(r["trials"]) == 30_001 for r in rows)
+
+
+@pytest.mark.gpu
+def test_sweep_streams_equal_one_stream(tmp_path):
+    """Cells spread over several streams (the default) write the byte-identical
+    CSV of one stream: every plan owns its deferral buffers, so concurrent cells
+    (including deferral chains at N=1024 / 2112 / 4096) are independent."""
+    args = ["sweep", "--N", "64,1024,2112,4096", "--steps", "4", "--per-cell", str(3 * (1 << 20) + 17), "--k-max", "12"]
+    env = dict(os.environ, PYTHONPATH=PKG)
+    outs = []
+    for streams in (1, 4, 3):
+        out = tmp_path / f"s{streams}.csv"
+        subprocess.run([sys.executable, "-m", "benor.cli", *args, "--streams", str(streams), "--out", str(out)],
+                       check=True, env=env, cwd=PKG, timeout=120)
+        outs.append(out.read_bytes())
+    assert outs[0] == outs[1] == outs[2]
+    assert len(outs[0].splitlines()) == 1 + 16

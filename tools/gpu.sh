@@ -26,6 +26,7 @@
 #   burst           tools/burst_time.py over BURST_SHAPES (10 back-to-back launches per shape)
 #   c5              the C5 sweep (CSV compared with results/$C5_REF) and its per-N breakdown
 #   c5phases        tools/c5_phases.py: the C5 sweep's wall time split (plans / queue / drain / read-back), twice
+#   c5trace         the same under rocprofv3 --kernel-trace --stats
 #   matrix          tools/perf_matrix.py over its built-in shape list
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R" || exit 1
@@ -135,8 +136,12 @@ for step in "$@"; do
         chk $? "c5 N=$N"
       done;;
     c5phases)
-      timeout -k 10 120 python -u tools/c5_phases.py > "$OUT/c5_phases.jsonl" 2> "$OUT/c5_phases.err"
+      timeout -k 10 200 python -u tools/c5_phases.py ${C5P_ARGS:-} > "$OUT/c5_phases.jsonl" 2> "$OUT/c5_phases.err"
       chk $? c5phases; cat "$OUT/c5_phases.jsonl";;
+    c5trace)
+      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/c5trace" -o c5 -- \
+        python3 "$R/tools/c5_phases.py" > "$OUT/c5trace.log" 2>&1)
+      chk $? c5trace;;
     matrix)
       timeout -k 10 400 python -u tools/perf_matrix.py > "$OUT/perf_matrix.jsonl" 2>&1
       chk $? matrix;;
