@@ -36,7 +36,10 @@
 
 namespace benor {
 
-template <int KIND, int NT, int BW>
+// CB: each tile's first product takes the phase's bias as its C operand (no
+// accumulator zeroing, no bias add per result) -- in the P-phase for blocks
+// without the last tile, whose dead rows need NaN.
+template <int KIND, int NT, int BW, bool CB>
 __global__ void __launch_bounds__(64 * BW) benor_mfma_coop_kernel(KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t lane = threadIdx.x & 63u, h = lane >> 5;
@@ -82,6 +85,9 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_coop_kernel(KParams p) {
   const uint32_t last_mask = last_bits >= 32 ? ~0u : (last_bits <= 0 ? 0u : ((1u << last_bits) - 1u));
 
   mf_v4i ones = {0x22222222, 0x22222222, 0x22222222, 0x22222222};
+  mf_v16f cb_r, cb_p;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) cb_r[j] = bias_r, cb_p[j] = bias_p;
   uint32_t f_all = 0, f_1 = 0, f_2 = 0;        // wave 0's counters
   const uint32_t ngroups = (trial_count + 31u) >> 5;
   uint32_t n_def = 0;
@@ -127,10 +133,23 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_coop_kernel(KParams p) {
     for (uint32_t b = wv; b < NB; b += BW) {
       const uint32_t i = b * (uint32_t)NT;
       mf_v16f acc[NT];
-#pragma unroll
-      for (int u = 0; u < NT; ++u) acc[u] = mf_v16f{};
       uint32_t wcur = X[lane];                 // chunk c + 1's word read among chunk c's products
-      for (uint32_t c = 0; c < W; ++c) {
+      uint32_t c0 = 0;
+      if constexpr (CB) {                      // chunk 0 with C = the bias (W >= 17)
+        const uint32_t wnext = X[64u + lane];
+        const mf_v4i bx = expand_votes(wcur);
+#pragma unroll
+        for (int u = 0; u < NT; ++u) {
+          asm volatile("" : "+v"(ones));
+          acc[u] = mfma_count<4>(ones, bx, cb_r);
+        }
+        wcur = wnext;
+        c0 = 1;
+      } else {
+#pragma unroll
+        for (int u = 0; u < NT; ++u) acc[u] = mf_v16f{};
+      }
+      for (uint32_t c = c0; c < W; ++c) {
         const uint32_t wnext = X[(c + 1u < W ? c + 1u : c) * 64u + lane];
         const mf_v4i bx = expand_votes(wcur);
 #pragma unroll
@@ -143,10 +162,12 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_coop_kernel(KParams p) {
         for (int k = 0; k < NT; ++k) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
         wcur = wnext;
       }
+      if constexpr (!CB) {
 #pragma unroll
-      for (int u = 0; u < NT; ++u)
+        for (int u = 0; u < NT; ++u)
 #pragma unroll
-        for (int j = 0; j < 16; ++j) acc[u][j] += bias_r;
+          for (int j = 0; j < 16; ++j) acc[u][j] += bias_r;
+      }
 #pragma unroll
       for (int q = 0; q < NT / 2; ++q) {      // tile pair (i + 2q, i + 2q + 1) -> proposal word (i >> 1) + q
         uint32_t n[4];
@@ -172,11 +193,25 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_coop_kernel(KParams p) {
     for (uint32_t b = wv; b < NB; b += BW) {
       const uint32_t i = b * (uint32_t)NT;
       const float nanf = __builtin_nanf("");
+      const bool cbb = CB && i + (uint32_t)NT < MT;   // every tile of the block has 32 live rows
       mf_v16f acc[NT];
-#pragma unroll
-      for (int u = 0; u < NT; ++u) acc[u] = mf_v16f{};
       uint32_t wcur = PL[lane];
-      for (uint32_t k = 0; k < KP; ++k) {
+      uint32_t k0 = 0;
+      if (cbb) {                               // chunk 0 with C = the bias (KP >= 17)
+        const uint32_t wnext = PL[64u + lane];
+        const mf_v4i bp = expand_votes(wcur);
+#pragma unroll
+        for (int u = 0; u < NT; ++u) {
+          asm volatile("" : "+v"(ones));
+          acc[u] = KIND == 2 ? mfma_count<1>(ones, bp, cb_p) : mfma_count(ones, bp, cb_p);
+        }
+        wcur = wnext;
+        k0 = 1;
+      } else {
+#pragma unroll
+        for (int u = 0; u < NT; ++u) acc[u] = mf_v16f{};
+      }
+      for (uint32_t k = k0; k < KP; ++k) {
         const uint32_t wnext = PL[(k + 1u < KP ? k + 1u : k) * 64u + lane];
         const mf_v4i bp = expand_votes(wcur);
 #pragma unroll
@@ -192,7 +227,8 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_coop_kernel(KParams p) {
 #pragma unroll
       for (int u = 0; u < NT; ++u) {
         const uint32_t ti = i + u;
-        if (ti + 1u < MT) {
+        if (cbb) {
+        } else if (ti + 1u < MT) {
 #pragma unroll
           for (int j = 0; j < 16; ++j) acc[u][j] += bias_p;
         } else {                               // rows with no receiver become NaN: the reductions skip them
@@ -301,7 +337,7 @@ uint32_t mfma_coop_block_waves(const KParams &p) {
 template <int KIND, int NT, int BW>
 static int coop_occupancy(const KParams &p) {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void *>(&benor_mfma_coop_kernel<KIND, NT, BW>),
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void *>(&benor_mfma_coop_kernel<KIND, NT, BW, true>),
                                                    64 * BW, mfma_coop_lds_bytes(p)) != hipSuccess)
     n = 1;
   const int lds_fit = (int)lds_groups_per_cu(mfma_coop_lds_bytes(p));
@@ -320,16 +356,24 @@ int mfma_coop_blocks_per_cu(const KParams &p) {
   return k == 0 ? coop_occupancy<0, 4, 4>(p) : k == 1 ? coop_occupancy<1, 4, 4>(p) : coop_occupancy<2, 4, 4>(p);
 }
 
-template <int KIND, int NT, int BW>
-static hipError_t launch_coop(const KParams &p, int grid, hipStream_t s) {
+template <int KIND, int NT, int BW, bool CB>
+static hipError_t launch_coop_cb(const KParams &p, int grid, hipStream_t s) {
   const uint32_t lds = mfma_coop_lds_bytes(p);
   if (lds > 64u * 1024u) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&benor_mfma_coop_kernel<KIND, NT, BW>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&benor_mfma_coop_kernel<KIND, NT, BW, CB>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((benor_mfma_coop_kernel<KIND, NT, BW>), dim3(grid), dim3(64 * BW), lds, s, p);
+  hipLaunchKernelGGL((benor_mfma_coop_kernel<KIND, NT, BW, CB>), dim3(grid), dim3(64 * BW), lds, s, p);
   return hipGetLastError();
+}
+
+// BENOR_COOP_CBIAS=0: accumulators zeroed and the bias added per result (A/B).
+template <int KIND, int NT, int BW>
+static hipError_t launch_coop(const KParams &p, int grid, hipStream_t s) {
+  const char *ev = getenv("BENOR_COOP_CBIAS");
+  if (ev && ev[0] == '0') return launch_coop_cb<KIND, NT, BW, false>(p, grid, s);
+  return launch_coop_cb<KIND, NT, BW, true>(p, grid, s);
 }
 
 template <int KIND, int NT>
