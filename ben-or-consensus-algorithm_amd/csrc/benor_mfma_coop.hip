@@ -33,14 +33,24 @@
 #include "benor_mfma_big.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace benor {
+
+// The x and proposal words as product operands: EXP planes hold them expanded
+// (the four e2m1 dwords of expand_votes), so a block's chunk costs one
+// ds_read_b128 instead of a ds_read_b32 and the expansion, which every one of
+// the MT / NT tile blocks would repeat.
+__device__ __forceinline__ mf_v4i as_votes(uint32_t w) { return expand_votes(w); }
+__device__ __forceinline__ mf_v4i as_votes(mf_v4i v) { return v; }
 
 // CB: each tile's first product takes the phase's bias as its C operand (no
 // accumulator zeroing, no bias add per result) -- in the P-phase for blocks
 // without the last tile, whose dead rows need NaN.
-template <int KIND, int NT, int BW, bool CB>
+template <int KIND, int NT, int BW, bool CB, bool EXP>
 __global__ void __launch_bounds__(64 * BW) benor_mfma_coop_kernel(KParams p) {
+  using XW = std::conditional_t<EXP, mf_v4i, uint32_t>;
+  constexpr uint32_t XS = EXP ? 4u : 1u;      // dwords per plane word
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t lane = threadIdx.x & 63u, h = lane >> 5;
   const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -55,8 +65,14 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_coop_kernel(KParams p) {
   uint32_t *lhist = reinterpret_cast<uint32_t *>(smem);
   uint32_t *keys = reinterpret_cast<uint32_t *>(smem + p.hist_bytes - kParamBytes);
   uint32_t *X = reinterpret_cast<uint32_t *>(smem + p.hist_bytes);   // [big_plane_words(W)][64]
-  uint32_t *PL = X + big_plane_words(W) * 64u;                        // [big_prop_words(W, NT)][64]
-  uint32_t *RED = PL + big_prop_words(W, NT) * 64u;                   // [BW][4] column masks
+  uint32_t *PL = X + big_plane_words(W) * 64u * XS;                   // [big_prop_words(W, NT)][64]
+  uint32_t *RED = PL + big_prop_words(W, NT) * 64u * XS;              // [BW][4] column masks
+  XW *const XR = reinterpret_cast<XW *>(X);
+  XW *const PR = reinterpret_cast<XW *>(PL);
+  auto put = [&](XW *plane, uint32_t c, uint32_t w) {   // word c of this lane
+    if constexpr (EXP) plane[c * 64u + lane] = expand_votes(w);
+    else plane[c * 64u + lane] = w;
+  };
   for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) lhist[i] = 0u;
   if (threadIdx.x == 0) {
     keys[0] = (uint32_t)p.seed;
@@ -104,7 +120,7 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_coop_kernel(KParams p) {
         const uint2 kk = lds_keys(keys);
         const uint4 r = coin_block(kk.x, kk.y, (uint32_t)trial, (uint32_t)(trial >> 32), 32u * (2u * c + h), cont - 1u);
         const uint32_t w = coin_word(r, cont - 1u);
-        X[c * 64u + lane] = c == W - 1u ? w & last_mask : w;
+        put(XR, c, c == W - 1u ? w & last_mask : w);
       }
     } else if (random_init) {                  // whole Philox blocks, the halves trading words
       const uint64_t trial = lds_u64(keys + 2) + t;
@@ -115,14 +131,14 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_coop_kernel(KParams p) {
 #pragma unroll
         for (uint32_t q = 0; q < 4u; ++q) {
           const uint32_t c = 4u * j + q;
-          X[c * 64u + lane] = c == W - 1u ? xw[q] & last_mask : xw[q];
+          put(XR, c, c == W - 1u ? xw[q] & last_mask : xw[q]);
         }
       }
     } else {
       for (uint32_t c = wv; c < W; c += BW) {
         const uint4 q = p.init_plane[c];
         const uint32_t w = h ? q.w : q.z;
-        X[c * 64u + lane] = c == W - 1u ? w & last_mask : w;
+        put(XR, c, c == W - 1u ? w & last_mask : w);
       }
     }
     __syncthreads();
@@ -133,11 +149,11 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_coop_kernel(KParams p) {
     for (uint32_t b = wv; b < NB; b += BW) {
       const uint32_t i = b * (uint32_t)NT;
       mf_v16f acc[NT];
-      uint32_t wcur = X[lane];                 // chunk c + 1's word read among chunk c's products
+      XW wcur = XR[lane];                      // chunk c + 1's word read among chunk c's products
       uint32_t c0 = 0;
       if constexpr (CB) {                      // chunk 0 with C = the bias (W >= 17)
-        const uint32_t wnext = X[64u + lane];
-        const mf_v4i bx = expand_votes(wcur);
+        const XW wnext = XR[64u + lane];
+        const mf_v4i bx = as_votes(wcur);
 #pragma unroll
         for (int u = 0; u < NT; ++u) {
           asm volatile("" : "+v"(ones));
@@ -150,8 +166,8 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_coop_kernel(KParams p) {
         for (int u = 0; u < NT; ++u) acc[u] = mf_v16f{};
       }
       for (uint32_t c = c0; c < W; ++c) {
-        const uint32_t wnext = X[(c + 1u < W ? c + 1u : c) * 64u + lane];
-        const mf_v4i bx = expand_votes(wcur);
+        const XW wnext = XR[(c + 1u < W ? c + 1u : c) * 64u + lane];
+        const mf_v4i bx = as_votes(wcur);
 #pragma unroll
         for (int u = 0; u < NT; ++u) {
           asm volatile("" : "+v"(ones));       // opaque per tile: no two tiles' products merge
@@ -182,7 +198,7 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_coop_kernel(KParams p) {
             qz |= (~n[2 * v] & k0 & 0x22222222u) | (~n[2 * v + 1] & k1 & 0x22222222u);
         }
         const uint32_t s = 0x88888888u;
-        PL[((i >> 1) + q) * 64u + lane] = (n[0] & s) | ((n[1] & s) >> 1) | ((n[2] & s) >> 2) | ((n[3] & s) >> 3);
+        put(PR, (i >> 1) + q, (n[0] & s) | ((n[1] & s) >> 1) | ((n[2] & s) >> 2) | ((n[3] & s) >> 3));
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -195,11 +211,11 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_coop_kernel(KParams p) {
       const float nanf = __builtin_nanf("");
       const bool cbb = CB && i + (uint32_t)NT < MT;   // every tile of the block has 32 live rows
       mf_v16f acc[NT];
-      uint32_t wcur = PL[lane];
+      XW wcur = PR[lane];
       uint32_t k0 = 0;
       if (cbb) {                               // chunk 0 with C = the bias (KP >= 17)
-        const uint32_t wnext = PL[64u + lane];
-        const mf_v4i bp = expand_votes(wcur);
+        const XW wnext = PR[64u + lane];
+        const mf_v4i bp = as_votes(wcur);
 #pragma unroll
         for (int u = 0; u < NT; ++u) {
           asm volatile("" : "+v"(ones));
@@ -212,8 +228,8 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_coop_kernel(KParams p) {
         for (int u = 0; u < NT; ++u) acc[u] = mf_v16f{};
       }
       for (uint32_t k = k0; k < KP; ++k) {
-        const uint32_t wnext = PL[(k + 1u < KP ? k + 1u : k) * 64u + lane];
-        const mf_v4i bp = expand_votes(wcur);
+        const XW wnext = PR[(k + 1u < KP ? k + 1u : k) * 64u + lane];
+        const mf_v4i bp = as_votes(wcur);
 #pragma unroll
         for (int u = 0; u < NT; ++u) {
           asm volatile("" : "+v"(ones));
@@ -317,10 +333,27 @@ static uint32_t coop_nt(const KParams &p) {
   return big_nt(p.W);
 }
 
-uint32_t mfma_coop_lds_bytes(const KParams &p) {
+static uint32_t coop_lds_bytes(const KParams &p, bool exp) {
   const uint32_t NT = coop_nt(p);
-  return p.hist_bytes + (big_plane_words(p.W) + big_prop_words(p.W, NT)) * 64u * 4u + 16u * 4u * 4u;
+  return p.hist_bytes + (big_plane_words(p.W) + big_prop_words(p.W, NT)) * 64u * 4u * (exp ? 4u : 1u) + 16u * 4u * 4u;
 }
+
+// Expanded planes with four-tile blocks (W = 22..27), where one expansion
+// serves only four products: x1.04 at N=1600 F=100, N=1700 F=300 and N=2048
+// F=682; eight-tile blocks (W >= 28) measured within -2..+1 % either way, so
+// they keep the packed words (profiles/r03-s3k_coop_exp_inproc.jsonl).
+// BENOR_COOP_EXP=0 / 1 overrides (1: whenever the planes fit one
+// workgroup's LDS, W = 64: 132 KB).
+static bool coop_exp(const KParams &p) {
+  const bool fits = coop_lds_bytes(p, true) <= 160u * 1024u;
+  if (const char *ev = getenv("BENOR_COOP_EXP")) {
+    if (ev[0] == '0') return false;
+    if (ev[0] == '1') return fits;
+  }
+  return fits && coop_nt(p) == 4u;
+}
+
+uint32_t mfma_coop_lds_bytes(const KParams &p) { return coop_lds_bytes(p, coop_exp(p)); }
 
 // Waves per workgroup: 8 with eight-tile blocks (W >= 28: N=4096 F=1365 x1.04
 // over 4 waves, F=0 equal), else 4 (W = 22..27: 8 waves x0.85-0.86, their
@@ -337,8 +370,9 @@ uint32_t mfma_coop_block_waves(const KParams &p) {
 template <int KIND, int NT, int BW>
 static int coop_occupancy(const KParams &p) {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void *>(&benor_mfma_coop_kernel<KIND, NT, BW, true>),
-                                                   64 * BW, mfma_coop_lds_bytes(p)) != hipSuccess)
+  const void *fn = coop_exp(p) ? reinterpret_cast<const void *>(&benor_mfma_coop_kernel<KIND, NT, BW, true, true>)
+                               : reinterpret_cast<const void *>(&benor_mfma_coop_kernel<KIND, NT, BW, true, false>);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, 64 * BW, mfma_coop_lds_bytes(p)) != hipSuccess)
     n = 1;
   const int lds_fit = (int)lds_groups_per_cu(mfma_coop_lds_bytes(p));
   if (n > lds_fit) n = lds_fit;
@@ -356,15 +390,15 @@ int mfma_coop_blocks_per_cu(const KParams &p) {
   return k == 0 ? coop_occupancy<0, 4, 4>(p) : k == 1 ? coop_occupancy<1, 4, 4>(p) : coop_occupancy<2, 4, 4>(p);
 }
 
-template <int KIND, int NT, int BW, bool CB>
+template <int KIND, int NT, int BW, bool CB, bool EXP>
 static hipError_t launch_coop_cb(const KParams &p, int grid, hipStream_t s) {
-  const uint32_t lds = mfma_coop_lds_bytes(p);
+  const uint32_t lds = coop_lds_bytes(p, EXP);
   if (lds > 64u * 1024u) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&benor_mfma_coop_kernel<KIND, NT, BW, CB>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&benor_mfma_coop_kernel<KIND, NT, BW, CB, EXP>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((benor_mfma_coop_kernel<KIND, NT, BW, CB>), dim3(grid), dim3(64 * BW), lds, s, p);
+  hipLaunchKernelGGL((benor_mfma_coop_kernel<KIND, NT, BW, CB, EXP>), dim3(grid), dim3(64 * BW), lds, s, p);
   return hipGetLastError();
 }
 
@@ -372,8 +406,9 @@ static hipError_t launch_coop_cb(const KParams &p, int grid, hipStream_t s) {
 template <int KIND, int NT, int BW>
 static hipError_t launch_coop(const KParams &p, int grid, hipStream_t s) {
   const char *ev = getenv("BENOR_COOP_CBIAS");
-  if (ev && ev[0] == '0') return launch_coop_cb<KIND, NT, BW, false>(p, grid, s);
-  return launch_coop_cb<KIND, NT, BW, true>(p, grid, s);
+  const bool cb = !(ev && ev[0] == '0');
+  if (coop_exp(p)) return cb ? launch_coop_cb<KIND, NT, BW, true, true>(p, grid, s) : launch_coop_cb<KIND, NT, BW, false, true>(p, grid, s);
+  return cb ? launch_coop_cb<KIND, NT, BW, true, false>(p, grid, s) : launch_coop_cb<KIND, NT, BW, false, false>(p, grid, s);
 }
 
 template <int KIND, int NT>
