@@ -47,7 +47,10 @@ __device__ __forceinline__ mf_v4i as_votes(mf_v4i v) { return v; }
 // CB: each tile's first product takes the phase's bias as its C operand (no
 // accumulator zeroing, no bias add per result) -- in the P-phase for blocks
 // without the last tile, whose dead rows need NaN.
-template <int KIND, int NT, int BW, bool CB, bool EXP>
+// PF: the next group's /start words are written right after this group's
+// P-phase products (X is free once the R-phase barrier has passed), so the
+// P-phase barrier also publishes them and a group needs two barriers, not three.
+template <int KIND, int NT, int BW, bool CB, bool EXP, bool PF>
 __global__ void __launch_bounds__(64 * BW) benor_mfma_coop_kernel(KParams p) {
   using XW = std::conditional_t<EXP, mf_v4i, uint32_t>;
   constexpr uint32_t XS = EXP ? 4u : 1u;      // dwords per plane word
@@ -108,12 +111,11 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_coop_kernel(KParams p) {
   const uint32_t ngroups = (trial_count + 31u) >> 5;
   uint32_t n_def = 0;
   uint32_t *seg = KIND == 0 ? nullptr : p.defer_seg + (size_t)blockIdx.x * p.defer_seg_cap;
-  for (uint32_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
+  // ---- /start (node.ts:167-188): x1 words 2c + h of group g's trials, the
+  // chunks split over the waves
+  auto start_x = [&](uint32_t g) {
     const uint32_t t = (g << 5) + (lane & 31u);
-    const bool valid = t < trial_count;
-    const uint32_t toff = cont ? (valid ? p.trial_list[t] : 0u) : t;   // the trial's offset in the launch
-    // ---- /start (node.ts:167-188): x1 words 2c + h of this lane's trial, the
-    // chunks split over the waves
+    const uint32_t toff = cont ? (t < trial_count ? p.trial_list[t] : 0u) : t;
     if (KIND != 0 && cont != 0u) {             // continuation: the coins of round cont-1
       const uint64_t trial = lds_u64(keys + 2) + toff;
       for (uint32_t c = wv; c < W; c += BW) {
@@ -141,7 +143,19 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_coop_kernel(KParams p) {
         put(XR, c, c == W - 1u ? w & last_mask : w);
       }
     }
+  };
+  if constexpr (PF) {
+    if (blockIdx.x < ngroups) start_x(blockIdx.x);
     __syncthreads();
+  }
+  for (uint32_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    const uint32_t t = (g << 5) + (lane & 31u);
+    const bool valid = t < trial_count;
+    const uint32_t toff = cont ? (valid ? p.trial_list[t] : 0u) : t;   // the trial's offset in the launch
+    if constexpr (!PF) {
+      start_x(g);
+      __syncthreads();
+    }
 
     // ---- R-phase: this wave's tile blocks; proposals to LDS as sign bits
     // (1 = proposal 0), packed as in benor_mfma_big.hip
@@ -263,6 +277,9 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_coop_kernel(KParams p) {
       }
       __builtin_amdgcn_sched_barrier(0);
     }
+    if constexpr (PF) {
+      if (g + gridDim.x < ngroups) start_x(g + gridDim.x);
+    }
     // this wave's columns: some receiver decided 1 / 0 (KIND 0, 1, 2: acc < 0
     // <=> decided 1), a "?" proposal or an undecided receiver (defer)
     {
@@ -303,9 +320,9 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_coop_kernel(KParams p) {
       f_2 += (uint32_t)__builtin_popcount(any1 & any0);
     }
     // No barrier here: the next group's /start writes only X (read before the
-    // R-phase barrier), its R-phase writes PL after the next /start barrier
-    // (every wave has finished this P-phase: it passed the barrier above), and
-    // RED is rewritten only after two more barriers that wave 0 must reach.
+    // R-phase barrier), its R-phase writes PL after the barrier above (every
+    // wave has finished this P-phase), and RED is rewritten only after the
+    // next R-phase barrier, which wave 0 must reach.
   }
   if (wv == 0u) {
     if (KIND > 0 && n_def) {                   // this workgroup's deferred trials -> the compact list
@@ -370,8 +387,8 @@ uint32_t mfma_coop_block_waves(const KParams &p) {
 template <int KIND, int NT, int BW>
 static int coop_occupancy(const KParams &p) {
   int n = 0;
-  const void *fn = coop_exp(p) ? reinterpret_cast<const void *>(&benor_mfma_coop_kernel<KIND, NT, BW, true, true>)
-                               : reinterpret_cast<const void *>(&benor_mfma_coop_kernel<KIND, NT, BW, true, false>);
+  const void *fn = coop_exp(p) ? reinterpret_cast<const void *>(&benor_mfma_coop_kernel<KIND, NT, BW, true, true, true>)
+                               : reinterpret_cast<const void *>(&benor_mfma_coop_kernel<KIND, NT, BW, true, false, true>);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, 64 * BW, mfma_coop_lds_bytes(p)) != hipSuccess)
     n = 1;
   const int lds_fit = (int)lds_groups_per_cu(mfma_coop_lds_bytes(p));
@@ -390,15 +407,15 @@ int mfma_coop_blocks_per_cu(const KParams &p) {
   return k == 0 ? coop_occupancy<0, 4, 4>(p) : k == 1 ? coop_occupancy<1, 4, 4>(p) : coop_occupancy<2, 4, 4>(p);
 }
 
-template <int KIND, int NT, int BW, bool CB, bool EXP>
+template <int KIND, int NT, int BW, bool CB, bool EXP, bool PF>
 static hipError_t launch_coop_cb(const KParams &p, int grid, hipStream_t s) {
   const uint32_t lds = coop_lds_bytes(p, EXP);
   if (lds > 64u * 1024u) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&benor_mfma_coop_kernel<KIND, NT, BW, CB, EXP>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&benor_mfma_coop_kernel<KIND, NT, BW, CB, EXP, PF>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((benor_mfma_coop_kernel<KIND, NT, BW, CB, EXP>), dim3(grid), dim3(64 * BW), lds, s, p);
+  hipLaunchKernelGGL((benor_mfma_coop_kernel<KIND, NT, BW, CB, EXP, PF>), dim3(grid), dim3(64 * BW), lds, s, p);
   return hipGetLastError();
 }
 
@@ -407,8 +424,14 @@ template <int KIND, int NT, int BW>
 static hipError_t launch_coop(const KParams &p, int grid, hipStream_t s) {
   const char *ev = getenv("BENOR_COOP_CBIAS");
   const bool cb = !(ev && ev[0] == '0');
-  if (coop_exp(p)) return cb ? launch_coop_cb<KIND, NT, BW, true, true>(p, grid, s) : launch_coop_cb<KIND, NT, BW, false, true>(p, grid, s);
-  return cb ? launch_coop_cb<KIND, NT, BW, true, false>(p, grid, s) : launch_coop_cb<KIND, NT, BW, false, false>(p, grid, s);
+  const char *pv = getenv("BENOR_COOP_PF");        // BENOR_COOP_PF=0: three barriers per group (A/B)
+  const bool pf = !(pv && pv[0] == '0');
+  if (!cb) return coop_exp(p) ? launch_coop_cb<KIND, NT, BW, false, true, false>(p, grid, s)
+                              : launch_coop_cb<KIND, NT, BW, false, false, false>(p, grid, s);
+  if (coop_exp(p)) return pf ? launch_coop_cb<KIND, NT, BW, true, true, true>(p, grid, s)
+                             : launch_coop_cb<KIND, NT, BW, true, true, false>(p, grid, s);
+  return pf ? launch_coop_cb<KIND, NT, BW, true, false, true>(p, grid, s)
+            : launch_coop_cb<KIND, NT, BW, true, false, false>(p, grid, s);
 }
 
 template <int KIND, int NT>
