@@ -63,7 +63,7 @@ EXPORTED_SYMBOLS = (
     "bo_plan_create", "bo_plan_launch", "bo_plan_run", "bo_plan_popc_words_per_node_round",
     "bo_plan_live_nodes", "bo_plan_destroy", "bo_run_trials", "bo_run_trial_states",
     "bo_popc_peak", "bo_last_error", "bo_abi_version", "bo_kernel_version", "bo_plan_kernel", "bo_kernel_for",
-    "bo_mfma_peak", "bo_consensus_start_sched",
+    "bo_mfma_peak", "bo_consensus_start_sched", "bo_plan_check",
 )
 
 
@@ -125,6 +125,7 @@ def lib() -> ctypes.CDLL:
     L.bo_plan_launch.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
                                  ctypes.c_void_p]
     L.bo_plan_run.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, P(ctypes.c_uint64)]
+    L.bo_plan_check.argtypes = [ctypes.c_void_p]
     L.bo_plan_popc_words_per_node_round.argtypes = [ctypes.c_void_p]
     L.bo_plan_popc_words_per_node_round.restype = ctypes.c_uint64
     L.bo_plan_live_nodes.argtypes = [ctypes.c_void_p]
@@ -223,8 +224,14 @@ class Network:
         if not stop_after:
             _check(lib().bo_consensus_start(self._h, seed, k_max))
             return
+        if not isinstance(stop_after, dict) and len(stop_after) != self.N:
+            raise ValueError(f"stop_after: a sequence must have N = {self.N} entries, got {len(stop_after)}")
         sched = [None] * self.N
         for i, v in (stop_after.items() if isinstance(stop_after, dict) else enumerate(stop_after)):
+            if isinstance(i, bool) or not isinstance(i, int) or not 0 <= i < self.N:
+                raise ValueError(f"stop_after: node {i!r} is not a node id in [0, {self.N})")
+            if v is not None and (isinstance(v, bool) or not isinstance(v, int) or not 0 <= v < NEVER):
+                raise ValueError(f"stop_after[{i}]: {v!r} is not a delivery count (uint32 < 2^32 - 1) or None")
             sched[i] = v
         arr = _crash_array(self.N, sched)
         _check(lib().bo_consensus_start_sched(self._h, seed, k_max, arr, self.N))
@@ -392,6 +399,11 @@ class TrialsPlan:
         """Asynchronous; adds into the device histogram at hist_dev_ptr."""
         _check(lib().bo_plan_launch(self._h, trial_begin, trial_count, ctypes.c_void_p(hist_dev_ptr),
                                     ctypes.c_void_p(stream_ptr)))
+
+    def check(self) -> None:
+        """bo_plan_check: synchronise and raise when a launch of this plan broke a
+        device-side invariant (its histogram is then incomplete)."""
+        _check(lib().bo_plan_check(self._h))
 
     def run(self, trial_begin: int, trial_count: int):
         import numpy as np

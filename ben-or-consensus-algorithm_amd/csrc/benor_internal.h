@@ -84,6 +84,10 @@ struct KParams {
   // (capacity trial_count) at defer_len
   uint32_t *defer_list, *defer_len, *defer_seg;
   uint32_t defer_seg_cap;
+  // set (atomic OR) by an owner that deferred more than defer_seg_cap trials: its
+  // extra trials are dropped, the launch's histogram is incomplete, and the
+  // runtime reports BO_ERR_INTERNAL (bo_plan_check / bo_plan_run)
+  uint32_t *defer_overflow;
   // W kernel trial-list mode: run the trials trial_begin + trial_list[i],
   // i < min(*trial_list_len, trial_count), instead of a contiguous range
   const uint32_t *trial_list, *trial_list_len;
@@ -95,6 +99,11 @@ struct KParams {
 
 
 constexpr uint32_t kMfmaContRounds = 3;        // matrix-core passes up to round 3, then the popcount kernel
+// The deferral buffer's 64-word length block: pass r's list length at
+// 16 (r - 1) (zeroed per chunk), the overflow flag at kDeferOverflowWord
+// (zeroed when the buffer is allocated and by bo_plan_check).
+constexpr uint32_t kDeferOverflowWord = 63;
+static_assert(16u * kMfmaContRounds <= kDeferOverflowWord, "deferral length words overlap the overflow flag");
 
 constexpr uint64_t kDeferChunk = 1ull << 22;   // trials per matrix-core launch when trials can be deferred
 

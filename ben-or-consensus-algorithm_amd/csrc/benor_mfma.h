@@ -392,7 +392,7 @@ __global__ void __launch_bounds__(256) benor_mfma_kernel(KParams p) {
           // the host sizes a segment for a wave's most groups per launch
           // (plan_launch_impl); the bound only guards the buffer
           const uint32_t idx = n_def + (uint32_t)__builtin_popcount(dcols & ((1u << lane) - 1u));
-          if (idx < p.defer_seg_cap) seg[idx] = toff;
+          if (idx < p.defer_seg_cap) seg[idx] = toff;   // beyond: counted, flagged below
         }
         n_def += (uint32_t)__builtin_popcount(dcols);
       }
@@ -415,6 +415,10 @@ __global__ void __launch_bounds__(256) benor_mfma_kernel(KParams p) {
     // shapes back (N=256 F=0 -26 % at 8 workgroups per CU against 2;
     // profiles/r03-s2n_mfma_blocks_per_cu_inproc.jsonl).  Parameter-block words
     // 4..7 hold the waves' counts, then the workgroup's base.
+    if (n_def > p.defer_seg_cap) {   // segment overflow: the extra trials are dropped and the launch flagged
+      if (lane == 0) atomicOr(p.defer_overflow, 1u);
+      n_def = p.defer_seg_cap;
+    }
     uint32_t *wdef = keys + 4;
     if (lane == 0) wdef[wv] = n_def;
     __syncthreads();

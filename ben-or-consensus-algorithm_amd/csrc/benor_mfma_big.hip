@@ -277,7 +277,7 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_big_kernel(KParams p) {
           // the host sizes a segment for a wave's most groups per launch
           // (plan_launch_impl); the bound only guards the buffer
           const uint32_t idx = n_def + (uint32_t)__builtin_popcount(dcols & ((1u << lane) - 1u));
-          if (idx < p.defer_seg_cap) seg[idx] = toff;
+          if (idx < p.defer_seg_cap) seg[idx] = toff;   // beyond: counted, flagged below
         }
         n_def += (uint32_t)__builtin_popcount(dcols);
       }
@@ -294,6 +294,10 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_big_kernel(KParams p) {
   if constexpr (KIND > 0) {
     // the waves' deferred trials -> the compact list, one global atomic per
     // workgroup (as benor_mfma.h; parameter-block words 4..7, BW <= 4)
+    if (n_def > p.defer_seg_cap) {   // segment overflow: the extra trials are dropped and the launch flagged
+      if (lane == 0) atomicOr(p.defer_overflow, 1u);
+      n_def = p.defer_seg_cap;
+    }
     uint32_t *wdef = keys + 4;
     if (lane == 0) wdef[wv] = n_def;
     __syncthreads();

@@ -308,7 +308,7 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_coop_kernel(KParams p) {
         if (dcols) {
           if (lane < 32u && ((dcols >> lane) & 1u)) {
             const uint32_t idx = n_def + (uint32_t)__builtin_popcount(dcols & ((1u << lane) - 1u));
-            if (idx < p.defer_seg_cap) seg[idx] = toff;
+            if (idx < p.defer_seg_cap) seg[idx] = toff;   // beyond: counted, flagged below
           }
           n_def += (uint32_t)__builtin_popcount(dcols);
         }
@@ -325,6 +325,10 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_coop_kernel(KParams p) {
     // next R-phase barrier, which wave 0 must reach.
   }
   if (wv == 0u) {
+    if (KIND > 0 && n_def > p.defer_seg_cap) {   // segment overflow: extra trials dropped, launch flagged
+      if (lane == 0) atomicOr(p.defer_overflow, 1u);
+      n_def = p.defer_seg_cap;
+    }
     if (KIND > 0 && n_def) {                   // this workgroup's deferred trials -> the compact list
       __threadfence();
       uint32_t base = 0u;

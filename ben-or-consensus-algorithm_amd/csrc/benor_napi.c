@@ -204,6 +204,12 @@ static napi_value network_start(napi_env env, napi_callback_info info) {
             j->stop_after[i] = (t == napi_null || t == napi_undefined) ? 0xFFFFFFFFu : get_u32(env, e, &ok);
         }
     }
+    if (!ok) {                                  /* kMax or a stopAfter entry is not a uint32 */
+        free(j->stop_after);
+        free(j);
+        napi_throw_type_error(env, NULL, "kMax and stopAfter entries must be uint32 (stopAfter entries may be null)");
+        return NULL;
+    }
     j->net = net;
     napi_create_reference(env, argv[0], 1, &j->net_ref);   /* keep the handle alive while running */
     napi_value promise, name;
@@ -233,6 +239,7 @@ static napi_value node_stop(napi_env env, napi_callback_info info) {
     if (!net) return NULL;
     int ok = 1;
     uint32_t i = get_u32(env, argv[1], &ok);
+    if (!ok) { napi_throw_type_error(env, NULL, "node index must be a uint32"); return NULL; }
     int rc = bo_node_stop(net, i);
     if (rc) { throw_bo(env, rc); return NULL; }
     return NULL;
@@ -246,6 +253,7 @@ static napi_value get_state(napi_env env, napi_callback_info info) {
     if (!net) return NULL;
     int ok = 1;
     uint32_t i = get_u32(env, argv[1], &ok);
+    if (!ok) { napi_throw_type_error(env, NULL, "node index must be a uint32"); return NULL; }
     bo_node_state s;
     int rc = bo_get_state(net, i, &s);
     if (rc) { throw_bo(env, rc); return NULL; }
@@ -274,6 +282,7 @@ static napi_value status(napi_env env, napi_callback_info info) {
     if (!net) return NULL;
     int ok = 1;
     uint32_t i = get_u32(env, argv[1], &ok);
+    if (!ok) { napi_throw_type_error(env, NULL, "node index must be a uint32"); return NULL; }
     int code = bo_status(net, i);
     if (code < 0) { throw_bo(env, -code); return NULL; }
     napi_value v;

@@ -86,6 +86,8 @@ struct bo_plan {
   uint32_t *d_scratch = nullptr;   // event mode
   uint32_t *d_defer = nullptr;     // matrix-core KIND > 0: deferred-trial list, its length, per-wave segments
   uint64_t defer_words = 0;
+  uint64_t defer_lens = 0;         // offset of the 64-word length block in d_defer
+  bool defer_overflowed = false;   // an overflow flag read back before a re-allocation
   int device = 0;
 };
 
@@ -179,11 +181,8 @@ int bo_consensus_start_sched(bo_network *net, uint64_t seed, uint32_t k_max, con
   if (!net) return fail(BO_ERR_INVALID_ARGUMENT, "net is NULL");
   if (k_max < 1 || k_max > BO_MAX_K) return fail(BO_ERR_INVALID_ARGUMENT, "k_max out of range");
   const uint32_t N = net->N;
-  if (stop_after && n_stop_after != N) return fail(BO_ERR_ARRAYS_DONT_MATCH, "stop schedule must have N entries");
-  bool scheduled = false;
-  for (uint32_t i = 0; stop_after && i < N; ++i) scheduled = scheduled || stop_after[i] != 0xFFFFFFFFu;
-  if (scheduled && N > benor::kMaxEventN)
-    return fail(BO_ERR_UNSUPPORTED, "a mid-run /stop schedule runs the event-level kernel: N <= 256");
+  if (stop_after && n_stop_after != N) return fail(BO_ERR_INVALID_ARGUMENT, "stop schedule must have N entries");
+  bool scheduled = false;   // a /stop lands on a node that runs (entries of killed nodes are moot)
   std::vector<uint8_t> crashed(N);
   std::vector<int8_t> x(N);
   std::vector<uint32_t> active, sched(N, 0xFFFFFFFFu);
@@ -208,6 +207,9 @@ int bo_consensus_start_sched(bo_network *net, uint64_t seed, uint32_t k_max, con
         if (stop_after) sched[i] = stop_after[i];
       }
     }
+    for (uint32_t i : active) scheduled = scheduled || sched[i] != 0xFFFFFFFFu;
+    if (scheduled && N > benor::kMaxEventN)
+      return fail(BO_ERR_UNSUPPORTED, "a mid-run /stop schedule runs the event-level kernel: N <= 256");
     if (active.empty()) { net->started = true; return BO_OK; }
     const int64_t quorum = (int64_t)N - (int64_t)net->F;
     // Fewer running senders than the quorum: no R-phase ever triggers
@@ -497,19 +499,33 @@ static int plan_launch_impl(bo_plan *pl, uint64_t trial_begin, uint64_t trial_co
       seg_words = std::max<uint64_t>(seg_words, u * seg_cap_of(u));
     }
     const uint64_t words = 2u * cap + 64u + seg_words;                  // two lists, three lengths, segments
+    // Test knob: a smaller segment capacity than the sizing rule's, so that a
+    // GPU test can see the overflow reported (tests/test_mfma.py).
+    const char *cap_ev = getenv("BENOR_TEST_DEFER_SEG_CAP");
+    const uint32_t test_seg_cap = cap_ev ? (uint32_t)strtoul(cap_ev, nullptr, 10) : 0u;
     if (pl->defer_words < words) {
-      if (pl->d_defer) (void)hipFree(pl->d_defer);
+      if (pl->d_defer) {
+        uint32_t flag = 0;   // keep an overflow of an earlier launch reportable
+        HIP_TRY(hipDeviceSynchronize());
+        HIP_TRY(hipMemcpy(&flag, pl->d_defer + pl->defer_lens + benor::kDeferOverflowWord,
+                          sizeof flag, hipMemcpyDeviceToHost));
+        pl->defer_overflowed = pl->defer_overflowed || flag != 0u;
+        (void)hipFree(pl->d_defer);
+      }
       pl->d_defer = nullptr;
       pl->defer_words = 0;
       HIP_TRY(hipMalloc(&pl->d_defer, sizeof(uint32_t) * words));
       pl->defer_words = words;
+      pl->defer_lens = cap;   // where the length block sits (bo_plan_check)
+      HIP_TRY(hipMemsetAsync(pl->d_defer + cap, 0, sizeof(uint32_t) * 64u, s));
     }
     uint32_t *const lens = pl->d_defer + cap;                           // pass r's output length: lens[16 (r - 1)]
     uint32_t *const segs = lens + 64u;
     uint32_t *const lists[2] = {pl->d_defer, segs + seg_words};         // pass r writes lists[(r - 1) & 1]
     for (uint64_t done = 0; done < trial_count;) {
       const uint64_t n = std::min<uint64_t>(trial_count - done, cap);
-      HIP_TRY(hipMemsetAsync(lens, 0, sizeof(uint32_t) * 48u, s));   // every pass's length, one fill
+      // every pass's length, one fill (the overflow flag after them persists)
+      HIP_TRY(hipMemsetAsync(lens, 0, sizeof(uint32_t) * 16u * std::max<uint32_t>(last_round, 1u), s));
       kp.trial_begin = trial_begin + done;
       kp.trial_count = n;
       kp.defer_seg = segs;
@@ -525,6 +541,8 @@ static int plan_launch_impl(bo_plan *pl, uint64_t trial_begin, uint64_t trial_co
         kc.defer_list = lists[(r - 1u) & 1u];
         kc.defer_len = lens + 16u * (r - 1u);
         kc.defer_seg_cap = (uint32_t)seg_cap_of(benor::defer_units(kc, g));
+        kc.defer_overflow = lens + benor::kDeferOverflowWord;
+        if (test_seg_cap) kc.defer_seg_cap = std::min<uint32_t>(kc.defer_seg_cap, test_seg_cap);
         HIP_TRY(benor::launch_lockstep(kc, g, s));
         r_last = r;
       }
@@ -570,7 +588,27 @@ int bo_plan_run(bo_plan *pl, uint64_t trial_begin, uint64_t trial_count, uint64_
   (void)hipFree(d);
   if (e != hipSuccess) return hip_fail(e, "bo_plan_run");
   if (rc) return rc;
+  rc = bo_plan_check(pl);
+  if (rc) return rc;
   for (uint32_t i = 0; i < H; ++i) hist_host[i] += h[i];
+  return BO_OK;
+}
+
+int bo_plan_check(bo_plan *pl) {
+  if (!pl) return fail(BO_ERR_INVALID_ARGUMENT, "NULL argument");
+  bool bad = pl->defer_overflowed;
+  if (pl->d_defer) {
+    HIP_TRY(hipDeviceSynchronize());
+    uint32_t *flag = pl->d_defer + pl->defer_lens + benor::kDeferOverflowWord;
+    uint32_t v = 0;
+    HIP_TRY(hipMemcpy(&v, flag, sizeof v, hipMemcpyDeviceToHost));
+    if (v) HIP_TRY(hipMemset(flag, 0, sizeof v));
+    bad = bad || v != 0u;
+  }
+  pl->defer_overflowed = false;
+  if (bad)
+    return fail(BO_ERR_INTERNAL, "a matrix-core launch deferred more trials than its segment holds: "
+                                 "its histogram is incomplete (deferral segment sizing)");
   return BO_OK;
 }
 

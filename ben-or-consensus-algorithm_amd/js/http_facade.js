@@ -27,6 +27,21 @@ const addon = require(path.join(__dirname, 'benor.node'));
 
 const BASE_NODE_PORT = 3000;   // src/config.ts:1
 
+
+// options.stopAfter -> an array of N entries (null = never stopped).  Keys
+// must be node ids in [0, N): a bad key is a RangeError, not a launch error.
+function stopSchedule(N, stopAfter) {
+  if (Array.isArray(stopAfter) && stopAfter.length !== N)
+    throw new RangeError(`stopAfter: an array must have N = ${N} entries, got ${stopAfter.length}`);
+  const sched = new Array(N).fill(null);
+  for (const [k, v] of Object.entries(stopAfter)) {
+    const i = Number(k);
+    if (!Number.isInteger(i) || i < 0 || i >= N) throw new RangeError(`stopAfter: node ${k} is not in [0, ${N})`);
+    sched[i] = v;
+  }
+  return sched;
+}
+
 async function launchNetwork(N, F, initialValues, faultyList, options = {}) {
   const basePort = options.basePort !== undefined ? options.basePort : BASE_NODE_PORT;
   const kMax = options.kMax !== undefined ? options.kMax : 64;
@@ -36,8 +51,7 @@ async function launchNetwork(N, F, initialValues, faultyList, options = {}) {
   // flight is ordered after it; a scheduled one lands mid-round.
   let sched;
   if (options.stopAfter !== undefined && options.stopAfter !== null) {
-    sched = new Array(N).fill(null);
-    for (const [i, v] of Object.entries(options.stopAfter)) sched[Number(i)] = v;
+    sched = stopSchedule(N, options.stopAfter);
   }
   const handle = addon.networkCreate(N, F, initialValues, faultyList);   // launchNodes.ts:10-13 errors
   const net = {

@@ -26,6 +26,21 @@ class NodeServer {
   closeAllConnections() {}
 }
 
+
+// options.stopAfter -> an array of N entries (null = never stopped).  Keys
+// must be node ids in [0, N): a bad key is a RangeError, not a launch error.
+function stopSchedule(N, stopAfter) {
+  if (Array.isArray(stopAfter) && stopAfter.length !== N)
+    throw new RangeError(`stopAfter: an array must have N = ${N} entries, got ${stopAfter.length}`);
+  const sched = new Array(N).fill(null);
+  for (const [k, v] of Object.entries(stopAfter)) {
+    const i = Number(k);
+    if (!Number.isInteger(i) || i < 0 || i >= N) throw new RangeError(`stopAfter: node ${k} is not in [0, ${N})`);
+    sched[i] = v;
+  }
+  return sched;
+}
+
 async function launchNetwork(N, F, initialValues, faultyList) {
   const handle = addon.networkCreate(N, F, initialValues, faultyList);   // throws the reference's Errors
   current = { handle, N };
@@ -63,8 +78,7 @@ async function startConsensus(N, options = {}) {
   const kMax = options.kMax !== undefined ? options.kMax : DEFAULT_K_MAX;
   let sched;
   if (options.stopAfter !== undefined && options.stopAfter !== null) {
-    sched = new Array(N).fill(null);
-    for (const [i, v] of Object.entries(options.stopAfter)) sched[Number(i)] = v;
+    sched = stopSchedule(N, options.stopAfter);
   }
   try {
     await addon.networkStart(net(N).handle, seed, kMax, sched);

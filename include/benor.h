@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define BENOR_ABI_VERSION 5
+#define BENOR_ABI_VERSION 6
 
 /* Return codes.  The first two are the reference's two launch errors. */
 enum {
@@ -41,7 +41,8 @@ enum {
     BO_ERR_HIP = 5,
     BO_ERR_OUT_OF_RANGE = 6,        /* node index >= N */
     BO_ERR_UNSUPPORTED = 7,         /* configuration outside what this build simulates */
-    BO_ERR_ALREADY_STARTED = 8      /* second start on one network: its inboxes persist (node.ts:29-30) */
+    BO_ERR_ALREADY_STARTED = 8,     /* second start on one network: its inboxes persist (node.ts:29-30) */
+    BO_ERR_INTERNAL = 9             /* a device-side invariant failed: the affected results are invalid */
 };
 
 /* Delivery model.  LOCKSTEP is the reference's semantics for its admissible
@@ -175,8 +176,15 @@ int bo_plan_create(const bo_trials_cfg *cfg, bo_plan **out);
 int bo_plan_launch(bo_plan *plan, uint64_t trial_begin, uint64_t trial_count,
                    uint64_t *hist_dev, void *stream);
 
-/* Same, blocking, host histogram (added into hist_host). */
+/* Same, blocking, host histogram (added into hist_host).  Includes bo_plan_check. */
 int bo_plan_run(bo_plan *plan, uint64_t trial_begin, uint64_t trial_count, uint64_t *hist_host);
+
+/* Synchronise the device and report device-side invariant failures of this
+ * plan's launches since the last check: BO_ERR_INTERNAL when a matrix-core
+ * launch deferred more trials than its segment holds (their outcomes are then
+ * missing from the histogram).  No reference counterpart: call it after a
+ * series of bo_plan_launch before trusting their histograms. */
+int bo_plan_check(bo_plan *plan);
 
 /* The roofline's algorithmic unit: VALU popcount words that the per-receiver
  * tallies of one live node-round need, m = live nodes, M = m - (number of "?"

@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol():
     L = benor.lib()
     for s in header_symbols():
         assert hasattr(L, s)
-    assert L.bo_abi_version() == 5
+    assert L.bo_abi_version() == 6
     assert L.bo_hist_len(64) == 65 * 3 + 1
 
 
@@ -130,3 +130,21 @@ def test_library_built_from_these_sources():
     import __graft_entry__ as g
 
     assert benor.kernel_version() == g.kernel_digest()
+
+
+def test_digest_covers_runtime_and_abi_header():
+    """A change to the runtime (plans, dispatch, grid and deferral sizing) or
+    to the C ABI header alone changes the digest, so the check above fails
+    on a library built before it."""
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import __graft_entry__ as g
+
+    srcs = g.digest_sources()
+    rt = os.path.join(g.PKG, "csrc", "benor_runtime.cpp")
+    hdr = os.path.join(ROOT, "include", "benor.h")
+    assert rt in srcs and hdr in srcs
+    base = g.kernel_digest()
+    for f in (rt, hdr):
+        assert g.kernel_digest({f: open(f, "rb").read() + b"\n// edit\n"}) != base

@@ -355,3 +355,60 @@ def test_mfma_big_fixed_init_matches_oracle(N, F, q):
 def test_mfma_peak_probe():
     peak = benor.mfma_peak(3)
     assert 1e15 < peak < 6e15                # dense e2m1 spec: 5e15 multiply-adds/s
+
+
+# ------------------------------------------------- deferral segment invariant
+def seg_cap_of(trials, units):
+    """The runtime's segment sizing (benor_runtime.cpp plan_launch_impl):
+    ceil(groups / units) 32-trial groups per owner."""
+    groups = (trials + 31) // 32
+    return (groups + units - 1) // units * 32
+
+
+@pytest.mark.parametrize("trials", [1, 31, 32, 33, 1000, 4096 * 32 + 5, (1 << 22)])
+@pytest.mark.parametrize("units", [1, 3, 64, 1024, 2048 * 4, 1 << 16])
+def test_deferral_segment_sizing_covers_every_owner(trials, units):
+    """Owner w of a launch (wave, or workgroup of the cooperative form) walks
+    the 32-trial groups w, w + units, ... (grid-stride), and every trial of a
+    group can defer: the segment must hold 32 x the most groups an owner gets."""
+    groups = (trials + 31) // 32
+    most = max(len(range(w, groups, units)) for w in range(min(units, groups))) if groups else 0
+    assert 32 * most <= seg_cap_of(trials, units)
+
+
+class _env:
+    """Set environment variables for a block (None = leave unset)."""
+    def __init__(self, **kv):
+        self.kv = {k: v for k, v in kv.items() if v is not None}
+
+    def __enter__(self):
+        self.old = {k: os.environ.get(k) for k in self.kv}
+        os.environ.update(self.kv)
+
+    def __exit__(self, *a):
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,F,form", [(256, 0, None), (300, 120, None), (3000, 900, "coop"), (2048, 0, "wave")])
+def test_deferral_overflow_is_reported(N, F, form):
+    """A segment capacity below the sizing rule (BENOR_TEST_DEFER_SEG_CAP=1)
+    makes owners drop deferred trials: bo_plan_run must fail with
+    BO_ERR_INTERNAL instead of returning an incomplete histogram, and the
+    next run at the normal capacity is clean and matches the popcount kernel."""
+    T = 200_000 if N <= 300 else 40_000
+    with _env(BENOR_BIG_FORM=form):
+        p = plan(N, F, seed=3, k_max=12)
+        assert p.kernel == benor.BO_KERNEL_MFMA
+        with _env(BENOR_TEST_DEFER_SEG_CAP="1"):
+            with pytest.raises(RuntimeError, match="libbenor error 9"):
+                p.run(0, T)
+        got = p.run(0, T)
+        p.check()
+    with _env(BENOR_NO_MFMA="1", BENOR_NO_MFMA_BIG="1"):
+        ref = benor.TrialsPlan(N, F, seed=3, k_max=12).run(0, T)
+    np.testing.assert_array_equal(got, ref)

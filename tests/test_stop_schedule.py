@@ -86,7 +86,11 @@ def test_schedule_validation():
     benor.launchNetwork(5, 1, [1, 1, 1, 0, 0], [False, False, False, False, True])
     L = benor.lib()
     sched = (benor.ctypes.c_uint32 * 3)(1, 2, 3)
-    assert L.bo_consensus_start_sched(benor._current._h, 1, 16, sched, 3) == benor.BO_ERR_ARRAYS_DONT_MATCH
+    assert L.bo_consensus_start_sched(benor._current._h, 1, 16, sched, 3) == benor.BO_ERR_INVALID_ARGUMENT
+    # the mirrors refuse bad node ids and lengths before the C ABI sees them
+    for bad in ({-1: 3}, {5: 3}, {"2": 3}, [1, 2, 3], {1: -4}, {1: 2.5}):
+        with pytest.raises(ValueError):
+            benor.startConsensus(5, seed=1, stop_after=bad)
 
 
 def test_schedule_cases_land_where_intended():
