@@ -76,6 +76,7 @@ struct KParams {
   // random delivery (variant 2): Bernoulli + fix-up sampler with p = rd_a / 16 and
   // rd_b-bit index fields; rd_a = 0 selects Floyd (oracle_delivery_bernoulli)
   uint32_t rd_a, rd_b;
+  uint32_t rd_rows;                // Bernoulli sampler: bitset rows per lane, max(ceil(m/32), 2^rd_b / 32)
   uint64_t ev_lanes;               // lanes the scratch buffer holds
   uint32_t *scratch;               // [ev_lanes][ev_stride]
   // matrix-core kernel (variant 7, KIND > 0): trials that do not halt in round 1,
@@ -111,6 +112,11 @@ constexpr uint64_t kDeferChunk = 1ull << 22;   // trials per matrix-core launch 
 void plan_geometry(KParams &p);
 
 hipError_t launch_lockstep(const KParams &p, int grid_blocks, hipStream_t stream);
+
+// Random delivery, Bernoulli + fix-up sampler (benor_random.hip, r04).
+uint32_t random_bern_rows(uint32_t m, uint32_t b);
+hipError_t launch_random_bern(const KParams &p, int grid_blocks, hipStream_t stream);
+bool random_bern_v1(const KParams &p);   // BENOR_RANDOM_V1=1: the r02 kernel (A/B knob)
 
 // Per-shape launchers, explicitly instantiated in benor_w_*.hip (W = 1..32)
 // and benor_blocked.hip (G = 11..22).

@@ -762,6 +762,10 @@ void plan_geometry(KParams &p) {
       p.rd_b = b;
     }
     p.wave_bytes = 2u * W * 16u + 2u * W * 64u * 4u;   // X, P records + per-lane bitset
+    if (p.rd_a && !random_bern_v1(p)) {               // benor_random.hip: padded bitset rows
+      p.rd_rows = random_bern_rows(p.m, p.rd_b);
+      p.wave_bytes = 2u * W * 16u + p.rd_rows * 64u * 4u;
+    }
     p.lds_bytes = p.hist_bytes + kWavesPerBlock * p.wave_bytes;
     return;
   }
@@ -898,6 +902,7 @@ hipError_t launch_lockstep(const KParams &p, int grid, hipStream_t s) {
     q.lds_bytes = q.hist_bytes + kWavesPerBlock * q.wave_bytes;
     return launch_lockstep(q, grid, s);
   }
+  if (p.variant == 2 && p.rd_a && p.rd_rows) return launch_random_bern(p, grid, s);
   if (p.variant == 2) {
     if (p.lds_bytes > 64u * 1024u) {
       hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&benor_random_kernel),
@@ -932,6 +937,12 @@ uint32_t block_waves(const KParams &p) {
 
 uint64_t defer_units(const KParams &p, int grid) {
   return mfma_big_coop(p) ? (uint64_t)grid : (uint64_t)grid * block_waves(p);
+}
+
+bool random_bern_v1(const KParams &p) {
+  (void)p;
+  const char *ev = getenv("BENOR_RANDOM_V1");
+  return ev && ev[0] == '1';
 }
 
 // A packed-shape launch runs on the lane kernel when it writes per-node

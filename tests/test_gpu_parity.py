@@ -416,3 +416,25 @@ def test_event_mode_without_stop_equals_lockstep_kernel():
         a = benor.TrialsPlan(N, F, fl, seed=8, k_max=16, mode=EV).run(0, 50_000)
         b = benor.TrialsPlan(N, F, fl, seed=8, k_max=16).run(0, 50_000)
         np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("N,F,f,T,init", [(1024, 341, 0, 3000, None), (1024, 341, 100, 2000, None),
+                                          (600, 200, 37, 2000, "q"), (4096, 1365, 0, 64, None),
+                                          (3000, 1210, 0, 100, None), (257, 80, 1, 4000, "q")])
+def test_random_delivery_r04_kernel_equals_r02_kernel(N, F, f, T, init):
+    """The r04 Bernoulli kernel (benor_random.hip: uniform Philox rounds hoisted,
+    ds_mskor_rtn fix-up with speculative batches and undo, padded bitset rows)
+    gives the r02 kernel's histograms bit for bit (BENOR_RANDOM_V1=1 selects the
+    r02 kernel), on random and fixed initial values with "?" inputs."""
+    fl = first_f(N, f)
+    vals = None
+    if init == "q":
+        rng = np.random.default_rng(N)
+        vals = ["?" if rng.random() < 0.1 else int(rng.integers(0, 2)) for _ in range(N)]
+    new = benor.TrialsPlan(N, F, fl, seed=0xA5A5 ^ N, k_max=12, mode=RD, initial_values=vals)
+    os.environ["BENOR_RANDOM_V1"] = "1"
+    try:
+        old = benor.TrialsPlan(N, F, fl, seed=0xA5A5 ^ N, k_max=12, mode=RD, initial_values=vals)
+    finally:
+        os.environ.pop("BENOR_RANDOM_V1", None)
+    np.testing.assert_array_equal(new.run(99, T), old.run(99, T))
