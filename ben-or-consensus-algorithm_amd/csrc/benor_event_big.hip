@@ -1,0 +1,328 @@
+// benor_event_big.hip -- event-level mode for 256 < N <= 4096 (r04).
+//
+// The reference's GET /stop (node.ts:191-194) lands on a running consensus at
+// any network size; from then on the node drops every message (node.ts:45).
+// This kernel runs the message-granular model of oracle/benor_oracle.c (iii)
+// event_trial() -- the literal POST /message handler (node.ts:45-158), one
+// delivery per event in the seeded order, scheduled stops applied at their
+// delivery counts -- for networks too large for benor_event_kernel (one lane
+// per trial, N <= 256).  Definition and its bit-exact checks: the oracle.
+//
+// One wave = one trial (a 64-thread workgroup):
+//   * the message pool (uniform pick, swap-remove) lives in the workgroup's
+//     HBM scratch slice: 4N^2 + 64 u32 messages, to | ph << 12 | x << 13 |
+//     (k & 3) << 15 (k is recovered from the completion round `cur`, as in
+//     benor_event_kernel: a message to a running node is for [cur, cur + 2]);
+//   * per-node state lives in LDS: inbox counters {c0, c1, len} per phase
+//     (13 bits each, bit 63 = killed), x, k, the compact index for coins, and
+//     node bitsets (killed, decided, completion of rounds cur .. cur + 3).
+//     Every initially live node's message is needed for a quorum (exactly F
+//     faulty, launchNodes.ts:12-13), so a node's inbox for a phase holds one
+//     round at a time: R_k and R_{k+1} (P_k and P_{k+1}) are never in flight
+//     to it together, and the slot is cleared when its trigger fires;
+//   * the event chain is sequential (each pick depends on the pool's length,
+//     which a trigger changes).  Events go in batches of up to 64: lane i
+//     computes the pick of event e + i assuming no trigger (splitmix64 is a
+//     counter: state e + i is state e + (i + 1) * gamma) and loads both pool
+//     words the swap-remove touches, so one HBM round trip serves 64 events;
+//     the wave then applies them in order, resolving the batch's own earlier
+//     writes through a 64-entry overlay (lane j: position and value written by
+//     event j).  A trigger ends the batch: the overlay is written back, the
+//     triggered broadcast is appended, and the next batch starts after it.
+//     Batches also end before a scheduled stop.
+#include "benor_device.h"
+
+namespace benor {
+
+namespace {
+
+constexpr uint64_t kGamma = 0x9E3779B97F4A7C15ull;
+constexpr uint64_t kC13 = (1ull << 13) - 1ull;
+constexpr uint64_t kKilled = 1ull << 63;
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t lane) {   // v of `lane`, wave-uniform
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
+}
+
+__device__ __forceinline__ uint32_t last_lane(uint64_t mask) { return 63u - (uint32_t)__builtin_clzll(mask); }
+
+struct BigState {
+  uint64_t *ibox;     // [N][2] {c0, c1, len} per phase, bit 63 killed
+  int8_t *xs;         // [N]
+  int16_t *ks;        // [N]
+  uint16_t *cidx;     // [N] compact live index (coins)
+  uint64_t *killed;   // [64]
+  uint64_t *decided;  // [64]
+  uint64_t *comp;     // [4][64] completion of round k at k & 3
+};
+
+}  // namespace
+
+__global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t lane = threadIdx.x;
+  uint32_t *lhist = reinterpret_cast<uint32_t *>(smem);
+  for (uint32_t i = lane; i < p.hist_len; i += 64u) lhist[i] = 0u;
+
+  const uint32_t N = p.N, F = p.F, quorum = p.N - p.F, m = p.m;
+  const uint32_t NWd = (N + 63u) >> 6;                       // bitset words (<= 64: one per lane)
+  BigState S;
+  unsigned char *q = smem + p.hist_bytes;
+  S.ibox = reinterpret_cast<uint64_t *>(q);
+  S.killed = S.ibox + 2u * N;
+  S.decided = S.killed + 64;
+  S.comp = S.decided + 64;
+  S.ks = reinterpret_cast<int16_t *>(S.comp + 4 * 64);
+  S.cidx = reinterpret_cast<uint16_t *>(S.ks + ((N + 3u) & ~3u));
+  S.xs = reinterpret_cast<int8_t *>(S.cidx + ((N + 3u) & ~3u));
+  const uint64_t allw = lane < NWd ? (N >= 64u * (lane + 1u) ? ~0ull : (1ull << (N - 64u * lane)) - 1ull) : 0ull;
+  const uint64_t wmask = NWd >= 64u ? ~0ull : ((1ull << NWd) - 1ull);   // lanes holding a bitset word
+  const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
+  uint32_t *pool = p.scratch + (uint64_t)blockIdx.x * p.ev_stride;
+  const uint32_t cap = p.ev_cap;
+
+  // a | b == all, over the bitset words (one per lane)
+  auto full = [&](const uint64_t *a, const uint64_t *b) {
+    const bool ok = lane >= NWd || ((a[lane] | b[lane]) == allw);
+    return (__ballot(ok) & wmask) == wmask;
+  };
+
+  for (uint64_t t = blockIdx.x; t < p.trial_count; t += gridDim.x) {
+    const uint64_t trial = p.trial_begin + t;
+    const uint32_t tlo = (uint32_t)trial, thi = (uint32_t)(trial >> 32);
+    // ---- node.ts:21-26: faulty nodes killed, live nodes x = initial value
+    for (uint32_t w = lane; w < 64u; w += 64u) {
+      S.killed[w] = w < NWd ? allw : 0ull;   // every node, then the live ones cleared
+      S.decided[w] = 0ull;
+      for (int r = 0; r < 4; ++r) S.comp[r * 64 + w] = 0ull;
+    }
+    for (uint32_t i = lane; i < N; i += 64u) {
+      S.xs[i] = -1;
+      S.ks[i] = -1;
+      S.ibox[2u * i] = kKilled;
+      S.ibox[2u * i + 1u] = kKilled;
+    }
+    __syncthreads();
+    for (uint32_t c = lane; c < m; c += 64u) {
+      const uint32_t i = p.live_ids[c];
+      int8_t v;
+      if (p.init_mode == BO_INIT_RANDOM) {      // word c >> 5 of stream 1 (oracle_random_init)
+        const uint4 ir = philox4x32_10<false>(k0, k1, make_uint4(tlo, thi, c >> 7, kStreamInit << 24));
+        v = (int8_t)((coin_word(ir, ((c >> 5) & 3u) + 1u) >> (c & 31u)) & 1u);
+      } else {
+        v = p.init_x[i];
+      }
+      S.xs[i] = v;
+      S.ks[i] = 1;                              // /start: k = 1 (node.ts:172)
+      S.cidx[i] = (uint16_t)c;
+      S.ibox[2u * i] = 0ull;
+      S.ibox[2u * i + 1u] = 0ull;
+      __hip_atomic_fetch_and(reinterpret_cast<unsigned long long *>(&S.killed[i >> 6]), ~(1ull << (i & 63u)),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __syncthreads();
+    // ---- /start (node.ts:167-188): every live node broadcasts its x, in node order
+    uint32_t len = 0;
+    for (uint32_t c = 0; c < m; ++c) {
+      const uint32_t i = p.live_ids[c];
+      const uint32_t body = ((uint32_t)(S.xs[i] & 3) << 13) | (1u << 15);
+      for (uint32_t to = lane; to < N; to += 64u) pool[len + to] = to | body;
+      len += N;
+    }
+    uint64_t rng;
+    {
+      const uint4 o = philox4x32_10<false>(k0, k1, make_uint4(tlo, thi, 0u, kStreamOrder << 24));
+      rng = (((uint64_t)o.x << 32) | o.y) ^ 0xD1B54A32D192ED03ull;
+    }
+    __threadfence_block();
+    uint32_t next = 0, cur = 1, R = 0, halted = 0;
+    bool overflow = false;
+    uint64_t e = 0;
+    auto advance = [&]() {                      // complete rounds: halting (node.ts:116-145 as DESIGN §2)
+      while (full(S.comp + (cur & 3u) * 64u, S.killed)) {
+        if (full(S.decided, S.killed)) { halted = 1; R = cur; return; }
+        if (cur >= p.k_max) { halted = 2; R = cur; return; }
+        if (lane < 64u) S.comp[(cur & 3u) * 64u + lane] = 0ull;
+        ++cur;
+      }
+    };
+    while (!halted) {
+      // ---- scheduled GET /stop (node.ts:191-194) before delivery e
+      bool crashed = false;
+      while (next < p.ev_nstops && (p.ev_stops[next] >> 12) == e) {
+        const uint32_t i = (uint32_t)(p.ev_stops[next] & 4095u);
+        if (lane == 0u) {
+          S.killed[i >> 6] |= 1ull << (i & 63u);
+          S.ibox[2u * i] |= kKilled;
+          S.ibox[2u * i + 1u] |= kKilled;
+        }
+        crashed = true;
+        ++next;
+      }
+      if (crashed) {
+        __syncthreads();
+        const bool alive = lane < NWd && S.killed[lane] != allw;
+        if (!__any(alive)) { halted = 3; break; }
+        advance();
+        if (halted) break;
+      }
+      if (len == 0u) { halted = 3; break; }
+      // ---- a batch of speculative events e .. e + B - 1
+      uint64_t B = len < 64u ? len : 64u;
+      if (next < p.ev_nstops) {
+        const uint64_t until = (p.ev_stops[next] >> 12) - e;
+        if (until < B) B = until;
+      }
+      uint32_t pk = 0, pv = 0, tv = 0;
+      if (lane < B) {
+        const uint64_t z = mix64(rng + (uint64_t)(lane + 1u) * kGamma);
+        pk = (uint32_t)(((uint64_t)(uint32_t)(z >> 32) * (uint64_t)(len - lane)) >> 32);
+        // agent-scope loads are L2-served (no stale L1 line after the last batch's stores)
+        pv = __hip_atomic_load(&pool[pk], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        tv = __hip_atomic_load(&pool[len - 1u - lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      uint32_t ovp = 0xFFFFFFFFu, ovv = 0u;     // overlay: lane j = event j's write
+      uint32_t used = (uint32_t)B, trig = 0xFFFFFFFFu, tmsg = 0u;
+      uint64_t tbox = 0ull;
+      for (uint32_t i = 0; i < (uint32_t)B; ++i) {
+        const uint32_t qpos = rl(pk, i), tpos = len - 1u - i;
+        const uint64_t h1 = __ballot(ovp == qpos), h2 = __ballot(ovp == tpos);
+        const uint32_t msg = h1 ? rl(ovv, last_lane(h1)) : rl(pv, i);
+        const uint32_t moved = h2 ? rl(ovv, last_lane(h2)) : rl(tv, i);
+        if (lane == i) { ovp = qpos; ovv = moved; }
+        // ---- POST /message (node.ts:45-158)
+        const uint32_t to = msg & 4095u, ph = (msg >> 12) & 1u, xv = (msg >> 13) & 3u;
+        const uint32_t k = cur + (((msg >> 15) - cur) & 3u);
+        uint64_t *bp = &S.ibox[2u * to + ph];
+        uint64_t b = *bp;
+        if (b & kKilled) continue;             // node.ts:45
+        if (k >= p.k_max + 3u) continue;        // beyond the oracle's round window
+        b += 1ull << 26;                        // len
+        if (xv == 0u) b += 1ull;                // c0
+        else if (xv == 1u) b += 1ull << 13;     // c1
+        if (((b >> 26) & kC13) != quorum) {     // node.ts:52, :88
+          if (lane == 0u) *bp = b;
+          continue;
+        }
+        if (lane == 0u) *bp = 0ull;             // every message of the phase arrived: the slot is free
+        trig = i;
+        tmsg = msg;
+        tbox = b;
+        used = i + 1u;
+        break;
+      }
+      // ---- the batch's pool writes (the last write to each position wins)
+      {
+        bool live = lane < used && ovp < len - used;
+        for (uint32_t j = 1; j < used; ++j) {
+          const uint32_t v = rl(ovp, j);
+          live = live && !(j > lane && v == ovp);
+        }
+        if (live) pool[ovp] = ovv;
+      }
+      len -= used;
+      rng += (uint64_t)used * kGamma;
+      e += used;
+      if (trig == 0xFFFFFFFFu) {
+        __threadfence_block();
+        continue;
+      }
+      // ---- a trigger (node.ts:52-80 R-phase, :88-157 P-phase)
+      const uint32_t to = tmsg & 4095u, ph = (tmsg >> 12) & 1u;
+      const uint32_t k = cur + (((tmsg >> 15) - cur) & 3u);
+      const uint32_t c0 = (uint32_t)(tbox & kC13), c1 = (uint32_t)((tbox >> 13) & kC13);
+      uint32_t body;
+      if (ph == 0u) {
+        const uint32_t v = c0 > c1 ? 0u : (c1 > c0 ? 1u : 2u);
+        body = (1u << 12) | (v << 13) | ((k & 3u) << 15);
+      } else {
+        int8_t nx;
+        bool dec = true;
+        if (c0 > F) nx = 0;
+        else if (c1 > F) nx = 1;
+        else {
+          dec = false;
+          if (c0 + c1 > 0u && c0 > c1) nx = 0;
+          else if (c0 + c1 > 0u && c0 < c1) nx = 1;
+          else {
+            const uint32_t c = S.cidx[to];     // the coin of compact node c in round k (node.ts:111)
+            const uint4 rr = coin_block<false>(k0, k1, tlo, thi, c, k);
+            nx = (int8_t)((coin_word(rr, k) >> (c & 31u)) & 1u);
+          }
+        }
+        if (lane == 0u) {
+          S.xs[to] = nx;
+          S.ks[to] = (int16_t)(k + 1u);
+          if (dec) S.decided[to >> 6] |= 1ull << (to & 63u);
+          S.comp[(k & 3u) * 64u + (to >> 6)] |= 1ull << (to & 63u);
+        }
+        __syncthreads();
+        advance();
+        if (halted) break;
+        body = ((uint32_t)(nx & 3) << 13) | (((k + 1u) & 3u) << 15);
+      }
+      if ((uint64_t)len + N > cap) { overflow = true; halted = 3; break; }
+      __threadfence_block();
+      for (uint32_t d = lane; d < N; d += 64u) pool[len + d] = d | body;
+      len += N;
+      __threadfence_block();
+    }
+    // ---- outcome over the nodes still running
+    bool any0 = false, any1 = false, anyq = false, nl = false;
+    __syncthreads();
+    for (uint32_t i = lane; i < N; i += 64u) {
+      if ((S.killed[i >> 6] >> (i & 63u)) & 1ull) continue;
+      nl = true;
+      const int8_t v = S.xs[i];
+      if (v == 0) any0 = true; else if (v == 1) any1 = true; else anyq = true;
+    }
+    const bool g0 = __any(any0), g1 = __any(any1), gq = __any(anyq), gl = __any(nl);
+    const uint32_t v = (!gl || gq || (g0 && g1)) ? 2u : (g1 ? 1u : 0u);
+    if (lane == 0u) {
+      atomicAdd(&lhist[halted == 1u ? (R * 3u + v) : v], 1u);
+      if (halted == 1u && v == 2u) atomicAdd(&lhist[p.hist_len - 1u], 1u);
+      if (overflow && p.rounds_out) atomicOr(p.rounds_out, 0x80000000u);
+      if (overflow && p.overflow) atomicOr(p.overflow, 2u);
+      if (p.node_out && p.rounds_out) atomicOr(p.rounds_out, halted == 1u ? R : 0u);
+    }
+    if (p.node_out) {
+      for (uint32_t i = lane; i < N; i += 64u) {
+        bo_node_state ns;
+        const bool f = S.ks[i] < 0 && S.xs[i] < 0;   // faulty from launch (never ran)
+        ns.killed = (int8_t)((S.killed[i >> 6] >> (i & 63u)) & 1ull);
+        ns.x = S.xs[i];
+        ns.decided = f ? (int8_t)-1 : (int8_t)((S.decided[i >> 6] >> (i & 63u)) & 1ull);
+        ns.pad = 0;
+        ns.k = S.ks[i];
+        p.node_out[i] = ns;
+      }
+    }
+    __syncthreads();
+  }
+  __syncthreads();
+  flush_hist(lhist, p);
+}
+
+uint32_t event_big_lds_bytes(const KParams &p) {
+  const uint32_t N = p.N;
+  return p.hist_bytes + 16u * N + 8u * 64u * 6u + 2u * ((N + 3u) & ~3u) * 2u + ((N + 15u) & ~15u);
+}
+
+hipError_t launch_event_big(const KParams &p, int grid, hipStream_t s) {
+  const uint32_t lds = event_big_lds_bytes(p);
+  if (lds > 64u * 1024u) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&benor_event_big_kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(benor_event_big_kernel, dim3(grid), dim3(64), lds, s, p);
+  return hipGetLastError();
+}
+
+}  // namespace benor

@@ -26,7 +26,8 @@ constexpr uint32_t kMaxSmallMfmaM = 32;    // 2 <= m <= 32: packed matrix-core k
                                            // trials per wave iteration (benor_mfma_small.h)
 constexpr uint32_t kMaxMfmaM = 1024;       // matrix-core kernel (benor_mfma.h): W <= 16, operands in registers;
                                            // beyond, the big-network form (runtime W, proposals in LDS) to BO_MAX_N
-constexpr uint32_t kMaxEventN = 256;       // event level: node ids in 8 bits of a message
+constexpr uint32_t kMaxEventN = 256;       // event level, one lane per trial: node ids in 8 bits of a message;
+                                           // up to BO_MAX_N: one wave per trial (benor_event_big.hip)
 // Workgroups of `lds` dynamic LDS bytes that fit one CU's 160 KB: allocation
 // is in 512-byte granules (a 23216-byte group fits 6 per CU, not 7: the 7th
 // waits, and a grid sized for 7 per CU ran 1.45x longer).
@@ -85,10 +86,16 @@ struct KParams {
   // (capacity trial_count) at defer_len
   uint32_t *defer_list, *defer_len, *defer_seg;
   uint32_t defer_seg_cap;
-  // set (atomic OR) by an owner that deferred more than defer_seg_cap trials: its
-  // extra trials are dropped, the launch's histogram is incomplete, and the
-  // runtime reports BO_ERR_INTERNAL (bo_plan_check / bo_plan_run)
-  uint32_t *defer_overflow;
+  // per-plan device flag word, set (atomic OR) when a launch broke a capacity
+  // invariant -- bit 0: an owner deferred more than defer_seg_cap trials (its
+  // extra trials are dropped); bit 1: an event-level message pool filled up.
+  // The launch's histogram is then incomplete; bo_plan_check / bo_plan_run
+  // report BO_ERR_INTERNAL.
+  uint32_t *overflow;
+  // event level, N > kMaxEventN (benor_event_big.hip): explicit /stop schedule
+  // as (event << 12 | node), ascending
+  const uint64_t *ev_stops;
+  uint32_t ev_nstops;
   // W kernel trial-list mode: run the trials trial_begin + trial_list[i],
   // i < min(*trial_list_len, trial_count), instead of a contiguous range
   const uint32_t *trial_list, *trial_list_len;
@@ -100,11 +107,8 @@ struct KParams {
 
 
 constexpr uint32_t kMfmaContRounds = 3;        // matrix-core passes up to round 3, then the popcount kernel
-// The deferral buffer's 64-word length block: pass r's list length at
-// 16 (r - 1) (zeroed per chunk), the overflow flag at kDeferOverflowWord
-// (zeroed when the buffer is allocated and by bo_plan_check).
-constexpr uint32_t kDeferOverflowWord = 63;
-static_assert(16u * kMfmaContRounds <= kDeferOverflowWord, "deferral length words overlap the overflow flag");
+// The deferral buffer's 64-word length block: pass r's list length at 16 (r - 1).
+static_assert(16u * kMfmaContRounds <= 64u, "deferral length words overflow their block");
 
 constexpr uint64_t kDeferChunk = 1ull << 22;   // trials per matrix-core launch when trials can be deferred
 
@@ -117,6 +121,10 @@ hipError_t launch_lockstep(const KParams &p, int grid_blocks, hipStream_t stream
 uint32_t random_bern_rows(uint32_t m, uint32_t b);
 hipError_t launch_random_bern(const KParams &p, int grid_blocks, hipStream_t stream);
 bool random_bern_v1(const KParams &p);   // BENOR_RANDOM_V1=1: the r02 kernel (A/B knob)
+
+// Event level for kMaxEventN < N <= BO_MAX_N (benor_event_big.hip): one wave per trial.
+uint32_t event_big_lds_bytes(const KParams &p);
+hipError_t launch_event_big(const KParams &p, int grid_blocks, hipStream_t stream);
 
 // Per-shape launchers, explicitly instantiated in benor_w_*.hip (W = 1..32)
 // and benor_blocked.hip (G = 11..22).

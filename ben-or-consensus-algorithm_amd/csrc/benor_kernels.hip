@@ -731,6 +731,16 @@ void plan_geometry(KParams &p) {
   const uint32_t W = p.W;
   p.hist_len = (p.k_max + 1u) * 3u + 1u;
   p.hist_bytes = (((p.hist_len * 4u) + 15u) & ~15u) + kParamBytes;   // histogram + parameter block
+  if (p.mode == BO_MODE_EVENT && p.N > kMaxEventN) {   // one wave per trial (benor_event_big.hip)
+    p.G = 1;
+    p.nblocks = 1;
+    p.variant = 5;
+    p.wave_bytes = 0;
+    p.ev_cap = 4u * p.N * p.N + 64u;
+    p.ev_stride = p.ev_cap;                          // u32 messages
+    p.lds_bytes = event_big_lds_bytes(p);
+    return;
+  }
   if (p.mode == BO_MODE_EVENT) {
     p.G = 1;
     p.nblocks = 1;
@@ -892,6 +902,7 @@ hipError_t launch_lockstep(const KParams &p, int grid, hipStream_t s) {
     }
     return hipGetLastError();
   }
+  if (p.variant == 5) return launch_event_big(p, grid, s);
   if (p.variant == 6) return dispatch_lane(p, grid, s, std::make_integer_sequence<int, (int)kMaxLaneM>{});
   if (p.variant == 8 && !small_on_lane(p))
     return dispatch_mfma_small(p, grid, s, std::make_integer_sequence<int, (int)kMaxSmallMfmaM - 1>{});   // m = 2..32
@@ -964,6 +975,10 @@ bool small_on_lane(const KParams &p) {
 int lockstep_grid(const KParams &p, int device) {
   int cus = 256;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+  if (p.variant == 5) {   // big event level: one wave per trial, grid = the scratch's trial slots
+    const uint64_t g = p.trial_count < p.ev_lanes ? p.trial_count : p.ev_lanes;
+    return (int)(g < 1u ? 1u : g);
+  }
   if (p.variant == 4) {   // event mode: one lane per trial, grid = the scratch's lane count
     const uint64_t blocks_needed = (p.trial_count + 255u) / 256u;
     uint64_t grid = p.ev_lanes / 256u;

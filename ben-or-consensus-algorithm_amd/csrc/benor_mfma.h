@@ -416,7 +416,7 @@ __global__ void __launch_bounds__(256) benor_mfma_kernel(KParams p) {
     // profiles/r03-s2n_mfma_blocks_per_cu_inproc.jsonl).  Parameter-block words
     // 4..7 hold the waves' counts, then the workgroup's base.
     if (n_def > p.defer_seg_cap) {   // segment overflow: the extra trials are dropped and the launch flagged
-      if (lane == 0) atomicOr(p.defer_overflow, 1u);
+      if (lane == 0) atomicOr(p.overflow, 1u);
       n_def = p.defer_seg_cap;
     }
     uint32_t *wdef = keys + 4;

@@ -295,7 +295,7 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_big_kernel(KParams p) {
     // the waves' deferred trials -> the compact list, one global atomic per
     // workgroup (as benor_mfma.h; parameter-block words 4..7, BW <= 4)
     if (n_def > p.defer_seg_cap) {   // segment overflow: the extra trials are dropped and the launch flagged
-      if (lane == 0) atomicOr(p.defer_overflow, 1u);
+      if (lane == 0) atomicOr(p.overflow, 1u);
       n_def = p.defer_seg_cap;
     }
     uint32_t *wdef = keys + 4;

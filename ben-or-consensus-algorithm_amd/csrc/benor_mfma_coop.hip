@@ -326,7 +326,7 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_coop_kernel(KParams p) {
   }
   if (wv == 0u) {
     if (KIND > 0 && n_def > p.defer_seg_cap) {   // segment overflow: extra trials dropped, launch flagged
-      if (lane == 0) atomicOr(p.defer_overflow, 1u);
+      if (lane == 0) atomicOr(p.overflow, 1u);
       n_def = p.defer_seg_cap;
     }
     if (KIND > 0 && n_def) {                   // this workgroup's deferred trials -> the compact list

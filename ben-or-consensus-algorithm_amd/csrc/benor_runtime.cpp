@@ -86,8 +86,8 @@ struct bo_plan {
   uint32_t *d_scratch = nullptr;   // event mode
   uint32_t *d_defer = nullptr;     // matrix-core KIND > 0: deferred-trial list, its length, per-wave segments
   uint64_t defer_words = 0;
-  uint64_t defer_lens = 0;         // offset of the 64-word length block in d_defer
-  bool defer_overflowed = false;   // an overflow flag read back before a re-allocation
+  uint32_t *d_flag = nullptr;      // KParams::overflow (bo_plan_check)
+  uint64_t *d_stops = nullptr;     // event level, N > 256: sorted /stop schedule
   int device = 0;
 };
 
@@ -208,8 +208,6 @@ int bo_consensus_start_sched(bo_network *net, uint64_t seed, uint32_t k_max, con
       }
     }
     for (uint32_t i : active) scheduled = scheduled || sched[i] != 0xFFFFFFFFu;
-    if (scheduled && N > benor::kMaxEventN)
-      return fail(BO_ERR_UNSUPPORTED, "a mid-run /stop schedule runs the event-level kernel: N <= 256");
     if (active.empty()) { net->started = true; return BO_OK; }
     const int64_t quorum = (int64_t)N - (int64_t)net->F;
     // Fewer running senders than the quorum: no R-phase ever triggers
@@ -277,8 +275,9 @@ static int plan_host(const bo_trials_cfg *cfg, std::vector<uint32_t> &live, std:
   if (cfg->k_max < 1 || cfg->k_max > BO_MAX_K) return fail(BO_ERR_INVALID_ARGUMENT, "k_max must be in [1, 1024]");
   if (cfg->mode != BO_MODE_LOCKSTEP && cfg->mode != BO_MODE_RANDOM_DELIVERY && cfg->mode != BO_MODE_EVENT)
     return fail(BO_ERR_UNSUPPORTED, "unknown delivery mode");
-  if (cfg->mode == BO_MODE_EVENT && cfg->N > benor::kMaxEventN)
-    return fail(BO_ERR_UNSUPPORTED, "event mode simulates N <= 256");
+  if (cfg->mode == BO_MODE_EVENT && cfg->N > benor::kMaxEventN && !cfg->crash_at && cfg->crash_count > 0)
+    return fail(BO_ERR_UNSUPPORTED, "event mode: a random /stop schedule (crash_count) needs N <= 256; "
+                                    "give crash_at for larger networks");
   if (cfg->init_mode != BO_INIT_RANDOM && cfg->init_mode != BO_INIT_FIXED)
     return fail(BO_ERR_INVALID_ARGUMENT, "unknown init_mode");
   if (!cfg->faulty) return fail(BO_ERR_INVALID_ARGUMENT, "faulty is NULL");
@@ -364,6 +363,11 @@ int bo_plan_create(const bo_trials_cfg *cfg, bo_plan **out) {
   pl->kp = kp0;
   benor::KParams &kp = pl->kp;
   const uint32_t m = kp.m;
+  {
+    hipError_t e = hipMalloc(&pl->d_flag, sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemset(pl->d_flag, 0, sizeof(uint32_t));
+    if (e != hipSuccess) { bo_plan_destroy(pl); return hip_fail(e, "plan flag"); }
+  }
   if (m > 0) {
     hipError_t e = hipMalloc(&pl->d_live, sizeof(uint32_t) * m);
     if (e == hipSuccess) e = hipMalloc(&pl->d_init, sizeof(uint4) * kp.W);
@@ -372,7 +376,36 @@ int bo_plan_create(const bo_trials_cfg *cfg, bo_plan **out) {
     if (e != hipSuccess) { bo_plan_destroy(pl); return hip_fail(e, "plan upload"); }
     kp.live_ids = pl->d_live;
     kp.init_plane = pl->d_init;
-    if (cfg->mode == BO_MODE_EVENT) {
+    if (cfg->mode == BO_MODE_EVENT && kp.variant == 5) {
+      // one wave per trial, each with a pool of ev_cap messages: as many
+      // concurrent trials as CUs, within ~4 GiB of pools
+      std::vector<int8_t> ix(cfg->N, 0);
+      if (cfg->init_mode == BO_INIT_FIXED)
+        for (uint32_t i = 0; i < cfg->N; ++i) ix[i] = cfg->init[i];
+      std::vector<uint64_t> stops;
+      if (cfg->crash_at)
+        for (uint32_t i = 0; i < cfg->N; ++i)
+          if (cfg->crash_at[i] != 0xFFFFFFFFu) stops.push_back(((uint64_t)cfg->crash_at[i] << 12) | i);
+      std::sort(stops.begin(), stops.end());
+      int cus = 256;
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      const uint64_t slot = (uint64_t)kp.ev_stride * 4u;
+      uint64_t slots = std::max<uint64_t>(1u, std::min<uint64_t>((uint64_t)cus, (4ull << 30) / slot));
+      kp.ev_lanes = slots;
+      e = hipMalloc(&pl->d_init_x, cfg->N);
+      if (e == hipSuccess) e = hipMemcpy(pl->d_init_x, ix.data(), cfg->N, hipMemcpyHostToDevice);
+      if (e == hipSuccess && !stops.empty()) {
+        e = hipMalloc(&pl->d_stops, sizeof(uint64_t) * stops.size());
+        if (e == hipSuccess)
+          e = hipMemcpy(pl->d_stops, stops.data(), sizeof(uint64_t) * stops.size(), hipMemcpyHostToDevice);
+      }
+      if (e == hipSuccess) e = hipMalloc(&pl->d_scratch, slots * slot);
+      if (e != hipSuccess) { bo_plan_destroy(pl); return hip_fail(e, "event-mode scratch"); }
+      kp.init_x = pl->d_init_x;
+      kp.ev_stops = pl->d_stops;
+      kp.ev_nstops = (uint32_t)stops.size();
+      kp.scratch = pl->d_scratch;
+    } else if (cfg->mode == BO_MODE_EVENT) {
       std::vector<int8_t> ix(cfg->N, 0);
       if (cfg->init_mode == BO_INIT_FIXED)
         for (uint32_t i = 0; i < cfg->N; ++i) ix[i] = cfg->init[i];
@@ -418,6 +451,8 @@ void bo_plan_destroy(bo_plan *pl) {
   if (pl->d_crash) (void)hipFree(pl->d_crash);
   if (pl->d_scratch) (void)hipFree(pl->d_scratch);
   if (pl->d_defer) (void)hipFree(pl->d_defer);
+  if (pl->d_flag) (void)hipFree(pl->d_flag);
+  if (pl->d_stops) (void)hipFree(pl->d_stops);
   delete pl;
 }
 
@@ -452,6 +487,7 @@ static int plan_launch_impl(bo_plan *pl, uint64_t trial_begin, uint64_t trial_co
     return BO_OK;
   }
   kp.hist = reinterpret_cast<unsigned long long *>(hist_dev);
+  kp.overflow = pl->d_flag;
   kp.node_out = node_out;
   kp.rounds_out = rounds_out;
   if (kp.variant == 7 && kp.G > 0u && !node_out && !rounds_out) {
@@ -504,28 +540,18 @@ static int plan_launch_impl(bo_plan *pl, uint64_t trial_begin, uint64_t trial_co
     const char *cap_ev = getenv("BENOR_TEST_DEFER_SEG_CAP");
     const uint32_t test_seg_cap = cap_ev ? (uint32_t)strtoul(cap_ev, nullptr, 10) : 0u;
     if (pl->defer_words < words) {
-      if (pl->d_defer) {
-        uint32_t flag = 0;   // keep an overflow of an earlier launch reportable
-        HIP_TRY(hipDeviceSynchronize());
-        HIP_TRY(hipMemcpy(&flag, pl->d_defer + pl->defer_lens + benor::kDeferOverflowWord,
-                          sizeof flag, hipMemcpyDeviceToHost));
-        pl->defer_overflowed = pl->defer_overflowed || flag != 0u;
-        (void)hipFree(pl->d_defer);
-      }
+      if (pl->d_defer) (void)hipFree(pl->d_defer);
       pl->d_defer = nullptr;
       pl->defer_words = 0;
       HIP_TRY(hipMalloc(&pl->d_defer, sizeof(uint32_t) * words));
       pl->defer_words = words;
-      pl->defer_lens = cap;   // where the length block sits (bo_plan_check)
-      HIP_TRY(hipMemsetAsync(pl->d_defer + cap, 0, sizeof(uint32_t) * 64u, s));
     }
     uint32_t *const lens = pl->d_defer + cap;                           // pass r's output length: lens[16 (r - 1)]
     uint32_t *const segs = lens + 64u;
     uint32_t *const lists[2] = {pl->d_defer, segs + seg_words};         // pass r writes lists[(r - 1) & 1]
     for (uint64_t done = 0; done < trial_count;) {
       const uint64_t n = std::min<uint64_t>(trial_count - done, cap);
-      // every pass's length, one fill (the overflow flag after them persists)
-      HIP_TRY(hipMemsetAsync(lens, 0, sizeof(uint32_t) * 16u * std::max<uint32_t>(last_round, 1u), s));
+      HIP_TRY(hipMemsetAsync(lens, 0, sizeof(uint32_t) * 16u * std::max<uint32_t>(last_round, 1u), s));   // every pass's length
       kp.trial_begin = trial_begin + done;
       kp.trial_count = n;
       kp.defer_seg = segs;
@@ -541,7 +567,6 @@ static int plan_launch_impl(bo_plan *pl, uint64_t trial_begin, uint64_t trial_co
         kc.defer_list = lists[(r - 1u) & 1u];
         kc.defer_len = lens + 16u * (r - 1u);
         kc.defer_seg_cap = (uint32_t)seg_cap_of(benor::defer_units(kc, g));
-        kc.defer_overflow = lens + benor::kDeferOverflowWord;
         if (test_seg_cap) kc.defer_seg_cap = std::min<uint32_t>(kc.defer_seg_cap, test_seg_cap);
         HIP_TRY(benor::launch_lockstep(kc, g, s));
         r_last = r;
@@ -596,20 +621,16 @@ int bo_plan_run(bo_plan *pl, uint64_t trial_begin, uint64_t trial_count, uint64_
 
 int bo_plan_check(bo_plan *pl) {
   if (!pl) return fail(BO_ERR_INVALID_ARGUMENT, "NULL argument");
-  bool bad = pl->defer_overflowed;
-  if (pl->d_defer) {
-    HIP_TRY(hipDeviceSynchronize());
-    uint32_t *flag = pl->d_defer + pl->defer_lens + benor::kDeferOverflowWord;
-    uint32_t v = 0;
-    HIP_TRY(hipMemcpy(&v, flag, sizeof v, hipMemcpyDeviceToHost));
-    if (v) HIP_TRY(hipMemset(flag, 0, sizeof v));
-    bad = bad || v != 0u;
-  }
-  pl->defer_overflowed = false;
-  if (bad)
+  if (!pl->d_flag) return BO_OK;
+  HIP_TRY(hipDeviceSynchronize());
+  uint32_t v = 0;
+  HIP_TRY(hipMemcpy(&v, pl->d_flag, sizeof v, hipMemcpyDeviceToHost));
+  if (!v) return BO_OK;
+  HIP_TRY(hipMemset(pl->d_flag, 0, sizeof v));
+  if (v & 1u)
     return fail(BO_ERR_INTERNAL, "a matrix-core launch deferred more trials than its segment holds: "
                                  "its histogram is incomplete (deferral segment sizing)");
-  return BO_OK;
+  return fail(BO_ERR_INTERNAL, "an event-level message pool filled up: the affected trials stopped early");
 }
 
 int bo_run_trials(const bo_trials_cfg *cfg, uint64_t trial_begin, uint64_t trial_count, uint64_t *hist_host) {
@@ -731,6 +752,7 @@ int bo_run_trial_states(const bo_trials_cfg *cfg, uint64_t trial, bo_node_state 
   bo_plan_destroy(pl);
   if (e != hipSuccess) return hip_fail(e, "bo_run_trial_states");
   if (rc) return rc;
+  if (rounds & 0x80000000u) return fail(BO_ERR_INTERNAL, "event-level message pool filled up: the run stopped early");
   if (rounds_out) *rounds_out = rounds;
   return BO_OK;
 }

@@ -578,7 +578,7 @@ int oracle_run_trials(const orc_trials_cfg *cfg, uint64_t *hist, orc_node_state 
 }
 
 /* ===================================================================== */
-/* (iii) event-level asynchronous mode, N <= 256          */
+/* (iii) event-level asynchronous mode, N <= 4096         */
 /* ===================================================================== */
 /* Message-granular restatement of node.ts:43-199 with the reference's own
  * mid-run crash: GET /stop (node.ts:191-194) may hit a live node at any
@@ -614,14 +614,23 @@ typedef struct {
 
 typedef struct { int16_t c0, c1, len, pad; } orc_ibox;
 
+static int cmp_u64(const void *a, const void *b) {
+    const uint64_t x = *(const uint64_t *)a, y = *(const uint64_t *)b;
+    return x < y ? -1 : x > y;
+}
+
 /* bitsets over node ids (N <= ORC_EV_MAX_N) */
-#define ORC_EV_MAX_N 256u
+#define ORC_EV_MAX_N 4096u
 #define ORC_EV_NW (ORC_EV_MAX_N / 64u)
 typedef struct { uint64_t w[ORC_EV_NW]; } orc_set;
 static inline int set_has(const orc_set *s, uint32_t i) { return (int)((s->w[i >> 6] >> (i & 63u)) & 1u); }
 static inline void set_add(orc_set *s, uint32_t i) { s->w[i >> 6] |= 1ull << (i & 63u); }
+static uint32_t ev_nw = ORC_EV_NW;        /* words in use: ceil(N / 64) (set per trial, below) */
+#ifdef _OPENMP
+#pragma omp threadprivate(ev_nw)
+#endif
 static inline int set_union_full(const orc_set *a, const orc_set *b, const orc_set *all) {
-    for (uint32_t j = 0; j < ORC_EV_NW; ++j) if ((a->w[j] | b->w[j]) != all->w[j]) return 0;
+    for (uint32_t j = 0; j < ev_nw; ++j) if ((a->w[j] | b->w[j]) != all->w[j]) return 0;
     return 1;
 }
 
@@ -635,6 +644,7 @@ static uint32_t event_trial(const orc_event_cfg *cfg, uint64_t trial, orc_node_s
     uint32_t *live_ids = (uint32_t *)malloc(sizeof(uint32_t) * N), *cidx = (uint32_t *)malloc(sizeof(uint32_t) * N);
     uint32_t m = 0;
     orc_set killed, decided, all;
+    ev_nw = (N + 63u) / 64u;
     memset(&killed, 0, sizeof killed);
     memset(&decided, 0, sizeof decided);
     memset(&all, 0, sizeof all);
@@ -677,12 +687,12 @@ static uint32_t event_trial(const orc_event_cfg *cfg, uint64_t trial, orc_node_s
     uint8_t *pdone = (uint8_t *)calloc((size_t)N * KR, 1);
     size_t cap = (size_t)4 * N * N + 64, len = 0;
     uint32_t *pool = (uint32_t *)malloc(cap * sizeof(uint32_t));
-    /* message: to (8) | phase << 8 | (x & 3) << 9 | k << 11 */
+    /* message: to (12 bits) | phase << 12 | (x & 3) << 13 | k << 15 */
 #define EV_SEND(K, X, PH)                                                               \
     do {                                                                                \
         for (uint32_t to_ = 0; to_ < N; ++to_) {                                        \
             if (len == cap) { cap *= 2; pool = (uint32_t *)realloc(pool, cap * 4); }   \
-            pool[len++] = to_ | ((uint32_t)(PH) << 8) | ((uint32_t)((X) & 3) << 9) | ((uint32_t)(K) << 11); \
+            pool[len++] = to_ | ((uint32_t)(PH) << 12) | ((uint32_t)((X) & 3) << 13) | ((uint32_t)(K) << 15); \
         }                                                                               \
     } while (0)
     orc_rng rng;
@@ -693,11 +703,20 @@ static uint32_t event_trial(const orc_event_cfg *cfg, uint64_t trial, orc_node_s
     uint32_t cur = 1, R = 0;
     int halted = 0;                                      /* 1 decided, 2 k_max, 3 stall */
     uint64_t e = 0;
+    /* the schedule as (event, node) pairs in ascending order: the stops of
+     * event e are applied in node order, as a scan over i would */
+    uint64_t *stops = (uint64_t *)malloc(sizeof(uint64_t) * (N + 1));
+    uint32_t n_stops = 0, next_stop = 0;
+    for (uint32_t i = 0; i < N; ++i)
+        if (crash_at[i] != 0xFFFFFFFFu) stops[n_stops++] = ((uint64_t)crash_at[i] << 32) | i;
+    qsort(stops, n_stops, sizeof(uint64_t), cmp_u64);
     for (;;) {
         /* scheduled /stop (node.ts:191-194) */
         int crashed = 0;
-        for (uint32_t i = 0; i < N; ++i)
-            if (crash_at[i] == e && !set_has(&killed, i)) { set_add(&killed, i); st[i].killed = 1; crashed = 1; }
+        for (; next_stop < n_stops && (stops[next_stop] >> 32) == e; ++next_stop) {
+            const uint32_t i = (uint32_t)stops[next_stop];
+            if (!set_has(&killed, i)) { set_add(&killed, i); st[i].killed = 1; crashed = 1; }
+        }
         if (crashed && set_union_full(&killed, &killed, &all)) { halted = 3; break; }
         if (crashed) {
             while (cur < KR && set_union_full(&comp[cur], &killed, &all)) {
@@ -712,8 +731,8 @@ static uint32_t event_trial(const orc_event_cfg *cfg, uint64_t trial, orc_node_s
         const uint32_t msg = pool[pick];
         pool[pick] = pool[--len];
         ++e;
-        const uint32_t to = msg & 255u, ph = (msg >> 8) & 1u, k = msg >> 11;
-        const int8_t x = (int8_t)((msg >> 9) & 3u);
+        const uint32_t to = msg & 4095u, ph = (msg >> 12) & 1u, k = msg >> 15;
+        const int8_t x = (int8_t)((msg >> 13) & 3u);
         if (set_has(&killed, to)) continue;              /* node.ts:45 */
         if (k >= KR) continue;
         orc_ibox *b = &ib[((size_t)to * KR + k) * 2 + ph];
@@ -746,7 +765,7 @@ static uint32_t event_trial(const orc_event_cfg *cfg, uint64_t trial, orc_node_s
         }
     }
 #undef EV_SEND
-    free(ib); free(comp); free(pdone); free(pool); free(crash_at);
+    free(ib); free(comp); free(pdone); free(pool); free(crash_at); free(stops);
     if (events_out) *events_out = e;
     /* outcome over the nodes still running */
     int any0 = 0, any1 = 0, anyq = 0, nlive = 0;

@@ -8,10 +8,11 @@ delivery counts (bo_consensus_start_sched; startConsensus(..., stop_after) in
 Python, startConsensus(N, {stopAfter}) in js/index.js): the network API runs
 the event-level kernel for one trial and serves its final per-node states.
 
-GPU: per-node states equal oracle (iii) event_trial (oracle/benor_oracle.c
-:630-763, trial 0 of the same seed and schedule) at N = 5, 10 and 256, with
-stops inside round 1 and inside round 2, through the C ABI and through the
-N-API addon.  CPU: the schedule's validation.
+GPU: per-node states equal oracle (iii) event_trial (oracle/benor_oracle.c,
+trial 0 of the same seed and schedule) at N = 5, 10, 256 (one lane per
+trial, benor_event_kernel) and N = 1024, 4096 (one wave per trial,
+benor_event_big.hip), with stops inside round 1 and inside round 2, through
+the C ABI and through the N-API addon.  CPU: the schedule's validation.
 """
 import json
 import os
@@ -65,7 +66,23 @@ def cases():
     # stalls after it (node.ts:52, :88), as the reference's network hangs.
     out.append((case(256, 84, [i % 2 for i in range(172)], {90: 5000}, seed=32), {90: 1}))
     out.append((case(256, 84, [i % 2 for i in range(172)], {150: 140000}, seed=33), {150: 2}))
+    out.extend(big_cases())
     return out
+
+
+def big_cases():
+    """Networks above the one-lane event kernel's N <= 256 (benor_event_big.hip,
+    VERDICT r03 #2): BASELINE configs[3]'s N = 1024, F = 341 and configs[4]'s
+    N = 4096, F = 1365.  m is odd there, so a random start decides in round 1;
+    as many 1s as 0s plus one "?" make every R-phase tie (node.ts:63-69) and
+    every node take its coin, so the run reaches round 2.  Round 1 spans
+    2 m N deliveries (1 398 784 at N = 1024, 22 372 352 at N = 4096)."""
+    def half(m):
+        return [1] * (m // 2) + [0] * (m // 2) + ["?"]
+    return [(case(1024, 341, half(683), {500: 300_000}, seed=41), {500: 1}),
+            (case(1024, 341, half(683), {700: 1_900_000, 1000: 2_000_000}, seed=42), {700: 2, 1000: 2}),
+            (case(4096, 1365, half(2731), {3000: 5_000_000}, seed=43), {3000: 1}),
+            (case(4096, 1365, half(2731), {4000: 30_000_000}, seed=44), {4000: 2})]
 
 
 def oracle_states(c):
@@ -80,9 +97,9 @@ def oracle_states(c):
 
 
 def test_schedule_validation():
-    benor.launchNetwork(300, 0, [1] * 300, [False] * 300)
-    with pytest.raises(RuntimeError, match="libbenor error 7"):          # event-level kernel: N <= 256
-        benor.startConsensus(300, seed=1, stop_after={5: 10})
+    # a random /stop schedule (batch API crash_count) needs the one-lane event kernel: N <= 256
+    with pytest.raises(RuntimeError, match="libbenor error 7"):
+        benor.TrialsPlan(300, 0, [False] * 300, mode=benor.BO_MODE_EVENT, crash_count=3, crash_window=100)
     benor.launchNetwork(5, 1, [1, 1, 1, 0, 0], [False, False, False, False, True])
     L = benor.lib()
     sched = (benor.ctypes.c_uint32 * 3)(1, 2, 3)

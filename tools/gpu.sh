@@ -10,7 +10,8 @@
 # says which files were copied into profiles/ from which step.
 #
 #   smoke           __graft_entry__.smoke()
-#   tests           pytest -m gpu (PYTEST_ARGS: test paths / options, default the whole GPU suite)
+#   tests           pytest -m gpu (PYTEST_ARGS: test paths / options, default the whole GPU suite;
+#                   PYTEST_K: a -k expression, spaces allowed)
 #   probe           tools/mfma_fp4_layout_probe (e2m1 MFMA K pairing)
 #   bench           python bench.py (BENCH_ARGS, default the driver's --steps 20 --warmup 5)
 #   trace           rocprofv3 --kernel-trace --stats of the same bench command
@@ -61,7 +62,7 @@ for step in "$@"; do
       timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
       chk $? smoke; tail -1 "$OUT/smoke.log";;
     tests)
-      timeout -k 10 900 python -u -m pytest ${PYTEST_ARGS:-tests} -m gpu -x -v --timeout 200 --timeout-method thread \
+      timeout -k 10 900 python -u -m pytest ${PYTEST_ARGS:-tests} ${PYTEST_K:+-k "$PYTEST_K"} -m gpu -x -v --timeout 200 --timeout-method thread \
         > "$OUT/tests.log" 2>&1
       rc=$?; tail -3 "$OUT/tests.log"; chk $rc tests;;
     probe)
