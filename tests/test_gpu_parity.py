@@ -438,3 +438,53 @@ def test_random_delivery_r04_kernel_equals_r02_kernel(N, F, f, T, init):
     finally:
         os.environ.pop("BENOR_RANDOM_V1", None)
     np.testing.assert_array_equal(new.run(99, T), old.run(99, T))
+
+
+# ------------------------------------- event level above N = 256 (benor_event_big.hip)
+@pytest.mark.parametrize("N,F,trials,stops,init", [
+    (257, 0, 6, None, None), (300, 100, 5, {150: 20_000, 299: 55_000}, None), (512, 170, 3, None, "tied"),
+    (700, 233, 2, {300: 100}, None), (1000, 0, 2, None, None), (513, 256, 2, None, None)])
+def test_event_mode_big_matches_oracle(N, F, trials, stops, init):
+    """One wave per trial (256 < N <= 4096): histograms of several trials
+    (batched speculative picks, overlay write-back, triggers mid-batch, stops at
+    batch boundaries) equal oracle (iii) event_trial; with fixed tied starts the
+    runs reach round 2 through coins; F = N/2 - ... (513, 256) cannot decide."""
+    fl = first_f(N, F)
+    seed = 0xB16 ^ N
+    sched = None
+    if stops:
+        sched = [None] * N
+        for node, e in stops.items():
+            sched[node] = e
+    vals = None
+    if init == "tied":
+        m = N - F
+        vals = [0] * F + [i % 2 for i in range(m)]
+    got = benor.TrialsPlan(N, F, fl, seed=seed, k_max=8, mode=EV, crash_at=sched, initial_values=vals).run(7, trials)
+    ref, _ = oracle.event_trials(N, F, fl, seed=seed, trial_begin=7, trial_count=trials, k_max=8, crash_at=sched,
+                                 initial_values=vals)
+    np.testing.assert_array_equal(got, ref.hist)
+
+
+def test_event_mode_big_without_stop_equals_lockstep_kernel():
+    """Without a /stop every phase completes with the whole live set, so the
+    delivery order cannot change a tally: the big event kernel's histogram is
+    the lockstep kernel's."""
+    for N, F in [(300, 99), (1024, 341), (600, 0)]:
+        fl = first_f(N, F)
+        a = benor.TrialsPlan(N, F, fl, seed=9, k_max=16, mode=EV).run(0, 40)
+        b = benor.TrialsPlan(N, F, fl, seed=9, k_max=16).run(0, 40)
+        np.testing.assert_array_equal(a, b)
+
+
+def test_event_mode_big_states_match_oracle():
+    """Per-node states of one trial (bo_run_trial_states, the network API's
+    launch) at N = 1024 with two scheduled stops in round 1."""
+    N, F = 1024, 341
+    fl = first_f(N, F)
+    sched = [None] * N
+    sched[400], sched[900] = 120_000, 700_000
+    _, st = benor.run_trial_states(N, F, fl, seed=77, trial=0, k_max=16, mode=EV, crash_at=sched)
+    ref, _ = oracle.event_trials(N, F, fl, seed=77, trial_begin=0, trial_count=1, k_max=16, crash_at=sched,
+                                 want_states=True)
+    assert st == ref.states
