@@ -218,7 +218,7 @@ class Network:
     def start(self, seed: int | None = None, k_max: int = DEFAULT_K_MAX, stop_after=None) -> None:
         """stop_after: GET /stop requests that land during the run -- {node: deliveries} or a
         length-N sequence (None = not stopped); deliveries = POST /message handled network-wide
-        before the stop (bo_consensus_start_sched: the event-level kernel, N <= 256)."""
+        before the stop (bo_consensus_start_sched: the event-level kernels, N <= 4096)."""
         if seed is None:
             seed = secrets.randbits(64)        # the reference's coin is Math.random()
         if not stop_after:

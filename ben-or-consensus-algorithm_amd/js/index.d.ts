@@ -37,7 +37,7 @@ export interface StartOptions {
   kMax?: number;
   /** GET /stop requests landing mid-run (node.ts:191-194): per node, the number of
    * POST /message deliveries (network-wide, seeded order) after which it is stopped;
-   * an array of N entries (null = never) or {nodeId: deliveries}.  Event-level kernel, N <= 256. */
+   * an array of N entries (null = never) or {nodeId: deliveries}.  Event-level kernels, N <= 4096. */
   stopAfter?: (number | null)[] | { [nodeId: number]: number };
   /** Reject a second start on one network (libbenor error 8) instead of resolving as a no-op. */
   strict?: boolean;
@@ -63,7 +63,7 @@ export interface TrialsConfig {
   kMax?: number;
   trialBegin?: bigint | number;
   trialCount?: bigint | number;
-  /** 0 lockstep (default), 1 random delivery (f <= F), 2 event level (N <= 256) */
+  /** 0 lockstep (default), 1 random delivery (f <= F), 2 event level (N <= 4096; crashCount needs N <= 256) */
   mode?: 0 | 1 | 2;
   /** event mode: deliveries after which node i is stopped (null = never) */
   crashAt?: (number | null)[];

@@ -68,7 +68,7 @@ function randomSeed() {
 // (node.ts:191-194) -- an array of N delivery counts or an object
 // {nodeId: deliveries}; a node is stopped after that many POST /message have
 // been handled network-wide (seeded delivery order, the event-level kernel,
-// N <= 256).
+// N <= 4096).
 // A second start on the same network resolves, as the reference's GET /start
 // answers 200, but runs nothing: its round inboxes outlive a run (node.ts:29-30),
 // so no fresh consensus can follow (options.strict: reject with libbenor error 8).

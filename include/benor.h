@@ -56,7 +56,9 @@ enum {
 /* EVENT is message-granular: the reference's handler
  * (node.ts:45-158) delivery by delivery, in a seeded random order, with the
  * reference's mid-run GET /stop (node.ts:191-194) applied at scheduled
- * delivery counts.  Exactly F crash-faulty nodes; N <= 256. */
+ * delivery counts.  Exactly F crash-faulty nodes; N <= 4096 (one lane per
+ * trial up to N = 256, one wave per trial above; a random /stop schedule,
+ * crash_count, needs N <= 256). */
 enum { BO_MODE_LOCKSTEP = 0, BO_MODE_RANDOM_DELIVERY = 1, BO_MODE_EVENT = 2 };
 
 enum { BO_INIT_RANDOM = 0, BO_INIT_FIXED = 1 };
@@ -108,8 +110,9 @@ int bo_consensus_start(bo_network *net, uint64_t seed, uint32_t k_max);
  * UINT32_MAX = not stopped.  Deliveries follow BO_MODE_EVENT's seeded order
  * (trial 0 of `seed`), so a schedule is reproducible.  With every entry
  * UINT32_MAX (or stop_after NULL) this is bo_consensus_start; otherwise the
- * run is message-granular on the event-level kernel (N <= 256, else
- * BO_ERR_UNSUPPORTED) and the per-node states are its final ones, scheduled
+ * run is message-granular on the event-level kernel (any N <= BO_MAX_N; a
+ * schedule whose entries all name killed nodes is bo_consensus_start) and the
+ * per-node states are its final ones, scheduled
  * stops included (killed, x / decided / k as of the stop).  The auto-stop and
  * one-start rules of bo_consensus_start apply. */
 int bo_consensus_start_sched(bo_network *net, uint64_t seed, uint32_t k_max,
