@@ -109,10 +109,39 @@ def cmd_sweep(a) -> int:
         # a cell's rows depend only on (N, F, seed, per-cell trials, k_max)
         cells = [tuple(_int(x) for x in c.split(":")) for c in a.cells.split(",")]
     else:
-        Ns = _ints(a.N)
-        phis = [i * 0.5 / a.steps for i in range(a.steps)]
-        cells = [(N, int(phi * N)) for N in Ns for phi in phis]
+        cells = grid_cells(_ints(a.N), a.steps)
     per_cell = _int(str(a.per_cell)) if a.per_cell else max(1, _int(str(a.trials)) // len(cells))
+    rows, elapsed = run_sweep(cells, per_cell, a.seed, a.k_max, a.streams, rank, world, a.progress)
+    if rank == 0:
+        out = open(a.out, "w") if a.out else sys.stdout
+        out.write(rows_csv(rows))
+        if a.out:
+            out.close()
+        total = per_cell * len(cells)
+        print(json.dumps({"cells": len(cells), "trials": total, "seconds": elapsed, "gpus": world}), file=sys.stderr)
+    return 0
+
+
+def grid_cells(Ns: list[int], steps: int) -> list[tuple[int, int]]:
+    """C5 cells: every N crossed with F = floor(phi N), phi on a `steps` grid in [0, 0.5)."""
+    phis = [i * 0.5 / steps for i in range(steps)]
+    return [(N, int(phi * N)) for N in Ns for phi in phis]
+
+
+def rows_csv(rows: list[dict]) -> str:
+    keys = list(rows[0].keys())
+    return ",".join(keys) + "\n" + "".join(",".join(str(r[k]) for k in keys) + "\n" for r in rows)
+
+
+def run_sweep(cells, per_cell, seed, k_max, streams_n=4, rank=0, world=1, progress=False):
+    """The sweep's GPU work on the current device: (rows, seconds).  Under
+    torch.distributed (world > 1) each cell's trials are split over the ranks
+    and the histograms merged by one all-reduce."""
+    import torch
+
+    import benor
+    from benor.parallel import merge_histogram, strong_range
+
     # The device context comes up before the clock starts (~0.08 s on a fresh
     # process): "seconds" times the sweep -- plans, launches, merge, read-back.
     torch.zeros(1, device="cuda")
@@ -124,34 +153,26 @@ def cmd_sweep(a) -> int:
     # round-robin over --streams streams: each plan owns its buffers, so cells are
     # independent, and one cell's short passes (deferred-trial rounds, the last
     # groups of a launch) overlap the next cell's launches instead of idling CUs.
-    plans = [benor.TrialsPlan(N, F, seed=a.seed ^ (N << 20) ^ F, k_max=a.k_max) for (N, F) in cells]
+    plans = [benor.TrialsPlan(N, F, seed=seed ^ (N << 20) ^ F, k_max=k_max) for (N, F) in cells]
     H = plans[0].hist_len
     hists = torch.zeros((len(cells), H), dtype=torch.int64, device="cuda")
-    streams = [stream] + [torch.cuda.Stream() for _ in range(max(1, a.streams) - 1)]
+    streams = [stream] + [torch.cuda.Stream() for _ in range(max(1, streams_n) - 1)]
     for s in streams[1:]:
         s.wait_stream(stream)                      # the zeroed histograms
     b, n = strong_range(0, per_cell, rank, world)
     for ci, plan in enumerate(plans):
         plan.launch(b, n, hists[ci].data_ptr(), streams[ci % len(streams)].cuda_stream)
-        if rank == 0 and a.progress:
+        if rank == 0 and progress:
             print(f"[{ci + 1}/{len(cells)}] N={cells[ci][0]} F={cells[ci][1]} queued", file=sys.stderr, flush=True)
     for s in streams[1:]:
         stream.wait_stream(s)
     merge_histogram(hists)
     allh = hists.cpu().numpy().astype(np.uint64)
-    rows = [summarize(allh[ci], N, F, a.k_max) for ci, (N, F) in enumerate(cells)]
+    rows = [summarize(allh[ci], N, F, k_max) for ci, (N, F) in enumerate(cells)]
     elapsed = time.perf_counter() - t0
-    if rank == 0:
-        keys = list(rows[0].keys())
-        out = open(a.out, "w") if a.out else sys.stdout
-        out.write(",".join(keys) + "\n")
-        for r in rows:
-            out.write(",".join(str(r[k]) for k in keys) + "\n")
-        if a.out:
-            out.close()
-        total = per_cell * len(cells)
-        print(json.dumps({"cells": len(cells), "trials": total, "seconds": elapsed, "gpus": world}), file=sys.stderr)
-    return 0
+    for plan in plans:
+        plan.check()                               # device-side capacity invariants of every cell
+    return rows, elapsed
 
 
 def main(argv=None) -> int:

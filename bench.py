@@ -301,6 +301,44 @@ def random_delivery_config(benor, torch, k_max, seed, N=1024, F=341, f=0, T=100_
                          "floor_frac": rate * 41 * 2 * d["floor_blocks"] / SPEC_PEAK_POPC}}
 
 
+def c5_sweep():
+    """BASELINE configs[4] on this GPU: the full C5 phase diagram (N in
+    {64..4096} x 32 values of F/N in [0, 0.5), 2^30 trials; benor.cli sweep,
+    DESIGN.md §4.5) in this process, wall time from the first plan to the
+    read-back, and whether its CSV equals the committed one byte for byte."""
+    from benor.cli import grid_cells, rows_csv, run_sweep
+
+    cells = grid_cells([64, 128, 256, 512, 1024, 2048, 4096], 32)
+    per_cell = (1 << 30) // len(cells)
+    rows, seconds = run_sweep(cells, per_cell, 0x243F6A8885A308D3, 32)
+    csv = rows_csv(rows)
+    ref = os.path.join(ROOT, "results", "r02_sweep_c5.csv")
+    same = os.path.exists(ref) and open(ref).read() == csv
+    return {"cells": len(cells), "trials": per_cell * len(cells), "seconds": seconds,
+            "trials_per_s": per_cell * len(cells) / seconds, "csv_sha256": hashlib.sha256(csv.encode()).hexdigest()[:16],
+            "csv_equals_results_r02_sweep_c5": same}
+
+
+def event_network(benor, N=1024, F=341, stop_node=500, stop_after=300_000, seed=41):
+    """SURVEY §8f #2 at BASELINE configs[3]'s size: one network through the
+    reference's calls -- launchNetwork, startConsensus with a mid-run GET /stop
+    of one node after `stop_after` deliveries (node.ts:191-194) -- on the
+    event-level kernel for N > 256 (one wave per trial, benor_event_big.hip).
+    Wall time of startConsensus and the deliveries it simulated."""
+    m = N - F
+    init = [0] * F + [1] * (m // 2) + [0] * (m // 2) + ["?"] * (m % 2)
+    faulty = [i < F for i in range(N)]
+    out = {}
+    for label, sched in (("no stop (lockstep kernel)", None), ("stop inside round 1", {stop_node: stop_after})):
+        benor.launchNetwork(N, F, init, faulty)
+        t0 = time.perf_counter()
+        benor.startConsensus(N, seed=seed, stop_after=sched)
+        dt = time.perf_counter() - t0
+        st = benor.getNodesState(N)
+        out[label] = {"seconds": dt, "stopped_nodes": sum(1 for s in st[F:] if s["killed"])}
+    return {"N": N, "F": F, "initial_values": "half 1, half 0, one '?' (every R-phase ties)", **out}
+
+
 def network_latency(benor, reps=200):
     """BASELINE configs[0]: one start.ts-style network (N=5, F=1, node 4 faulty,
     initial values [1,1,1,0,0], benorconsensus.test.ts:179-223) through the
@@ -458,6 +496,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = [a.elapsed_time(b) for a, b in ev]
+    plan.check()                                   # device-side capacity invariants of the timed launches
     t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     if distributed:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -526,6 +565,8 @@ def main():
         out["other_configs"] = other_configs(benor, torch, k_max, args.seed)
         out["other_configs"]["C1 N=5,F=1 network API"] = network_latency(benor)
         out["other_configs"]["C4 N=1024,F=341,f=0 random delivery"] = random_delivery_config(benor, torch, k_max, args.seed)
+        out["other_configs"]["C4 N=1024,F=341 network API, mid-run /stop"] = event_network(benor)
+        out["other_configs"]["C5 sweep (2^30 trials, 224 cells)"] = c5_sweep()
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(N, F, k_max, args.seed, args.cpu_seconds)
     if rank == 0:
