@@ -54,8 +54,9 @@ struct DStream {
   uint32_t k0, k1, c0, c1, c2, c3;
   uint4 buf;
   uint32_t widx;
+  uint32_t sh;           // block index position in c2: 0 (delivery stream), 12 (crash stream)
   __device__ __forceinline__ uint32_t next() {
-    if ((widx & 3u) == 0u) buf = philox4x32_10(k0, k1, make_uint4(c0, c1, c2 | ((widx >> 2) << 12), c3));
+    if ((widx & 3u) == 0u) buf = philox4x32_10(k0, k1, make_uint4(c0, c1, c2 | ((widx >> 2) << sh), c3));
     const uint32_t j = widx & 3u;
     ++widx;
     return j == 0 ? buf.x : j == 1 ? buf.y : j == 2 ? buf.z : buf.w;
@@ -120,7 +121,7 @@ __device__ __forceinline__ void bernoulli_fixup(uint32_t *__restrict__ B, uint32
   const uint32_t lb = (uint32_t)(uintptr_t)(lds_u32 *)B + lane * 4u;   // LDS address of this lane's word 0
   for (uint32_t blk = blk0;; ++blk) {
     if (!__any(need != 0u)) break;
-    const uint4 bb = philox4x32_10(k0, k1, make_uint4(tlo, thi, c2 | (blk << 12), c3));
+    const uint4 bb = philox4x32_10(k0, k1, make_uint4(tlo, thi, c2 | blk, c3));
     const uint32_t u4[4] = {bb.x, bb.y, bb.z, bb.w};
 #pragma unroll
     for (int g = 0; g < NF; g += 4) {
@@ -167,7 +168,7 @@ __device__ __forceinline__ uint32_t bernoulli_words(uint32_t *__restrict__ B, ui
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
       if (j == 0 || w0 + (uint32_t)((4 * j) / NW) < W32) {    // blocks a partial super-block needs
-        const uint4 bb = philox4x32_10(k0, k1, make_uint4(tlo, thi, c2 | ((blk + j) << 12), c3));
+        const uint4 bb = philox4x32_10(k0, k1, make_uint4(tlo, thi, c2 | (blk + j), c3));
         u[4 * j] = bb.x, u[4 * j + 1] = bb.y, u[4 * j + 2] = bb.z, u[4 * j + 3] = bb.w;
       }
     }
@@ -237,7 +238,8 @@ __device__ __forceinline__ void random_tally(const uint4 *__restrict__ plane, ui
   // lane's stream position is block-aligned and none of the 4 products needs
   // Lemire's exact rejection test; otherwise one exact DStream step (same
   // words, same result -- the oracle's definition).
-  const uint32_t c2 = node & 0xFFFu, c3 = (r & 0xFFFFFu) | ((phase & 1u) << 20) | (kStreamDelivery << 24);
+  // delivery counter {tlo, thi, block | round << 16 | phase << 31, node | 2 << 24} (oracle_delivery_mask)
+  const uint32_t c2 = ((r & 0x7FFFu) << 16) | ((phase & 1u) << 31), c3 = (node & 0xFFFu) | (kStreamDelivery << 24);
   if (bern) bernoulli_mask(B, m, q, active, rd_a, rd_b, k0, k1, tlo, thi, c2, c3);
   const uint32_t lb = (uint32_t)(uintptr_t)(lds_u32 *)B + lane * 4u;   // LDS address of this lane's word 0
   uint32_t jj = m - k, widx = 0;
@@ -246,7 +248,7 @@ __device__ __forceinline__ void random_tally(const uint4 *__restrict__ plane, ui
     if (!__any(go)) break;
     bool fast = go && (widx & 3u) == 0u;
     if (fast) {
-      const uint4 b = philox4x32_10(k0, k1, make_uint4(tlo, thi, c2 | ((widx >> 2) << 12), c3));
+      const uint4 b = philox4x32_10(k0, k1, make_uint4(tlo, thi, c2 | (widx >> 2), c3));
       const uint64_t q0 = (uint64_t)b.x * (jj + 1u), q1 = (uint64_t)b.y * (jj + 2u);
       const uint64_t q2 = (uint64_t)b.z * (jj + 3u), q3 = (uint64_t)b.w * (jj + 4u);
       // Lemire's exact test is needed only when a low word is below its range;
@@ -273,7 +275,7 @@ __device__ __forceinline__ void random_tally(const uint4 *__restrict__ plane, ui
     }
     if (go && !fast) {
       DStream ds;
-      ds.k0 = k0; ds.k1 = k1; ds.c0 = tlo; ds.c1 = thi; ds.c2 = c2; ds.c3 = c3;
+      ds.k0 = k0; ds.k1 = k1; ds.c0 = tlo; ds.c1 = thi; ds.c2 = c2; ds.c3 = c3; ds.sh = 0u;
       ds.widx = widx & ~3u;                                      // refill the current block, then skip to widx
       for (uint32_t i = ds.widx; i < widx; ++i) (void)ds.next();
       const uint32_t t = ds.uniform(jj + 1u);
@@ -558,6 +560,7 @@ __global__ void __launch_bounds__(256) benor_event_kernel(KParams p) {
     } else if (p.crash_count > 0 && m > 0 && p.crash_window > 0) {
       DStream ds;
       ds.k0 = k0; ds.k1 = k1; ds.c0 = tlo; ds.c1 = thi; ds.c2 = 0u; ds.c3 = kStreamCrash << 24; ds.widx = 0;
+      ds.sh = 12u;
       const uint32_t kk = p.crash_count < m ? p.crash_count : m;
       // Floyd over compact live indices; the picks go to the crash list first
       // (node field = compact index), then get their event indices in pick order

@@ -12,11 +12,12 @@
 // One wave = one trial, lane l of receiver group j = live node 64 j + l.  What
 // changed against r02 (the same bits, fewer instructions):
 //
-//   * Philox: the delivery counter is {trial_lo, trial_hi, node | blk << 12,
-//     round | phase << 20 | 2 << 24}; only its third word varies across the
-//     lanes, so round 1's first product and round 2's second product are
-//     wave-uniform.  They are computed once per (trial, round, phase) in SGPRs
-//     (DlvUni): 18 v_mad_u64_u32 and 19 xors per block instead of 20 and 20.
+//   * Philox: the delivery counter is {trial_lo, trial_hi, blk | round << 16 |
+//     phase << 31, node | 2 << 24} (r04 layout: the receiver in the last word,
+//     the block in the third), so the first rounds' products that do not
+//     involve the receiver are wave-uniform (scalar unit) and the one that
+//     does not involve the block is computed once per receiver-phase
+//     (dlv_block): 15 v_mad_u64_u32 and 17 xors per block instead of 20 and 20.
 //   * fix-up: one ds_mskor_rtn_b32 per field tests and flips in one LDS op
 //     (mask = the sender's bit, data = its target value), so a sender named
 //     twice is refused by the LDS state itself, in stream order.  The fields
@@ -41,34 +42,48 @@ constexpr uint32_t kM0 = 0xD2511F53u, kM1 = 0xCD9E8D57u, kW0 = 0x9E3779B9u, kW1 
 
 typedef __attribute__((address_space(3))) uint32_t lds_word;
 
-// Wave-uniform part of the delivery stream's Philox for one (trial, round,
-// phase): counter {tlo, thi, c2 (per lane), c3}.
-struct DlvUni {
-  uint32_t u1;    // thi ^ K0[1]                     round 1: x1 = hi(M1 c2) ^ u1
-  uint32_t u2x;   // hi(M1 z1) ^ K0[2]               round 2: x2 = lo(M1 c2) ^ u2x
-  uint32_t u2z;   // lo(M0 tlo) ^ K1[2]              round 2: z2 = hi(M0 x1) ^ u2z
-  uint32_t u3x;   // lo(M1 z1) ^ K0[3]               round 3: x3 = hi(M1 z2) ^ u3x
+// The delivery stream's counter is {tlo, thi, c2 = block | round << 16 |
+// phase << 31, c3 = node | 2 << 24} (oracle_delivery_mask): within a trial's
+// (round, phase) only c3 differs between receivers and only c2 between
+// blocks.  So, per Philox4x32-10 block:
+//   round 1: M0 tlo is per trial; M1 c2 is per block (wave-uniform);
+//            x1 = hi(M1 c2) ^ thi ^ K0[1] is wave-uniform; z1 = hi(M0 tlo) ^ c3 ^ K1[1]
+//            is per receiver but the same for every block;
+//   round 2: M0 x1 is per block (uniform); M1 z1 is per receiver (once per
+//            receiver-phase); x2 = hi(M1 z1) ^ lo(M1 c2) ^ K0[2] -- one xor;
+//   round 3: M1 z2 is per block (uniform); M0 x2 is the first per-lane product;
+//   rounds 4..10 as Philox.
+// 15 v_mad_u64_u32 and 17 xors per block instead of 20 and 20; the uniform
+// products go to the scalar unit.
+struct DlvUni {            // per (trial, round, phase), wave-uniform
+  uint32_t k0, k1, thi, c2, a1, w1;   // a1 = hi(M0 tlo) ^ K1[1], w1 = lo(M0 tlo)
+};
+struct DlvRecv {           // per receiver-phase (lane)
+  uint32_t h1, l1;         // M1 z1, z1 = c3 ^ a1
 };
 
 __device__ __forceinline__ uint32_t sgpr(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 
-__device__ __forceinline__ DlvUni dlv_uniforms(uint32_t k0, uint32_t k1, uint32_t tlo, uint32_t thi, uint32_t c3) {
-  // z1 = hi(M0 tlo) ^ c3 ^ K1[1]; round 2's second product M1 z1
+__device__ __forceinline__ DlvUni dlv_uniforms(uint32_t k0, uint32_t k1, uint32_t tlo, uint32_t thi, uint32_t r,
+                                              uint32_t phase) {
   const uint64_t p0 = (uint64_t)kM0 * tlo;
-  const uint32_t z1 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
-  const uint64_t p1 = (uint64_t)kM1 * z1;
   DlvUni u;
-  u.u1 = sgpr(thi ^ k0);
-  u.u2x = sgpr((uint32_t)(p1 >> 32) ^ (k0 + kW0));
-  u.u2z = sgpr((uint32_t)p0 ^ (k1 + kW1));
-  u.u3x = sgpr((uint32_t)p1 ^ (k0 + 2u * kW0));
+  u.k0 = sgpr(k0);
+  u.k1 = sgpr(k1);
+  u.thi = sgpr(thi);
+  u.c2 = sgpr(((r & 0x7FFFu) << 16) | ((phase & 1u) << 31));
+  u.a1 = sgpr((uint32_t)(p0 >> 32) ^ k1);
+  u.w1 = sgpr((uint32_t)p0);
   return u;
 }
 
-// 32 x 32 -> 64-bit product: the compiler selects v_mad_u64_u32 (carry-out to
-// an SGPR pair it allocates, so its hazard recognizer sees every write; the
-// inline-asm form with a VCC clobber costs an s_nop per product).
 __device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t m) { return (uint64_t)a * m; }
+
+__device__ __forceinline__ DlvRecv dlv_receiver(const DlvUni &u, uint32_t node) {
+  const uint32_t z1 = (node & 0xFFFu) ^ (kStreamDelivery << 24) ^ u.a1;
+  const uint64_t p = mad64(z1, kM1);
+  return DlvRecv{(uint32_t)(p >> 32), (uint32_t)p};
+}
 
 __device__ __forceinline__ uint32_t xor_s(uint32_t v, uint32_t s) {   // v ^ s, s wave-uniform
   uint32_t r;
@@ -76,26 +91,34 @@ __device__ __forceinline__ uint32_t xor_s(uint32_t v, uint32_t s) {   // v ^ s, 
   return r;
 }
 
-// Philox4x32-10 block {x, y, z, w} of the delivery counter {tlo, thi, c2, c3}
-// -- the same value as philox4x32_10(k0, k1, {tlo, thi, c2, c3}).
-__device__ __forceinline__ uint4 dlv_block(uint32_t k0, uint32_t k1, const DlvUni &u, uint32_t c2) {
-  // round 1: (hi0, lo0) = M0 tlo is uniform (in u), (h1, l1) = M1 c2
-  const uint64_t a = mad64(c2, kM1);
-  const uint32_t x1 = xor_s((uint32_t)(a >> 32), u.u1), y1 = (uint32_t)a;
-  // round 2: (h0, l0) = M0 x1; M1 z1 is uniform
-  const uint64_t b = mad64(x1, kM0);
-  uint4 c = make_uint4(xor_s(y1, u.u2x), 0u, xor_s((uint32_t)(b >> 32), u.u2z), (uint32_t)b);
-  // round 3: y2 = lo(M1 z1) is uniform (folded into u3x)
-  {
-    const uint64_t p0 = mad64(c.x, kM0), p1 = mad64(c.z, kM1);
-    c = make_uint4(xor_s((uint32_t)(p1 >> 32), u.u3x), (uint32_t)p1, xor3_key((uint32_t)(p0 >> 32), c.w, k1 + 2u * kW1),
-                   (uint32_t)p0);
-  }
+// Philox4x32-10 block `blk` of the receiver's delivery stream -- the value of
+// philox4x32_10(k0, k1, {tlo, thi, c2 | blk, c3}).
+__device__ __forceinline__ uint4 dlv_block(const DlvUni &u, const DlvRecv &v, uint32_t blk) {
+  const uint32_t k0 = u.k0, k1 = u.k1;
+  // wave-uniform part (scalar unit)
+  const uint64_t P = (uint64_t)kM1 * sgpr(u.c2 | blk);            // round 1: M1 c2
+  const uint32_t x1 = (uint32_t)(P >> 32) ^ u.thi ^ k0;
+  const uint64_t Q = (uint64_t)kM0 * x1;                           // round 2: M0 x1
+  const uint32_t z2 = (uint32_t)(Q >> 32) ^ u.w1 ^ (k1 + kW1);
+  const uint64_t S = (uint64_t)kM1 * z2;                           // round 3: M1 z2
+  const uint32_t s_x2 = sgpr((uint32_t)P ^ (k0 + kW0));
+  const uint32_t s_x3 = sgpr((uint32_t)(S >> 32) ^ (k0 + 2u * kW0));
+  const uint32_t s_z3 = sgpr((uint32_t)Q ^ (k1 + 2u * kW1));
+  const uint32_t s_x4 = sgpr((uint32_t)S ^ (k0 + 3u * kW0));
+  // round 2: x2 = hi(M1 z1) ^ lo(M1 c2) ^ K0[2]; y2 = lo(M1 z1)
+  const uint32_t x2 = xor_s(v.h1, s_x2);
+  // round 3: x3 = hi(M1 z2) ^ y2 ^ K0[3]; z3 = hi(M0 x2) ^ lo(M0 x1) ^ K1[3]
+  const uint64_t a = mad64(x2, kM0);
+  const uint32_t x3 = xor_s(v.l1, s_x3), z3 = xor_s((uint32_t)(a >> 32), s_z3), w3 = (uint32_t)a;
+  // round 4: y3 = lo(M1 z2) is uniform (in s_x4)
+  const uint64_t p0 = mad64(x3, kM0), p1 = mad64(z3, kM1);
+  uint4 c = make_uint4(xor_s((uint32_t)(p1 >> 32), s_x4), (uint32_t)p1,
+                       xor3_key((uint32_t)(p0 >> 32), w3, k1 + 3u * kW1), (uint32_t)p0);
 #pragma unroll
-  for (uint32_t r = 3; r < 10; ++r) {
-    const uint64_t p0 = mad64(c.x, kM0), p1 = mad64(c.z, kM1);
-    c = make_uint4(xor3_key((uint32_t)(p1 >> 32), c.y, k0 + r * kW0), (uint32_t)p1,
-                   xor3_key((uint32_t)(p0 >> 32), c.w, k1 + r * kW1), (uint32_t)p0);
+  for (uint32_t r = 4; r < 10; ++r) {
+    const uint64_t q0 = mad64(c.x, kM0), q1 = mad64(c.z, kM1);
+    c = make_uint4(xor3_key((uint32_t)(q1 >> 32), c.y, k0 + r * kW0), (uint32_t)q1,
+                   xor3_key((uint32_t)(q0 >> 32), c.w, k1 + r * kW1), (uint32_t)q0);
   }
   return c;
 }
@@ -137,11 +160,11 @@ __device__ __forceinline__ uint32_t mskor_rtn(uint32_t addr, uint32_t mask, uint
 template <int NW, int B>
 __device__ __forceinline__ void bern_tally(const uint4 *__restrict__ plane, uint32_t lb, uint32_t m, uint32_t q,
                                            uint32_t W32, uint32_t rows, uint32_t amask1, uint32_t amask2,
-                                           uint32_t amask3, bool active, bool one_plane, uint32_t k0, uint32_t k1,
-                                           const DlvUni &u, uint32_t node, uint32_t &c0, uint32_t &c1) {
+                                           uint32_t amask3, bool active, bool one_plane, const DlvUni &u,
+                                           uint32_t node, uint32_t &c0, uint32_t &c1) {
   constexpr int L = NW == 3 ? 12 : 4, NB = L / 4, MW = L / NW;   // stream words, blocks, mask words per super-block
   constexpr int PER = 32 / B, NF = 4 * PER;
-  const uint32_t c2n = node & 0xFFFu;
+  const DlvRecv rv = dlv_receiver(u, node);
   const uint32_t tail = m & 31u ? (1u << (m & 31u)) - 1u : ~0u;   // the last mask word's live bits
   // ---- Bernoulli(a/16) mask: bit = (u < a), bits tz(a).. 3 of u from the
   // mask word's NW stream words, lowest first (oracle: r = ~u_tz; then
@@ -152,7 +175,7 @@ __device__ __forceinline__ void bern_tally(const uint4 *__restrict__ plane, uint
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
       if (j == 0 || w0 + (uint32_t)((4 * j) / NW) < W32) {    // blocks a partial super-block needs
-        const uint4 bb = dlv_block(k0, k1, u, c2n | ((blk + (uint32_t)j) << 12));
+        const uint4 bb = dlv_block(u, rv, blk + (uint32_t)j);
         s[4 * j] = bb.x, s[4 * j + 1] = bb.y, s[4 * j + 2] = bb.z, s[4 * j + 3] = bb.w;
       }
     }
@@ -189,7 +212,7 @@ __device__ __forceinline__ void bern_tally(const uint4 *__restrict__ plane, uint
   }
   const uint32_t addm = rm ? 0u : ~0u;           // data = bit when adding
   for (; __any(rem != 0u); ++blk) {
-    const uint4 bb = dlv_block(k0, k1, u, c2n | (blk << 12));
+    const uint4 bb = dlv_block(u, rv, blk);
     if (rem != 0u) {
       uint32_t addr[NF], bit[NF], old[NF];
 #pragma unroll
@@ -302,17 +325,16 @@ __global__ void __launch_bounds__(256) benor_random_bern_kernel(KParams p) {
     uint32_t R = 0;
     bool all_dec = false;
     for (uint32_t r = 1; r <= p.k_max; ++r) {
-      const uint32_t c3r = (r & 0xFFFFFu) | (kStreamDelivery << 24);
       // ---- R-phase ("proposal phase", node.ts:46-82) over each receiver's first N-F arrivals
       {
-        const DlvUni u = dlv_uniforms(k0, k1, tlo, thi, c3r);
+        const DlvUni u = dlv_uniforms(k0, k1, tlo, thi, r, 0u);
         const bool one = r > 1u || r1_plain;
         for (uint32_t j = 0; j < W; ++j) {
           const uint32_t c = j * 64u + lane;
           const bool active = c < m;
           const uint32_t node = active ? p.live_ids[c] : 0u;
           uint32_t a0, a1;
-          bern_tally<NW, B>(X, lb, m, q, W32, rows, am1, am2, am3, active, one, k0, k1, u, node, a0, a1);
+          bern_tally<NW, B>(X, lb, m, q, W32, rows, am1, am2, am3, active, one, u, node, a0, a1);
           const uint64_t vm = group_mask(j, m);
           const uint64_t p0 = ballot(a0 > a1) & vm;
           const uint64_t p1 = ballot(a1 > a0) & vm;
@@ -321,13 +343,13 @@ __global__ void __launch_bounds__(256) benor_random_bern_kernel(KParams p) {
       }
       // ---- P-phase ("voting phase", node.ts:83-158)
       {
-        const DlvUni u = dlv_uniforms(k0, k1, tlo, thi, c3r | (1u << 20));
+        const DlvUni u = dlv_uniforms(k0, k1, tlo, thi, r, 1u);
         for (uint32_t j = 0; j < W; ++j) {
           const uint32_t c = j * 64u + lane;
           const bool active = c < m;
           const uint32_t node = active ? p.live_ids[c] : 0u;
           uint32_t a0, a1;
-          bern_tally<NW, B>(P, lb, m, q, W32, rows, am1, am2, am3, active, false, k0, k1, u, node, a0, a1);
+          bern_tally<NW, B>(P, lb, m, q, W32, rows, am1, am2, am3, active, false, u, node, a0, a1);
           const uint64_t vm = group_mask(j, m);
           const bool d0l = a0 > F, d1l = a1 > F;
           const uint64_t d0 = ballot(d0l) & vm;

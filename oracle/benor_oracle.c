@@ -293,9 +293,12 @@ typedef struct {
  * independent per (receiver, round, phase).  At f == F it is every live
  * sender, i.e. lockstep.
  *
- * Random words: Philox stream 2, ctr {trial_lo, trial_hi, (node & 0xFFF) |
- * (block << 12), (round & 0xFFFFF) | (phase << 20) | (2 << 24)}, consumed in
- * order (word i = block i>>2, lane i&3).  `node` is the receiver's node id.
+ * Random words: Philox stream 2, ctr {trial_lo, trial_hi, block |
+ * (round & 0x7FFF) << 16 | phase << 31, node | (2 << 24)}, consumed in order
+ * (word i = block i>>2, lane i&3).  `node` is the receiver's node id.  Only
+ * the last counter word differs between the receivers of a trial, so the
+ * GPU computes the first rounds' products that depend only on the other
+ * three once per (trial, round, phase, block) (r04, benor_random.hip).
  * Two exact samplers, picked by the plan constants (m, q); k = min(e, q),
  * e = m - q:
  *
@@ -321,11 +324,12 @@ typedef struct {
     uint32_t key[2], ctr[4];
     uint32_t buf[4];
     uint32_t widx;
+    uint32_t blk_shift;       /* the block index goes to ctr[2] << blk_shift */
 } orc_dstream;
 
 static inline uint32_t dstream_next(orc_dstream *s) {
     if ((s->widx & 3u) == 0) {
-        uint32_t c[4] = {s->ctr[0], s->ctr[1], s->ctr[2] | ((s->widx >> 2) << 12), s->ctr[3]};
+        uint32_t c[4] = {s->ctr[0], s->ctr[1], s->ctr[2] | ((s->widx >> 2) << s->blk_shift), s->ctr[3]};
         oracle_philox4x32_10(s->key, c, s->buf);
     }
     return s->buf[s->widx++ & 3u];
@@ -366,9 +370,10 @@ void oracle_delivery_mask(uint64_t seed, uint64_t trial, uint32_t node, uint32_t
     orc_dstream s;
     s.key[0] = (uint32_t)seed; s.key[1] = (uint32_t)(seed >> 32);
     s.ctr[0] = (uint32_t)trial; s.ctr[1] = (uint32_t)(trial >> 32);
-    s.ctr[2] = node & 0xFFFu;
-    s.ctr[3] = (round & 0xFFFFFu) | ((phase & 1u) << 20) | (ORC_STREAM_DELIVERY << 24);
+    s.ctr[2] = ((round & 0x7FFFu) << 16) | ((phase & 1u) << 31);
+    s.ctr[3] = (node & 0xFFFu) | (ORC_STREAM_DELIVERY << 24);
     s.widx = 0;
+    s.blk_shift = 0;
     uint32_t a, b;
     if (oracle_delivery_bernoulli(m, q, &a, &b)) {          /* sampler (b) */
         uint32_t M32[128];
@@ -667,7 +672,7 @@ static uint32_t event_trial(const orc_event_cfg *cfg, uint64_t trial, orc_node_s
         orc_dstream s;
         s.key[0] = (uint32_t)cfg->seed; s.key[1] = (uint32_t)(cfg->seed >> 32);
         s.ctr[0] = (uint32_t)trial; s.ctr[1] = (uint32_t)(trial >> 32);
-        s.ctr[2] = 0; s.ctr[3] = ORC_STREAM_CRASH << 24; s.widx = 0;
+        s.ctr[2] = 0; s.ctr[3] = ORC_STREAM_CRASH << 24; s.widx = 0; s.blk_shift = 12;
         const uint32_t k = cfg->crash_count < m ? cfg->crash_count : m;
         orc_set T;
         memset(&T, 0, sizeof T);
