@@ -146,6 +146,22 @@ __device__ __forceinline__ uint32_t cmp_step_first(uint32_t u1, uint32_t u0, uin
   return o;
 }
 
+// This lane's bitset row of field bits [off, off + w): lb + (field << 8), one
+// v_bfe_u32 and one v_lshl_add_u32 (the compiler's shift / and / add is three).
+__device__ __forceinline__ uint32_t row_addr(uint32_t wd, uint32_t off, uint32_t w, uint32_t lb) {
+  const uint32_t t = __builtin_amdgcn_ubfe(wd, off, w);
+  uint32_t a;
+  asm("v_lshl_add_u32 %0, %1, 8, %2" : "=v"(a) : "v"(t), "v"(lb));
+  return a;
+}
+
+// 1 << (s & 31) as the all-VGPR VOP2 v_lshlrev_b32 (the shift reads s's low 5 bits).
+__device__ __forceinline__ uint32_t bit_of(uint32_t s, uint32_t one) {
+  uint32_t r;
+  asm("v_lshlrev_b32 %0, %1, %2" : "=v"(r) : "v"(s), "v"(one));
+  return r;
+}
+
 __device__ __forceinline__ uint32_t mskor_rtn(uint32_t addr, uint32_t mask, uint32_t data) {
   uint32_t old;
   asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3" : "=v"(old) : "v"(addr), "v"(mask), "v"(data) : "memory");
@@ -210,20 +226,23 @@ __device__ __forceinline__ void bern_tally(const uint4 *__restrict__ plane, uint
     }
     for (uint32_t w = W32; w < rows; ++w) *(lds_word *)(uintptr_t)(lb + w * 256u) = fill;
   }
-  const uint32_t addm = rm ? 0u : ~0u;           // data = bit when adding
+  uint32_t addm = rm ? 0u : ~0u;                 // data = bit when adding
+  uint32_t one = 1u;                              // a VGPR 1: 1 << s as an all-VGPR v_lshlrev_b32
+  asm volatile("" : "+v"(one), "+v"(addm));       // VGPRs: v_and_b32 (VOP2) for data, not v_cndmask
   for (; __any(rem != 0u); ++blk) {
     const uint4 bb = dlv_block(u, rv, blk);
     if (rem != 0u) {
-      uint32_t addr[NF], bit[NF], old[NF];
+      uint32_t addr[NF], bit[NF], data[NF], old[NF];
 #pragma unroll
       for (int f = 0; f < NF; ++f) {
         // field f: bits [off, off + B) of stream word f / PER; sender idx = row
         // idx >> 5 (the field's top B - 5 bits), bit idx & 31 (its low 5 bits)
         const uint32_t wd = word_of(bb, f / PER);
         const uint32_t off = (uint32_t)(f % PER) * B;   // a constant once unrolled
-        addr[f] = lb + (__builtin_amdgcn_ubfe(wd, off + 5u, B - 5u) << 8);
-        bit[f] = 1u << ((off ? (wd >> off) : wd) & 31u);
-        old[f] = mskor_rtn(addr[f], bit[f], bit[f] & addm);
+        addr[f] = row_addr(wd, off + 5u, B - 5u, lb);
+        bit[f] = off ? bit_of(__builtin_amdgcn_ubfe(wd, off, 5u), one) : bit_of(wd, one);
+        data[f] = bit[f] & addm;
+        old[f] = mskor_rtn(addr[f], bit[f], data[f]);
       }
       // one wait for the NF returns (their consumers read the values after it)
       asm volatile("s_waitcnt lgkmcnt(0)"
@@ -236,7 +255,7 @@ __device__ __forceinline__ void bern_tally(const uint4 *__restrict__ plane, uint
       uint32_t cnt = 0, acc[NF];
 #pragma unroll
       for (int f = 0; f < NF; ++f) {
-        acc[f] = (old[f] ^ (bit[f] & addm)) & bit[f];   // the flip happened
+        acc[f] = (old[f] ^ data[f]) & bit[f];            // the flip happened
         cnt = tally(acc[f], cnt);
       }
       if (cnt > rem) {                           // past the quota in this block: undo the last accepted
