@@ -64,6 +64,7 @@ EXPORTED_SYMBOLS = (
     "bo_plan_live_nodes", "bo_plan_destroy", "bo_run_trials", "bo_run_trial_states",
     "bo_popc_peak", "bo_last_error", "bo_abi_version", "bo_kernel_version", "bo_plan_kernel", "bo_kernel_for",
     "bo_mfma_peak", "bo_consensus_start_sched", "bo_plan_check",
+    "bo_consensus_start_live", "bo_consensus_wait", "bo_live_stop_events",
 )
 
 
@@ -111,6 +112,9 @@ def lib() -> ctypes.CDLL:
     L.bo_consensus_start.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32]
     L.bo_consensus_start_sched.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, P(ctypes.c_uint32),
                                            ctypes.c_uint32]
+    L.bo_consensus_start_live.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32]
+    L.bo_consensus_wait.argtypes = [ctypes.c_void_p]
+    L.bo_live_stop_events.argtypes = [ctypes.c_void_p, P(ctypes.c_uint32), ctypes.c_uint32]
     L.bo_consensus_stop.argtypes = [ctypes.c_void_p]
     L.bo_node_stop.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
     L.bo_get_state.argtypes = [ctypes.c_void_p, ctypes.c_uint32, P(NodeStateC)]
@@ -236,6 +240,26 @@ class Network:
         arr = _crash_array(self.N, sched)
         _check(lib().bo_consensus_start_sched(self._h, seed, k_max, arr, self.N))
 
+    def start_live(self, seed: int | None = None, k_max: int = DEFAULT_K_MAX) -> None:
+        """GET /start as the reference serves it (node.ts:167-188): launch the
+        event-level kernel and return; stop() / stop_node() then land in the
+        running kernel (bo_consensus_start_live) and wait() ends the run."""
+        if seed is None:
+            seed = secrets.randbits(64)
+        _check(lib().bo_consensus_start_live(self._h, seed, k_max))
+
+    def wait(self) -> None:
+        """End of a live run: its final states replace the pre-run ones (no-op otherwise)."""
+        _check(lib().bo_consensus_wait(self._h))
+
+    def live_stop_events(self) -> list:
+        """After wait(): per node, the delivery count at which the live run applied its
+        /stop (None = none) -- as stop_after on a fresh network with the same seed it
+        reproduces the run."""
+        out = (ctypes.c_uint32 * max(1, self.N))()
+        _check(lib().bo_live_stop_events(self._h, out, self.N))
+        return [None if v == NEVER else int(v) for v in out[:self.N]]
+
     def stop(self) -> None:
         _check(lib().bo_consensus_stop(self._h))
 
@@ -274,17 +298,25 @@ def _net(N: int) -> Network:
 
 
 def startConsensus(N: int, seed: int | None = None, k_max: int = DEFAULT_K_MAX, stop_after=None,
-                   strict: bool = False) -> None:
+                   strict: bool = False, live: bool = False) -> None:
     """src/nodes/consensus.ts:3-8: GET /start on every node, then the round
     loop (node.ts:43-163) on the GPU until every live node decided or k_max.
-    stop_after: mid-run GET /stop schedule (Network.start).  A second start on
-    a network resolves as the reference's does (every GET /start answers 200)
-    but runs nothing: its inboxes persist (node.ts:29-30), so no fresh
-    consensus can follow; strict=True raises Error instead."""
+    stop_after: mid-run GET /stop schedule (Network.start).  live=True returns
+    once the kernel is launched (Network.start_live): stopConsensus / a node's
+    stop land in the running kernel, and getNodesState / getNodeState wait for
+    the run.  A second start on a network resolves as the reference's does
+    (every GET /start answers 200) but runs nothing: its inboxes persist
+    (node.ts:29-30), so no fresh consensus can follow; strict=True raises
+    Error instead."""
     if N == 0:
         return
+    if live and stop_after:
+        raise ValueError("stop_after and live are exclusive: a live run takes /stop as it comes")
     try:
-        _net(N).start(seed, k_max, stop_after)
+        if live:
+            _net(N).start_live(seed, k_max)
+        else:
+            _net(N).start(seed, k_max, stop_after)
     except AlreadyStartedError:
         if strict:
             raise
@@ -301,12 +333,14 @@ def getNodeState(nodeId: int) -> dict:
     """__test__/tests/utils.ts:4-12 (GET /getState)."""
     if _current is None:
         raise RuntimeError("no launched network")
+    _current.wait()                      # a live run's final states
     return _current.get_state(nodeId)
 
 
 def getNodesState(N: int) -> list[dict]:
-    """__test__/tests/utils.ts:14-20."""
+    """__test__/tests/utils.ts:14-20 (after a live run has ended)."""
     net = _net(N)
+    net.wait()
     return [net.get_state(i) for i in range(N)]
 
 

@@ -1,4 +1,5 @@
-// benor_event_big.hip -- event-level mode for 256 < N <= 4096 (r04).
+// benor_event_big.hip -- event-level mode for 256 < N <= 4096, and live runs at any N
+// (r04).
 //
 // The reference's GET /stop (node.ts:191-194) lands on a running consensus at
 // any network size; from then on the node drops every message (node.ts:45).
@@ -30,6 +31,11 @@
 //     event j).  A trigger ends the batch: the overlay is written back, the
 //     triggered broadcast is appended, and the next batch starts after it.
 //     Batches also end before a scheduled stop.
+//   * a live run (bo_consensus_start_live, any N) also polls a host-mapped
+//     mailbox between batches, about every 10 us of wall clock, for GET /stop
+//     requests served while it runs; a request is applied before the next
+//     delivery e, exactly like a scheduled stop at e, and e is written back so
+//     the host can replay the run as a schedule (bo_live_stop_events).
 #include "benor_device.h"
 
 namespace benor {
@@ -141,7 +147,8 @@ __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
       rng = (((uint64_t)o.x << 32) | o.y) ^ 0xD1B54A32D192ED03ull;
     }
     __threadfence_block();
-    uint32_t next = 0, cur = 1, R = 0, halted = 0;
+    uint32_t next = 0, cur = 1, R = 0, halted = 0, seen = 0;
+    long long polled = wall_clock64() - (long long)kLivePollTicks;   // the first batch polls
     bool overflow = false;
     uint64_t e = 0;
     auto advance = [&]() {                      // complete rounds: halting (node.ts:116-145 as DESIGN §2)
@@ -164,6 +171,33 @@ __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
         }
         crashed = true;
         ++next;
+      }
+      // ---- live GET /stop requests (bo_consensus_start_live): every ~10 us the
+      // wave reads the host-mapped mailbox; a new request lands before delivery e,
+      // and e goes back to the host so the run can be replayed as a schedule
+      if (p.live_box && (uint64_t)(wall_clock64() - polled) >= kLivePollTicks) {
+        polled = wall_clock64();
+        uint32_t seq = 0u;
+        if (lane == 0u) seq = __hip_atomic_load(p.live_box, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        seq = rl(seq, 0u);
+        if (seq != seen) {
+          seen = seq;
+          uint64_t fresh = 0ull;
+          if (lane < NWd) {
+            const uint32_t *rq = p.live_box + kLiveReq + 2u * lane;
+            const uint32_t lo = __hip_atomic_load(rq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            const uint32_t hi = __hip_atomic_load(rq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            fresh = ((uint64_t)hi << 32 | lo) & allw & ~S.killed[lane];
+            S.killed[lane] |= fresh;
+          }
+          for (uint64_t f = fresh; f; f &= f - 1ull) {
+            const uint32_t i = 64u * lane + (uint32_t)__builtin_ctzll(f);
+            S.ibox[2u * i] |= kKilled;
+            S.ibox[2u * i + 1u] |= kKilled;
+            __hip_atomic_store(p.live_box + kLiveEv + i, e < 0xFFFFFFFFull ? (uint32_t)e : 0xFFFFFFFEu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+          crashed = crashed || __any(fresh != 0ull);
+        }
       }
       if (crashed) {
         __syncthreads();

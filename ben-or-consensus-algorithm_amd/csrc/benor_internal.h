@@ -96,6 +96,12 @@ struct KParams {
   // as (event << 12 | node), ascending
   const uint64_t *ev_stops;
   uint32_t ev_nstops;
+  // live run (bo_consensus_start_live): the wave-per-trial event kernel at any
+  // N, polling a host-mapped mailbox for GET /stop requests served while it
+  // runs -- live_box[0] request sequence, [kLiveReq ..) requested-stop bits,
+  // [kLiveEv + i] the delivery count at which node i's stop landed (device)
+  uint32_t live;
+  uint32_t *live_box;
   // W kernel trial-list mode: run the trials trial_begin + trial_list[i],
   // i < min(*trial_list_len, trial_count), instead of a contiguous range
   const uint32_t *trial_list, *trial_list_len;
@@ -106,7 +112,11 @@ struct KParams {
 };
 
 
-constexpr uint32_t kMfmaContRounds = 3;        // matrix-core passes up to round 3, then the popcount kernel
+constexpr uint32_t kLiveReq = 2;                 // live mailbox: request bitset words (BO_MAX_N / 32)
+constexpr uint32_t kLiveEv = kLiveReq + 128;     // live mailbox: per-node stop delivery counts
+constexpr uint64_t kLivePollTicks = 1000;        // wall-clock ticks (100 MHz) between mailbox polls
+
+constexpr uint32_t kMfmaContRounds = 3;       // matrix-core passes up to round 3, then the popcount kernel
 // The deferral buffer's 64-word length block: pass r's list length at 16 (r - 1).
 static_assert(16u * kMfmaContRounds <= 64u, "deferral length words overflow their block");
 

@@ -734,7 +734,7 @@ void plan_geometry(KParams &p) {
   const uint32_t W = p.W;
   p.hist_len = (p.k_max + 1u) * 3u + 1u;
   p.hist_bytes = (((p.hist_len * 4u) + 15u) & ~15u) + kParamBytes;   // histogram + parameter block
-  if (p.mode == BO_MODE_EVENT && p.N > kMaxEventN) {   // one wave per trial (benor_event_big.hip)
+  if (p.mode == BO_MODE_EVENT && (p.N > kMaxEventN || p.live)) {   // one wave per trial (benor_event_big.hip)
     p.G = 1;
     p.nblocks = 1;
     p.variant = 5;

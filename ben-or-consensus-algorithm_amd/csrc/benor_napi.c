@@ -11,6 +11,11 @@
  *       libuv worker thread (napi_async_work), so the event loop stays free;
  *       stopAfter (array of N delivery counts, null/undefined = never): GET /stop
  *       requests landing mid-run, node.ts:191-194 (bo_consensus_start_sched)
+ *   networkStartLive(handle, seed:BigInt, kMax)     consensus.ts:3-8 as the reference
+ *       runs it: launches the event-level kernel and returns; GET /stop served
+ *       while it runs lands in it (bo_consensus_start_live)
+ *   networkWait(handle) -> Promise<void>            end of a live run (bo_consensus_wait)
+ *   liveStopEvents(handle) -> Array<number|null>    where a live run applied each /stop
  *   networkStop(handle) / nodeStop(handle, i)       consensus.ts:10-15, node.ts:191-194
  *   getState(handle, i) -> {killed, x, decided, k}  node.ts:197-199
  *   status(handle, i) -> 500 | 200                  node.ts:33-39
@@ -218,6 +223,103 @@ static napi_value network_start(napi_env env, napi_callback_info info) {
     NAPI_CALL(env, napi_create_async_work(env, NULL, name, start_execute, start_complete, j, &j->work));
     NAPI_CALL(env, napi_queue_async_work(env, j->work));
     return promise;
+}
+
+static int get_seed(napi_env env, napi_value v, uint64_t *seed) {
+    bool lossless = true;
+    if (napi_get_value_bigint_uint64(env, v, seed, &lossless) == napi_ok) return 1;
+    double d = 0;
+    if (napi_get_value_double(env, v, &d) != napi_ok || d < 0) return 0;
+    *seed = (uint64_t)d;
+    return 1;
+}
+
+static napi_value network_start_live(napi_env env, napi_callback_info info) {
+    size_t argc = 3;
+    napi_value argv[3];
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    if (argc < 3) { napi_throw_type_error(env, NULL, "networkStartLive(handle, seed, kMax)"); return NULL; }
+    bo_network *net = get_net(env, argv[0]);
+    if (!net) return NULL;
+    uint64_t seed = 0;
+    int ok = get_seed(env, argv[1], &seed);
+    uint32_t k_max = get_u32(env, argv[2], &ok);
+    if (!ok) { napi_throw_type_error(env, NULL, "seed must be a BigInt or number, kMax a uint32"); return NULL; }
+    int rc = bo_consensus_start_live(net, seed, k_max);
+    if (rc) { throw_bo(env, rc); return NULL; }
+    return NULL;
+}
+
+/* ---- async wait for a live run ---- */
+typedef struct {
+    napi_async_work work;
+    napi_deferred deferred;
+    napi_ref net_ref;
+    bo_network *net;
+    int rc;
+    char err[512];
+} wait_job;
+
+static void wait_execute(napi_env env, void *data) {
+    (void)env;
+    wait_job *j = (wait_job *)data;
+    j->rc = bo_consensus_wait(j->net);
+    if (j->rc) snprintf(j->err, sizeof j->err, "libbenor error %d: %s", j->rc, bo_last_error());
+}
+
+static void wait_complete(napi_env env, napi_status status, void *data) {
+    wait_job *j = (wait_job *)data;
+    if (status == napi_ok && j->rc == 0) {
+        napi_value u;
+        napi_get_undefined(env, &u);
+        napi_resolve_deferred(env, j->deferred, u);
+    } else {
+        napi_value msg, err;
+        napi_create_string_utf8(env, j->rc ? j->err : "async work failed", NAPI_AUTO_LENGTH, &msg);
+        napi_create_error(env, NULL, msg, &err);
+        napi_reject_deferred(env, j->deferred, err);
+    }
+    napi_delete_reference(env, j->net_ref);
+    napi_delete_async_work(env, j->work);
+    free(j);
+}
+
+static napi_value network_wait(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1];
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    bo_network *net = get_net(env, argv[0]);
+    if (!net) return NULL;
+    wait_job *j = (wait_job *)calloc(1, sizeof *j);
+    j->net = net;
+    napi_create_reference(env, argv[0], 1, &j->net_ref);
+    napi_value promise, name;
+    NAPI_CALL(env, napi_create_promise(env, &j->deferred, &promise));
+    NAPI_CALL(env, napi_create_string_utf8(env, "benor.wait", NAPI_AUTO_LENGTH, &name));
+    NAPI_CALL(env, napi_create_async_work(env, NULL, name, wait_execute, wait_complete, j, &j->work));
+    NAPI_CALL(env, napi_queue_async_work(env, j->work));
+    return promise;
+}
+
+static napi_value live_stop_events(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1];
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    bo_network *net = get_net(env, argv[0]);
+    if (!net) return NULL;
+    const uint32_t N = bo_network_size(net);
+    uint32_t *ev = (uint32_t *)malloc(sizeof(uint32_t) * (N ? N : 1));
+    int rc = bo_live_stop_events(net, ev, N);
+    if (rc) { free(ev); throw_bo(env, rc); return NULL; }
+    napi_value arr, v;
+    napi_create_array_with_length(env, N, &arr);
+    for (uint32_t i = 0; i < N; ++i) {
+        if (ev[i] == 0xFFFFFFFFu) napi_get_null(env, &v);
+        else napi_create_uint32(env, ev[i], &v);
+        napi_set_element(env, arr, i, v);
+    }
+    free(ev);
+    return arr;
 }
 
 static napi_value network_stop(napi_env env, napi_callback_info info) {
@@ -449,6 +551,9 @@ static napi_value init_module(napi_env env, napi_value exports) {
     napi_property_descriptor d[] = {
         {"networkCreate", NULL, network_create, NULL, NULL, NULL, napi_default, NULL},
         {"networkStart", NULL, network_start, NULL, NULL, NULL, napi_default, NULL},
+        {"networkStartLive", NULL, network_start_live, NULL, NULL, NULL, napi_default, NULL},
+        {"networkWait", NULL, network_wait, NULL, NULL, NULL, napi_default, NULL},
+        {"liveStopEvents", NULL, live_stop_events, NULL, NULL, NULL, napi_default, NULL},
         {"networkStop", NULL, network_stop, NULL, NULL, NULL, napi_default, NULL},
         {"nodeStop", NULL, node_stop, NULL, NULL, NULL, napi_default, NULL},
         {"getState", NULL, get_state, NULL, NULL, NULL, napi_default, NULL},

@@ -66,13 +66,17 @@ __global__ void add_bin_kernel(unsigned long long *hist, uint32_t bin, unsigned 
 // run on a worker thread (the N-API addon's napi_async_work) while the caller's
 // thread serves /stop, /getState and /status.  The kernel runs without the
 // lock; its results are merged under it.
+struct bo_live;
 struct bo_network {
   uint32_t N = 0, F = 0;
   std::vector<bo_node_state> st;
   std::vector<uint8_t> faulty;
   bool started = false;     // GET /start was served (node.ts:167-188); inboxes persist after it
   bool in_flight = false;   // a start's kernel is running
+  bo_live *live = nullptr;  // a live run (bo_consensus_start_live) not yet waited for
+  std::vector<uint32_t> stop_events;   // its /stop delivery counts, after bo_consensus_wait
   mutable std::mutex mu;
+  std::mutex wait_mu;       // serialises bo_consensus_wait
 };
 
 struct bo_plan {
@@ -90,6 +94,29 @@ struct bo_plan {
   uint64_t *d_stops = nullptr;     // event level, N > 256: sorted /stop schedule
   int device = 0;
 };
+
+// A live run (bo_consensus_start_live): the event-level kernel runs on its own
+// stream while the caller serves /stop, /getState and /status; GET /stop
+// requests reach the running kernel through a host-mapped mailbox.
+struct bo_live {
+  bo_plan *pl = nullptr;
+  hipStream_t s = nullptr;
+  uint32_t *box = nullptr;             // host-mapped mailbox (benor::kLiveReq / kLiveEv layout)
+  bo_node_state *d_st = nullptr;
+  uint64_t *d_h = nullptr;
+  uint32_t *d_r = nullptr;
+  std::vector<uint32_t> active;
+};
+
+namespace {
+// Post GET /stop requests to a live run (caller holds net->mu): the nodes'
+// request bits first, then the sequence word the kernel polls.
+void live_post(bo_live *lr, const uint32_t *ids, uint32_t n) {
+  for (uint32_t j = 0; j < n; ++j)
+    __atomic_fetch_or(&lr->box[benor::kLiveReq + (ids[j] >> 5)], 1u << (ids[j] & 31u), __ATOMIC_RELAXED);
+  __atomic_fetch_add(&lr->box[0], 1u, __ATOMIC_RELEASE);
+}
+}  // namespace
 
 extern "C" {
 
@@ -135,7 +162,11 @@ int bo_network_create(uint32_t N, uint32_t F, const int8_t *init, uint32_t n_ini
 
 uint32_t bo_network_size(const bo_network *net) { return net ? net->N : 0u; }
 
-void bo_network_destroy(bo_network *net) { delete net; }
+void bo_network_destroy(bo_network *net) {
+  if (!net) return;
+  (void)bo_consensus_wait(net);   // a live run still holds device buffers
+  delete net;
+}
 
 int bo_status(const bo_network *net, uint32_t i) {   // node.ts:33-39
   if (!net) return -fail(BO_ERR_INVALID_ARGUMENT, "net is NULL");
@@ -157,6 +188,7 @@ int bo_node_stop(bo_network *net, uint32_t i) {   // node.ts:191-194
   if (i >= net->N) return fail(BO_ERR_OUT_OF_RANGE, "node index out of range");
   std::lock_guard<std::mutex> g(net->mu);
   net->st[i].killed = 1;
+  if (net->live) live_post(net->live, &i, 1u);
   return BO_OK;
 }
 
@@ -164,6 +196,11 @@ int bo_consensus_stop(bo_network *net) {   // consensus.ts:10-15
   if (!net) return fail(BO_ERR_INVALID_ARGUMENT, "net is NULL");
   std::lock_guard<std::mutex> g(net->mu);
   for (auto &s : net->st) s.killed = 1;
+  if (net->live) {
+    std::vector<uint32_t> all(net->N);
+    for (uint32_t i = 0; i < net->N; ++i) all[i] = i;
+    live_post(net->live, all.data(), net->N);
+  }
   return BO_OK;
 }
 
@@ -171,83 +208,85 @@ int bo_consensus_start(bo_network *net, uint64_t seed, uint32_t k_max) {   // co
   return bo_consensus_start_sched(net, seed, k_max, nullptr, 0u);
 }
 
-// startConsensus with GET /stop requests landing during the run (node.ts:191-194
-// served while the round loop is in flight).  Without a schedule: the lockstep
-// round loop (every running node hears every running node, SURVEY §8a).  With
-// one: the event-level kernel, delivery by delivery in the seeded order, each
-// scheduled /stop applied after its node's delivery count (oracle (iii)).
-int bo_consensus_start_sched(bo_network *net, uint64_t seed, uint32_t k_max, const uint32_t *stop_after,
-                             uint32_t n_stop_after) {
+namespace {
+// What a GET /start (node.ts:167-188) runs: the nodes not killed, their x, and
+// their /stop schedule entries.  `launch` is false when nothing needs a kernel.
+struct StartPlan {
+  std::vector<uint8_t> crashed;
+  std::vector<int8_t> x;
+  std::vector<uint32_t> active, sched;
+  bool scheduled = false;   // a /stop lands on a node that runs (entries of killed nodes are moot)
+  bool launch = false;
+};
+
+int start_prologue(bo_network *net, uint32_t k_max, const uint32_t *stop_after, uint32_t n_stop_after,
+                   StartPlan &sp) {
   if (!net) return fail(BO_ERR_INVALID_ARGUMENT, "net is NULL");
   if (k_max < 1 || k_max > BO_MAX_K) return fail(BO_ERR_INVALID_ARGUMENT, "k_max out of range");
   const uint32_t N = net->N;
   if (stop_after && n_stop_after != N) return fail(BO_ERR_INVALID_ARGUMENT, "stop schedule must have N entries");
-  bool scheduled = false;   // a /stop lands on a node that runs (entries of killed nodes are moot)
-  std::vector<uint8_t> crashed(N);
-  std::vector<int8_t> x(N);
-  std::vector<uint32_t> active, sched(N, 0xFFFFFFFFu);
-  {
-    std::lock_guard<std::mutex> g(net->mu);
-    // The reference's per-node inboxes (node.ts:29-30) live as long as the
-    // server: a second GET /start pushes round-1 messages onto inboxes that
-    // already hold them, and every push past N-F re-triggers the tally
-    // (node.ts:47-52).  That is not a fresh consensus, so it is refused.
-    if (net->started)
-      return fail(BO_ERR_ALREADY_STARTED, net->in_flight
-                  ? "consensus is already running on this network"
-                  : "consensus already started on this network: node inboxes persist across /start "
-                    "(node.ts:29-30), launch a new network to run again");
-    // Nodes that run: not killed (faulty from launch, or stopped).  They send
-    // and receive; killed nodes do neither (node.ts:45, :171).
-    for (uint32_t i = 0; i < N; ++i) {
-      crashed[i] = net->st[i].killed ? 1 : 0;
-      x[i] = net->st[i].killed ? 0 : net->st[i].x;
-      if (!net->st[i].killed) {
-        active.push_back(i);
-        if (stop_after) sched[i] = stop_after[i];
-      }
+  sp.crashed.assign(N, 0);
+  sp.x.assign(N, 0);
+  sp.sched.assign(N, 0xFFFFFFFFu);
+  std::lock_guard<std::mutex> g(net->mu);
+  // The reference's per-node inboxes (node.ts:29-30) live as long as the
+  // server: a second GET /start pushes round-1 messages onto inboxes that
+  // already hold them, and every push past N-F re-triggers the tally
+  // (node.ts:47-52).  That is not a fresh consensus, so it is refused.
+  if (net->started)
+    return fail(BO_ERR_ALREADY_STARTED, net->in_flight
+                ? "consensus is already running on this network"
+                : "consensus already started on this network: node inboxes persist across /start "
+                  "(node.ts:29-30), launch a new network to run again");
+  // Nodes that run: not killed (faulty from launch, or stopped).  They send
+  // and receive; killed nodes do neither (node.ts:45, :171).
+  for (uint32_t i = 0; i < N; ++i) {
+    sp.crashed[i] = net->st[i].killed ? 1 : 0;
+    sp.x[i] = net->st[i].killed ? 0 : net->st[i].x;
+    if (!net->st[i].killed) {
+      sp.active.push_back(i);
+      if (stop_after) sp.sched[i] = stop_after[i];
     }
-    for (uint32_t i : active) scheduled = scheduled || sched[i] != 0xFFFFFFFFu;
-    if (active.empty()) { net->started = true; return BO_OK; }
-    const int64_t quorum = (int64_t)N - (int64_t)net->F;
-    // Fewer running senders than the quorum: no R-phase ever triggers
-    // (node.ts:52), every running node stays at k = 1, undecided.
-    if ((int64_t)active.size() < quorum) {
-      for (uint32_t i : active) net->st[i].k = 1;   // node.ts:172
-      net->started = true;
-      return BO_OK;
-    }
-    int dev = 0;
-    const int rc = check_device(&dev);
-    if (rc) return rc;
-    net->started = true;
-    net->in_flight = true;
   }
+  for (uint32_t i : sp.active) sp.scheduled = sp.scheduled || sp.sched[i] != 0xFFFFFFFFu;
+  if (sp.active.empty()) { net->started = true; return BO_OK; }
+  const int64_t quorum = (int64_t)N - (int64_t)net->F;
+  // Fewer running senders than the quorum: no R-phase ever triggers
+  // (node.ts:52), every running node stays at k = 1, undecided.
+  if ((int64_t)sp.active.size() < quorum) {
+    for (uint32_t i : sp.active) net->st[i].k = 1;   // node.ts:172
+    net->started = true;
+    return BO_OK;
+  }
+  int dev = 0;
+  const int rc = check_device(&dev);
+  if (rc) return rc;
+  net->started = true;
+  net->in_flight = true;
+  sp.launch = true;
+  return BO_OK;
+}
 
+bo_trials_cfg start_cfg(const bo_network *net, uint64_t seed, uint32_t k_max, StartPlan &sp, int mode) {
   bo_trials_cfg cfg{};
-  cfg.N = N;
+  cfg.N = net->N;
   cfg.F = net->F;
   cfg.k_max = k_max;
   cfg.init_mode = BO_INIT_FIXED;
-  cfg.mode = scheduled ? BO_MODE_EVENT : BO_MODE_LOCKSTEP;
+  cfg.mode = mode;
   cfg.seed = seed;
-  cfg.faulty = crashed.data();
-  cfg.init = x.data();
-  cfg.crash_at = scheduled ? sched.data() : nullptr;
-  // Launch-time validation is already done; here the crashed set is the
-  // killed set, which has exactly N - quorum = F members at this point.
-  std::vector<bo_node_state> states(N);
-  uint32_t rounds = 0;
-  const int rc = bo_run_trial_states(&cfg, 0, states.data(), &rounds);
-  std::lock_guard<std::mutex> g(net->mu);
-  net->in_flight = false;
-  if (rc) {
-    net->started = false;          // nothing ran: the start may be retried
-    return rc;
-  }
-  // A scheduled /stop is part of the run (the kernel's killed flag); one
-  // served while the kernel ran is ordered after it: the node keeps its final
-  // x / decided / k and stays killed.
+  cfg.faulty = sp.crashed.data();
+  cfg.init = sp.x.data();
+  cfg.crash_at = sp.scheduled ? sp.sched.data() : nullptr;
+  return cfg;
+}
+
+// The run's final states into the network (caller holds net->mu).  A /stop
+// the run applied is part of it (the kernel's killed flag); one served while
+// the kernel ran but not applied by it is ordered after it: the node keeps its
+// final x / decided / k and stays killed.
+void merge_states(bo_network *net, const std::vector<uint32_t> &active, const std::vector<bo_node_state> &states) {
+  const uint32_t N = net->N;
   for (uint32_t i : active) {
     const int8_t killed = net->st[i].killed;
     net->st[i] = states[i];
@@ -262,6 +301,32 @@ int bo_consensus_start_sched(bo_network *net, uint64_t seed, uint32_t k_max, con
   for (uint32_t i = 0; i < N; ++i) all_decided = all_decided && net->st[i].decided == 1;
   if (all_decided)
     for (uint32_t i = 0; i < N; ++i) net->st[i].killed = 1;
+}
+}  // namespace
+
+// startConsensus with GET /stop requests landing during the run (node.ts:191-194
+// served while the round loop is in flight).  Without a schedule: the lockstep
+// round loop (every running node hears every running node, SURVEY §8a).  With
+// one: the event-level kernel, delivery by delivery in the seeded order, each
+// scheduled /stop applied after its node's delivery count (oracle (iii)).
+int bo_consensus_start_sched(bo_network *net, uint64_t seed, uint32_t k_max, const uint32_t *stop_after,
+                             uint32_t n_stop_after) {
+  StartPlan sp;
+  int rc = start_prologue(net, k_max, stop_after, n_stop_after, sp);
+  if (rc || !sp.launch) return rc;
+  // Launch-time validation is already done; here the crashed set is the
+  // killed set, which has exactly N - quorum = F members at this point.
+  const bo_trials_cfg cfg = start_cfg(net, seed, k_max, sp, sp.scheduled ? BO_MODE_EVENT : BO_MODE_LOCKSTEP);
+  std::vector<bo_node_state> states(net->N);
+  uint32_t rounds = 0;
+  rc = bo_run_trial_states(&cfg, 0, states.data(), &rounds);
+  std::lock_guard<std::mutex> g(net->mu);
+  net->in_flight = false;
+  if (rc) {
+    net->started = false;          // nothing ran: the start may be retried
+    return rc;
+  }
+  merge_states(net, sp.active, states);
   return BO_OK;
 }
 
@@ -269,7 +334,7 @@ int bo_consensus_start_sched(bo_network *net, uint64_t seed, uint32_t k_max, con
 // Validation and kernel planning of a trial configuration, host only: the
 // live-node map, the fixed-init plane and the KParams shape (no device fields).
 static int plan_host(const bo_trials_cfg *cfg, std::vector<uint32_t> &live, std::vector<uint4> &plane,
-                     benor::KParams &kp) {
+                     benor::KParams &kp, bool live_run = false) {
   if (!cfg) return fail(BO_ERR_INVALID_ARGUMENT, "NULL argument");
   if (cfg->N < 1 || cfg->N > BO_MAX_N) return fail(BO_ERR_UNSUPPORTED, "N must be in [1, 4096]");
   if (cfg->k_max < 1 || cfg->k_max > BO_MAX_K) return fail(BO_ERR_INVALID_ARGUMENT, "k_max must be in [1, 1024]");
@@ -306,6 +371,7 @@ static int plan_host(const bo_trials_cfg *cfg, std::vector<uint32_t> &live, std:
   kp.q = cfg->N - cfg->F;
   kp.crash_count = cfg->crash_count;
   kp.crash_window = cfg->crash_window;
+  kp.live = live_run && cfg->mode == BO_MODE_EVENT ? 1u : 0u;
   for (uint32_t i = 0; i < cfg->N && i < 4u * 64u; ++i)
     if (cfg->faulty[i]) kp.faulty_mask[i >> 6] |= 1ull << (i & 63u);
   if (m == 0) {
@@ -341,13 +407,13 @@ int bo_kernel_for(const bo_trials_cfg *cfg, int *kernel_out) {
   return BO_OK;
 }
 
-int bo_plan_create(const bo_trials_cfg *cfg, bo_plan **out) {
+static int plan_create_impl(const bo_trials_cfg *cfg, bo_plan **out, bool live_run) {
   if (!cfg || !out) return fail(BO_ERR_INVALID_ARGUMENT, "NULL argument");
   *out = nullptr;
   std::vector<uint32_t> live;
   std::vector<uint4> plane;
   benor::KParams kp0;
-  int rc = plan_host(cfg, live, plane, kp0);
+  int rc = plan_host(cfg, live, plane, kp0, live_run);
   if (rc) return rc;
   int dev = 0;
   rc = check_device(&dev);
@@ -391,6 +457,7 @@ int bo_plan_create(const bo_trials_cfg *cfg, bo_plan **out) {
       (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
       const uint64_t slot = (uint64_t)kp.ev_stride * 4u;
       uint64_t slots = std::max<uint64_t>(1u, std::min<uint64_t>((uint64_t)cus, (4ull << 30) / slot));
+      if (live_run) slots = 1u;                      // a live run is one trial
       kp.ev_lanes = slots;
       e = hipMalloc(&pl->d_init_x, cfg->N);
       if (e == hipSuccess) e = hipMemcpy(pl->d_init_x, ix.data(), cfg->N, hipMemcpyHostToDevice);
@@ -442,6 +509,8 @@ int bo_plan_create(const bo_trials_cfg *cfg, bo_plan **out) {
   *out = pl;
   return BO_OK;
 }
+
+int bo_plan_create(const bo_trials_cfg *cfg, bo_plan **out) { return plan_create_impl(cfg, out, false); }
 
 void bo_plan_destroy(bo_plan *pl) {
   if (!pl) return;
@@ -715,17 +784,11 @@ int run_states_lockstep(const bo_trials_cfg *cfg, uint64_t trial, bo_node_state 
 }
 }  // namespace
 
-int bo_run_trial_states(const bo_trials_cfg *cfg, uint64_t trial, bo_node_state *nodes_out, uint32_t *rounds_out) {
-  if (!cfg || !nodes_out) return fail(BO_ERR_INVALID_ARGUMENT, "NULL argument");
-  if (cfg->mode == BO_MODE_LOCKSTEP) return run_states_lockstep(cfg, trial, nodes_out, rounds_out);
-  bo_plan *pl = nullptr;
-  int rc = bo_plan_create(cfg, &pl);
-  if (rc) return rc;
-  const uint32_t N = cfg->N, H = bo_hist_len(cfg->k_max);
-  // Host-side initial states (node.ts:21-26); live entries are overwritten
-  // by the kernel.
-  std::vector<bo_node_state> st(N);
-  for (uint32_t i = 0; i < N; ++i) {
+namespace {
+// Host-side initial states (node.ts:21-26); live entries are overwritten by the kernel.
+void initial_states(const bo_trials_cfg *cfg, std::vector<bo_node_state> &st) {
+  st.resize(cfg->N);
+  for (uint32_t i = 0; i < cfg->N; ++i) {
     const bool f = cfg->faulty[i] != 0;
     st[i].killed = f ? 1 : 0;
     st[i].x = f ? -1 : (cfg->init_mode == BO_INIT_FIXED ? cfg->init[i] : -1);
@@ -733,6 +796,18 @@ int bo_run_trial_states(const bo_trials_cfg *cfg, uint64_t trial, bo_node_state 
     st[i].pad = 0;
     st[i].k = f ? -1 : 0;
   }
+}
+}  // namespace
+
+int bo_run_trial_states(const bo_trials_cfg *cfg, uint64_t trial, bo_node_state *nodes_out, uint32_t *rounds_out) {
+  if (!cfg || !nodes_out) return fail(BO_ERR_INVALID_ARGUMENT, "NULL argument");
+  if (cfg->mode == BO_MODE_LOCKSTEP) return run_states_lockstep(cfg, trial, nodes_out, rounds_out);
+  bo_plan *pl = nullptr;
+  int rc = bo_plan_create(cfg, &pl);
+  if (rc) return rc;
+  const uint32_t N = cfg->N, H = bo_hist_len(cfg->k_max);
+  std::vector<bo_node_state> st;
+  initial_states(cfg, st);
   bo_node_state *d_st = nullptr;
   uint64_t *d_h = nullptr;
   uint32_t *d_r = nullptr;
@@ -754,6 +829,115 @@ int bo_run_trial_states(const bo_trials_cfg *cfg, uint64_t trial, bo_node_state 
   if (rc) return rc;
   if (rounds & 0x80000000u) return fail(BO_ERR_INTERNAL, "event-level message pool filled up: the run stopped early");
   if (rounds_out) *rounds_out = rounds;
+  return BO_OK;
+}
+
+// ------------------------------------------------------------ live runs
+namespace {
+void live_free(bo_live *lr) {
+  if (!lr) return;
+  if (lr->s) (void)hipStreamSynchronize(lr->s);
+  if (lr->d_st) (void)hipFree(lr->d_st);
+  if (lr->d_h) (void)hipFree(lr->d_h);
+  if (lr->d_r) (void)hipFree(lr->d_r);
+  if (lr->box) (void)hipHostFree(lr->box);
+  if (lr->s) (void)hipStreamDestroy(lr->s);
+  if (lr->pl) bo_plan_destroy(lr->pl);
+  delete lr;
+}
+
+// Plan, mailbox, state buffers and the launch on the run's own stream.
+int live_launch(bo_live *lr, const bo_trials_cfg *cfg) {
+  int rc = plan_create_impl(cfg, &lr->pl, true);
+  if (rc) return rc;
+  const uint32_t N = cfg->N, H = bo_hist_len(cfg->k_max);
+  HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&lr->box), sizeof(uint32_t) * (benor::kLiveEv + N),
+                        hipHostMallocMapped | hipHostMallocCoherent));
+  std::memset(lr->box, 0, sizeof(uint32_t) * benor::kLiveEv);
+  for (uint32_t i = 0; i < N; ++i) lr->box[benor::kLiveEv + i] = 0xFFFFFFFFu;
+  uint32_t *dbox = nullptr;
+  HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&dbox), lr->box, 0));
+  lr->pl->kp.live_box = dbox;
+  std::vector<bo_node_state> st;
+  initial_states(cfg, st);
+  HIP_TRY(hipMalloc(&lr->d_st, sizeof(bo_node_state) * N));
+  HIP_TRY(hipMalloc(&lr->d_h, sizeof(uint64_t) * H));
+  HIP_TRY(hipMalloc(&lr->d_r, sizeof(uint32_t)));
+  HIP_TRY(hipMemcpy(lr->d_st, st.data(), sizeof(bo_node_state) * N, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemset(lr->d_h, 0, sizeof(uint64_t) * H));
+  HIP_TRY(hipMemset(lr->d_r, 0, sizeof(uint32_t)));
+  HIP_TRY(hipStreamCreateWithFlags(&lr->s, hipStreamNonBlocking));
+  return plan_launch_impl(lr->pl, 0, 1, lr->d_h, lr->d_st, lr->d_r, lr->s);
+}
+}  // namespace
+
+// startConsensus whose GET /stop requests land while it runs (node.ts:191-194
+// served during the round loop): the event-level kernel is launched and the
+// call returns, as the reference's GET /start answers before consensus
+// finishes (node.ts:167-188).  bo_node_stop / bo_consensus_stop post to the
+// running kernel; bo_consensus_wait ends the run.
+int bo_consensus_start_live(bo_network *net, uint64_t seed, uint32_t k_max) {
+  StartPlan sp;
+  int rc = start_prologue(net, k_max, nullptr, 0u, sp);
+  if (rc || !sp.launch) return rc;
+  const bo_trials_cfg cfg = start_cfg(net, seed, k_max, sp, BO_MODE_EVENT);
+  auto *lr = new bo_live();
+  lr->active = sp.active;
+  rc = live_launch(lr, &cfg);
+  std::lock_guard<std::mutex> g(net->mu);
+  if (rc) {
+    live_free(lr);
+    net->in_flight = false;
+    net->started = false;          // nothing ran: the start may be retried
+    return rc;
+  }
+  net->live = lr;
+  net->stop_events.clear();
+  // stops served between the prologue and now reach the kernel too
+  std::vector<uint32_t> late;
+  for (uint32_t i : sp.active)
+    if (net->st[i].killed) late.push_back(i);
+  if (!late.empty()) live_post(lr, late.data(), (uint32_t)late.size());
+  return BO_OK;
+}
+
+int bo_consensus_wait(bo_network *net) {
+  if (!net) return fail(BO_ERR_INVALID_ARGUMENT, "net is NULL");
+  std::lock_guard<std::mutex> w(net->wait_mu);
+  bo_live *lr = nullptr;
+  {
+    std::lock_guard<std::mutex> g(net->mu);
+    lr = net->live;
+  }
+  if (!lr) return BO_OK;
+  const uint32_t N = net->N;
+  std::vector<bo_node_state> states(N);
+  uint32_t rounds = 0;
+  hipError_t e = hipStreamSynchronize(lr->s);
+  if (e == hipSuccess) e = hipMemcpy(states.data(), lr->d_st, sizeof(bo_node_state) * N, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(&rounds, lr->d_r, sizeof(uint32_t), hipMemcpyDeviceToHost);
+  int rc = e != hipSuccess ? hip_fail(e, "bo_consensus_wait") : bo_plan_check(lr->pl);
+  if (!rc && (rounds & 0x80000000u))
+    rc = fail(BO_ERR_INTERNAL, "event-level message pool filled up: the run stopped early");
+  {
+    std::lock_guard<std::mutex> g(net->mu);
+    net->live = nullptr;           // from here a /stop is ordered after the run
+    net->in_flight = false;
+    if (!rc) {
+      net->stop_events.assign(lr->box + benor::kLiveEv, lr->box + benor::kLiveEv + N);
+      merge_states(net, lr->active, states);
+    }
+  }
+  live_free(lr);
+  return rc;
+}
+
+int bo_live_stop_events(const bo_network *net, uint32_t *events_out, uint32_t n) {
+  if (!net || !events_out) return fail(BO_ERR_INVALID_ARGUMENT, "NULL argument");
+  if (n != net->N) return fail(BO_ERR_INVALID_ARGUMENT, "events_out must have N entries");
+  std::lock_guard<std::mutex> g(net->mu);
+  if (net->live) return fail(BO_ERR_INVALID_ARGUMENT, "a live run is in flight: bo_consensus_wait first");
+  for (uint32_t i = 0; i < n; ++i) events_out[i] = i < net->stop_events.size() ? net->stop_events[i] : 0xFFFFFFFFu;
   return BO_OK;
 }
 

@@ -49,8 +49,14 @@ async function launchNetwork(N, F, initialValues, faultyList, options = {}) {
   // counts per node (array of N, null = never; bo_consensus_start_sched).  The
   // run is one kernel, so a /stop request arriving over HTTP while it is in
   // flight is ordered after it; a scheduled one lands mid-round.
+  // options.live: the run starts when every running node has served /start
+  // and /start answers at once (node.ts:167-188 answers before consensus
+  // finishes); a GET /stop served over HTTP while it runs lands in the kernel
+  // (bo_consensus_start_live), and /getState shows the final states once the
+  // run has ended.
   let sched;
   if (options.stopAfter !== undefined && options.stopAfter !== null) {
+    if (options.live) throw new RangeError('stopAfter and live are exclusive: a live run takes /stop as it comes');
     sched = stopSchedule(N, options.stopAfter);
   }
   const handle = addon.networkCreate(N, F, initialValues, faultyList);   // launchNodes.ts:10-13 errors
@@ -65,17 +71,28 @@ async function launchNetwork(N, F, initialValues, faultyList, options = {}) {
   };
 
   function maybeRun() {
-    if (net.running || net.ran) return net.running;
+    if (net.running || net.ran) return options.live ? null : net.running;
     const live = runningNodes();
     if (live.length === 0 || !live.every((i) => net.started[i])) return null;
     let seed = net.seed;
     if (seed === undefined) {
       seed = (BigInt(Math.floor(Math.random() * 2 ** 32)) << 32n) | BigInt(Math.floor(Math.random() * 2 ** 32));
     }
-    net.running = addon.networkStart(handle, BigInt(seed), kMax, sched).then(() => {
+    const done = () => {
       net.ran = true;
       net.running = null;
-    });
+    };
+    if (options.live) {
+      try {
+        addon.networkStartLive(handle, BigInt(seed), kMax);
+      } catch (e) {
+        return Promise.reject(e);
+      }
+      net.running = addon.networkWait(handle).then(done);
+      net.running.catch(() => {});
+      return Promise.resolve();   // launched: /start answers now
+    }
+    net.running = addon.networkStart(handle, BigInt(seed), kMax, sched).then(done);
     return net.running;
   }
 
@@ -107,7 +124,8 @@ async function launchNetwork(N, F, initialValues, faultyList, options = {}) {
         const p = maybeRun();
         const reply = () => send(res, 200, { message: 'Algorithm started' }, true);
         // respond once the round loop has landed, so a caller that polls
-        // /getState right after startConsensus sees final states
+        // /getState right after startConsensus sees final states (live: once
+        // the kernel is launched)
         if (p) p.then(reply, (e) => send(res, 500, { message: String(e && e.message) }, true));
         else reply();
         return undefined;

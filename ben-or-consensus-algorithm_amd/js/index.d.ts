@@ -41,6 +41,10 @@ export interface StartOptions {
   stopAfter?: (number | null)[] | { [nodeId: number]: number };
   /** Reject a second start on one network (libbenor error 8) instead of resolving as a no-op. */
   strict?: boolean;
+  /** Resolve once the kernel is launched (GET /start answers before consensus finishes);
+   * stopNode / stopConsensus then land in the running kernel, getNodesState / getNodeState /
+   * waitConsensus wait for the run.  Exclusive with stopAfter. */
+  live?: boolean;
 }
 
 export declare function startConsensus(N: number, options?: StartOptions): Promise<void>;
@@ -51,6 +55,11 @@ export declare function getNodesState(N: number): Promise<NodeState[]>;
 export declare function getNodeStatus(nodeId: number): Promise<{ status: 200 | 500; body: "live" | "faulty" }>;
 export declare function reachedFinality(states: NodeState[]): boolean;
 export declare function delay(ms: number): Promise<void>;
+/** End of a live run (startConsensus(N, {live: true})); resolves at once otherwise. */
+export declare function waitConsensus(N: number): Promise<void>;
+/** After a live run: per node, the delivery count at which its /stop landed (null = none);
+ * as stopAfter on a fresh network with the same seed it reproduces the run. */
+export declare function liveStopEvents(N: number): Promise<(number | null)[]>;
 
 export interface TrialsConfig {
   N: number;

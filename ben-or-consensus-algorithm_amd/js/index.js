@@ -43,7 +43,7 @@ function stopSchedule(N, stopAfter) {
 
 async function launchNetwork(N, F, initialValues, faultyList) {
   const handle = addon.networkCreate(N, F, initialValues, faultyList);   // throws the reference's Errors
-  current = { handle, N };
+  current = { handle, N, running: null };
   const servers = [];
   for (let i = 0; i < N; i++) servers.push(new NodeServer(i));
   return servers;
@@ -69,6 +69,11 @@ function randomSeed() {
 // {nodeId: deliveries}; a node is stopped after that many POST /message have
 // been handled network-wide (seeded delivery order, the event-level kernel,
 // N <= 4096).
+// options.live: resolve as soon as the kernel is launched, as the reference's
+// GET /start answers before consensus finishes; stopConsensus / stopNode then
+// land in the running kernel (bo_consensus_start_live), and getNodesState /
+// getNodeState / waitConsensus wait for the run to end.  liveStopEvents(N)
+// gives the delivery count at which each /stop landed (replayable as stopAfter).
 // A second start on the same network resolves, as the reference's GET /start
 // answers 200, but runs nothing: its round inboxes outlive a run (node.ts:29-30),
 // so no fresh consensus can follow (options.strict: reject with libbenor error 8).
@@ -78,13 +83,41 @@ async function startConsensus(N, options = {}) {
   const kMax = options.kMax !== undefined ? options.kMax : DEFAULT_K_MAX;
   let sched;
   if (options.stopAfter !== undefined && options.stopAfter !== null) {
+    if (options.live) throw new RangeError('stopAfter and live are exclusive: a live run takes /stop as it comes');
     sched = stopSchedule(N, options.stopAfter);
   }
+  const cur = net(N);
   try {
-    await addon.networkStart(net(N).handle, seed, kMax, sched);
+    if (options.live) {
+      addon.networkStartLive(cur.handle, seed, kMax);
+      cur.running = addon.networkWait(cur.handle);
+      cur.running.catch(() => {});   // surfaced by the next settle()
+      return;
+    }
+    await addon.networkStart(cur.handle, seed, kMax, sched);
   } catch (e) {
     if (options.strict || !/libbenor error 8:/.test(e.message)) throw e;
   }
+}
+
+// The end of a live run (a no-op otherwise).
+async function settle(cur) {
+  if (cur.running) {
+    const p = cur.running;
+    cur.running = null;
+    await p;
+  }
+}
+
+async function waitConsensus(N) {
+  if (N === 0) return;
+  await settle(net(N));
+}
+
+async function liveStopEvents(N) {
+  const cur = net(N);
+  await settle(cur);
+  return addon.liveStopEvents(cur.handle);
 }
 
 async function stopConsensus(N) {
@@ -94,10 +127,16 @@ async function stopConsensus(N) {
 
 async function stopNode(nodeId) { addon.nodeStop(net().handle, nodeId); }
 
-async function getNodeState(nodeId) { return addon.getState(net().handle, nodeId); }
+async function getNodeState(nodeId) {
+  const cur = net();
+  await settle(cur);
+  return addon.getState(cur.handle, nodeId);
+}
 
 async function getNodesState(N) {
-  const h = net(N).handle;
+  const cur = net(N);
+  await settle(cur);
+  const h = cur.handle;
   const out = [];
   for (let i = 0; i < N; i++) out.push(addon.getState(h, i));
   return out;
@@ -122,4 +161,5 @@ const delay = (ms) => new Promise((res) => setTimeout(res, ms));   // src/utils.
 module.exports = {
   BASE_NODE_PORT, DEFAULT_K_MAX, launchNetwork, startConsensus, stopConsensus, stopNode,
   getNodeState, getNodesState, getNodeStatus, reachedFinality, runTrials, delay,
+  waitConsensus, liveStopEvents,
 };

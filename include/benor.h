@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define BENOR_ABI_VERSION 6
+#define BENOR_ABI_VERSION 7
 
 /* Return codes.  The first two are the reference's two launch errors. */
 enum {
@@ -118,10 +118,37 @@ int bo_consensus_start(bo_network *net, uint64_t seed, uint32_t k_max);
 int bo_consensus_start_sched(bo_network *net, uint64_t seed, uint32_t k_max,
                              const uint32_t *stop_after, uint32_t n_stop_after);
 
+/* startConsensus(N) as the reference runs it (consensus.ts:3-8, node.ts:167-188):
+ * GET /start answers before consensus finishes, and GET /stop requests served
+ * while it runs land in it (node.ts:191-194, :45).  Launches the event-level
+ * kernel (seeded delivery order, trial 0 of `seed`, any N <= BO_MAX_N) on its
+ * own HIP stream and returns.  While it runs, bo_node_stop / bo_consensus_stop
+ * also post to a host-mapped mailbox the kernel polls (every ~10 us): a
+ * request is applied before the next delivery, and that delivery count is
+ * recorded (bo_live_stop_events).  bo_get_state / bo_status answer from the
+ * pre-run states (killed flags include the posted stops) until
+ * bo_consensus_wait merges the run's final states (a request the kernel did
+ * not see before it finished is ordered after the run, as for
+ * bo_consensus_start).  The one-start and auto-stop rules of
+ * bo_consensus_start apply; bo_network_destroy waits for a live run. */
+int bo_consensus_start_live(bo_network *net, uint64_t seed, uint32_t k_max);
+
+/* Wait for a live run (bo_consensus_start_live) and merge its final states;
+ * BO_OK at once when none is in flight. */
+int bo_consensus_wait(bo_network *net);
+
+/* After bo_consensus_wait: for each node, the delivery count at which a live
+ * run applied its GET /stop, UINT32_MAX if it applied none (n == N).  Passed as
+ * bo_consensus_start_sched's stop_after on a fresh network of the same launch,
+ * with the same seed, it reproduces the live run exactly (counts below
+ * UINT32_MAX - 1). */
+int bo_live_stop_events(const bo_network *net, uint32_t *events_out, uint32_t n);
+
 /* stopConsensus(N)  (consensus.ts:10-15) -> GET /stop on every node (node.ts:191-194). */
 int bo_consensus_stop(bo_network *net);
 
-/* GET /stop on one node (node.ts:191-194): killed = true. */
+/* GET /stop on one node (node.ts:191-194): killed = true (and, during a live
+ * run, posted to the running kernel). */
 int bo_node_stop(bo_network *net, uint32_t node);
 
 /* GET /getState (node.ts:197-199). */
