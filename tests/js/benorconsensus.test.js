@@ -25,10 +25,13 @@ async function expectStatus(faultyArray) {   // :59-74
   }
 }
 
-async function runToFinality(faultyArray, initialValues) {   // :138-160
+// live: startConsensus resolves once the kernel is launched, as the reference's
+// does before consensus finishes (consensus.ts:3-8); the polling below is then
+// what the reference's suite relies on
+async function runToFinality(faultyArray, initialValues, live = false) {   // :138-160
   const servers = await b.launchNetwork(faultyArray.length, faultyArray.filter((e) => e === true).length,
     initialValues, faultyArray);
-  await b.startConsensus(faultyArray.length, { seed: 0x5EEDn });
+  await b.startConsensus(faultyArray.length, { seed: 0x5EEDn, live });
   const time = Date.now();
   let states = await b.getNodesState(faultyArray.length);
   while (Date.now() - time < 2000 && !b.reachedFinality(states)) {
@@ -70,9 +73,9 @@ const finality = [
     [0, 0, 1, 1, 1, 0, 0, 1, 1], 'agree'],                                                         // :227-286
   ['No Faulty Nodes', [false, false, false, false, false], [0, 1, 0, 1, 1], 'x1'],                // :351-393
 ];
-for (const [name, fa, init, kind] of finality) {
-  it(`Finality is reached - ${name}`, 'gpu', async () => {
-    const { servers, states } = await runToFinality(fa, init);
+for (const [name, fa, init, kind, live] of finality.flatMap((c) => [[...c, false], [...c, true]])) {
+  it(`Finality is reached - ${name}${live ? ' (live start)' : ''}`, 'gpu', async () => {
+    const { servers, states } = await runToFinality(fa, init, live);
     checkFaultyNull(fa, states);
     const vals = [];
     states.forEach((s, i) => {
@@ -86,15 +89,22 @@ for (const [name, fa, init, kind] of finality) {
   });
 }
 
-it('Finality is reached - Exceeding Fault Tolerance', 'gpu', async () => {   // :292-345
-  const fa = [true, true, true, true, true, false, false, false, false, false];
-  const { servers, states } = await runToFinality(fa, [0, 0, 1, 1, 1, 0, 0, 1, 1, 0]);
-  checkFaultyNull(fa, states);
-  states.forEach((s, i) => {
-    if (fa[i]) return;
-    assert.ok(!s.decided); assert.ok(s.k > 10); assert.notStrictEqual(s.x, null);
+for (const live of [false, true]) {
+  it(`Finality is reached - Exceeding Fault Tolerance${live ? ' (live start)' : ''}`, 'gpu', async () => {   // :292-345
+    const fa = [true, true, true, true, true, false, false, false, false, false];
+    const { servers, states } = await runToFinality(fa, [0, 0, 1, 1, 1, 0, 0, 1, 1, 0], live);
+    checkFaultyNull(fa, states);
+    states.forEach((s, i) => {
+      if (fa[i]) return;
+      assert.ok(!s.decided); assert.ok(s.k > 10); assert.notStrictEqual(s.x, null);
+    });
+    await b.stopConsensus(servers.length); await closeAllServers(servers);
   });
-  await b.stopConsensus(servers.length); await closeAllServers(servers);
+}
+
+it('live start and a stop schedule are exclusive', 'setup', async () => {
+  await b.launchNetwork(3, 0, [1, 1, 1], [false, false, false]);
+  await assert.rejects(b.startConsensus(3, { live: true, stopAfter: [null, 5, null] }), RangeError);
 });
 
 it('Finality is reached - Randomized', 'gpu', async () => {   // :399-450

@@ -45,9 +45,9 @@ const closeAll = (servers) => Promise.all(servers.map((s) => new Promise((r) => 
 const tests = [];
 const it = (name, group, fn) => tests.push({ name, group, fn });
 
-async function withNet(fa, init, fn) {
+async function withNet(fa, init, fn, live = false) {
   const servers = await facade.launchNetwork(fa.length, fa.filter((e) => e === true).length, init, fa,
-    { basePort: BASE, seed: 0x5EEDn });
+    { basePort: BASE, seed: 0x5EEDn, live });
   try { await fn(servers); } finally { await stopConsensus(fa.length); await closeAll(servers); }
 }
 
@@ -80,6 +80,11 @@ it('setup: getState JSON and /stop', 'setup', async () => {
   });
 });
 
+it('setup: live start and a stop schedule are exclusive', 'setup', async () => {
+  await assert.rejects(facade.launchNetwork(3, 0, [1, 1, 1], [false, false, false],
+    { basePort: BASE, live: true, stopAfter: [null, 5, null] }), RangeError);
+});
+
 const finality = [
   ['Unanimous Agreement', [false, false, false, false, false], [1, 1, 1, 1, 1], 'x1'],
   ['Simple Majority', [false, false, false, false, true], [1, 1, 1, 0, 0], 'x1'],
@@ -88,8 +93,11 @@ const finality = [
   ['No Faulty Nodes', [false, false, false, false, false], [0, 1, 0, 1, 1], 'x1'],
   ['One node', [false], [1], 'x1'],
 ];
-for (const [name, fa, init, kind] of finality) {
-  it(`Finality over HTTP - ${name}`, 'gpu', async () => {
+// live: /start answers once the kernel is launched (node.ts:167-188 answers
+// before consensus finishes) and the caller polls /getState, as the reference
+// suite does (benorconsensus.test.ts)
+for (const [name, fa, init, kind, live] of finality.flatMap((c) => [[...c, false], [...c, true]])) {
+  it(`Finality over HTTP - ${name}${live ? ' (live start)' : ''}`, 'gpu', async () => {
     await withNet(fa, init, async () => {
       await startConsensus(fa.length);
       const t = Date.now();
@@ -104,7 +112,7 @@ for (const [name, fa, init, kind] of finality) {
         vals.push(s.x);
       });
       if (kind === 'agree') assert.ok(vals.every((v) => v === vals[0]));
-    });
+    }, live);
   });
 }
 
