@@ -62,7 +62,7 @@ for step in "$@"; do
       timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
       chk $? smoke; tail -1 "$OUT/smoke.log";;
     tests)
-      timeout -k 10 900 python -u -m pytest ${PYTEST_ARGS:-tests} ${PYTEST_K:+-k "$PYTEST_K"} -m gpu -x -v --timeout 200 --timeout-method thread \
+      timeout -k 10 900 python -u -m pytest ${PYTEST_ARGS:-tests} ${PYTEST_K:+-k "$PYTEST_K"} -m gpu -x -v --durations=30 --timeout 200 --timeout-method thread \
         > "$OUT/tests.log" 2>&1
       rc=$?; tail -3 "$OUT/tests.log"; chk $rc tests;;
     probe)
