@@ -221,35 +221,69 @@ __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
         pv = __hip_atomic_load(&pool[pk], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         tv = __hip_atomic_load(&pool[len - 1u - lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+      // ---- the batch's messages: event i takes the message at its pick from
+      // the pool as the earlier events of the batch left it (overlay lookup)
       uint32_t ovp = 0xFFFFFFFFu, ovv = 0u;     // overlay: lane j = event j's write
-      uint32_t used = (uint32_t)B, trig = 0xFFFFFFFFu, tmsg = 0u;
-      uint64_t tbox = 0ull;
+      uint32_t mine = 0u;                       // lane i: the message event i delivers
       for (uint32_t i = 0; i < (uint32_t)B; ++i) {
         const uint32_t qpos = rl(pk, i), tpos = len - 1u - i;
         const uint64_t h1 = __ballot(ovp == qpos), h2 = __ballot(ovp == tpos);
         const uint32_t msg = h1 ? rl(ovv, last_lane(h1)) : rl(pv, i);
         const uint32_t moved = h2 ? rl(ovv, last_lane(h2)) : rl(tv, i);
-        if (lane == i) { ovp = qpos; ovv = moved; }
-        // ---- POST /message (node.ts:45-158)
-        const uint32_t to = msg & 4095u, ph = (msg >> 12) & 1u, xv = (msg >> 13) & 3u;
-        const uint32_t k = cur + (((msg >> 15) - cur) & 3u);
-        uint64_t *bp = &S.ibox[2u * to + ph];
-        uint64_t b = *bp;
-        if (b & kKilled) continue;             // node.ts:45
-        if (k >= p.k_max + 3u) continue;        // beyond the oracle's round window
-        b += 1ull << 26;                        // len
-        if (xv == 0u) b += 1ull;                // c0
-        else if (xv == 1u) b += 1ull << 13;     // c1
-        if (((b >> 26) & kC13) != quorum) {     // node.ts:52, :88
-          if (lane == 0u) *bp = b;
-          continue;
+        if (lane == i) { ovp = qpos; ovv = moved; mine = msg; }
+      }
+      // ---- POST /message (node.ts:45-158), all B deliveries at once: each
+      // adds {len, c0 | c1} to its receiver's inbox slot unless the receiver is
+      // killed (node.ts:45) or the round is beyond the oracle's window.  When
+      // no slot reaches the quorum (node.ts:52, :88) inside the batch, that is
+      // the sequential result (the adds commute); otherwise they are undone and
+      // the batch is replayed one delivery at a time up to its first trigger.
+      uint32_t used = (uint32_t)B, trig = 0xFFFFFFFFu, tmsg = 0u;
+      uint64_t tbox = 0ull;
+      {
+        uint64_t inc = 0ull;
+        uint64_t *bp = nullptr;
+        if (lane < B) {
+          const uint32_t to = mine & 4095u, ph = (mine >> 12) & 1u, xv = (mine >> 13) & 3u;
+          const uint32_t k = cur + (((mine >> 15) - cur) & 3u);
+          bp = &S.ibox[2u * to + ph];
+          if (!(*bp & kKilled) && k < p.k_max + 3u)
+            inc = (1ull << 26) + (xv == 0u ? 1ull : (xv == 1u ? 1ull << 13 : 0ull));
         }
-        if (lane == 0u) *bp = 0ull;             // every message of the phase arrived: the slot is free
-        trig = i;
-        tmsg = msg;
-        tbox = b;
-        used = i + 1u;
-        break;
+        bool crossed = false;
+        if (inc) {
+          const uint64_t old = __hip_atomic_fetch_add(reinterpret_cast<unsigned long long *>(bp), inc,
+                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          crossed = ((old >> 26) & kC13) + 1u == quorum;
+        }
+        if (__any(crossed)) {
+          if (inc)
+            __hip_atomic_fetch_add(reinterpret_cast<unsigned long long *>(bp), 0ull - inc, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+          __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the undo lands before the replay reads
+          for (uint32_t i = 0; i < (uint32_t)B; ++i) {
+            const uint32_t msg = rl(mine, i);
+            const uint32_t to = msg & 4095u, ph = (msg >> 12) & 1u, xv = (msg >> 13) & 3u;
+            const uint32_t k = cur + (((msg >> 15) - cur) & 3u);
+            uint64_t *sp = &S.ibox[2u * to + ph];
+            uint64_t b = *sp;
+            if (b & kKilled) continue;             // node.ts:45
+            if (k >= p.k_max + 3u) continue;        // beyond the oracle's round window
+            b += 1ull << 26;                        // len
+            if (xv == 0u) b += 1ull;                // c0
+            else if (xv == 1u) b += 1ull << 13;     // c1
+            if (((b >> 26) & kC13) != quorum) {     // node.ts:52, :88
+              if (lane == 0u) *sp = b;
+              continue;
+            }
+            if (lane == 0u) *sp = 0ull;             // every message of the phase arrived: the slot is free
+            trig = i;
+            tmsg = msg;
+            tbox = b;
+            used = i + 1u;
+            break;
+          }
+        }
       }
       // ---- the batch's pool writes (the last write to each position wins)
       {
