@@ -103,6 +103,33 @@ __device__ __forceinline__ uint32_t pack_fp4_8(const mf_v16f &acc, int base) {
   return r;
 }
 
+// h ? a : b for a lane-half flag, as one v_bfi_b32 on the 0 / ~0 VGPR mask hm:
+// a lane-varying ?: compiles to v_cndmask_b32 with an SGPR-pair mask, ~24 cycles
+// per wave instruction on gfx950 against ~4 for v_bfi_b32
+// (profiles/r03-v7_valu_probe.txt).
+__device__ __forceinline__ uint32_t half_sel(uint32_t hm, uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(hm), "v"(a), "v"(b));
+  return r;
+}
+
+// x1 words of chunks 4j .. 4j+3 of this lane half h from its /start Philox
+// block r (block 2j + h): half h keeps words h and 2 + h and trades the other
+// two with lane l ^ 32 (ds_bpermute).
+__device__ __forceinline__ void half_trade(const uint4 &r, uint32_t h, uint32_t (&xw)[4]) {
+  uint32_t hm = 0u - h;
+  asm volatile("" : "+v"(hm));                   // a VGPR mask, not a select condition
+  const uint32_t keep_a = half_sel(hm, r.y, r.x), keep_b = half_sel(hm, r.w, r.z);
+  const uint32_t give_a = half_sel(hm, r.x, r.y), give_b = half_sel(hm, r.z, r.w);
+  const int xa = (int)(((threadIdx.x & 63u) ^ 32u) << 2);   // lane l ^ 32 (no __shfl_xor bounds select)
+  const uint32_t recv_a = (uint32_t)__builtin_amdgcn_ds_bpermute(xa, (int)give_a);
+  const uint32_t recv_b = (uint32_t)__builtin_amdgcn_ds_bpermute(xa, (int)give_b);
+  xw[0] = half_sel(hm, recv_a, keep_a);
+  xw[1] = half_sel(hm, recv_b, keep_b);
+  xw[2] = half_sel(hm, keep_a, recv_a);
+  xw[3] = half_sel(hm, keep_b, recv_b);
+}
+
 // 32 sender bits -> the 4 VGPRs of one lane's B fragment (nibble i of VGPR v
 // = bit 4i + v of the word, as e2m1 1.0).
 __device__ __forceinline__ mf_v4i expand_votes(uint32_t w) {
@@ -224,14 +251,11 @@ __global__ void __launch_bounds__(256) benor_mfma_kernel(KParams p) {
         // words 4b + h, 4b + 2 + h and trades the other two with lane l ^ 32.
         const uint4 r = philox4x32_10(kk.x, kk.y,
                                       make_uint4((uint32_t)trial, (uint32_t)(trial >> 32), 2u * j + h, kStreamInit << 24));
-        const uint32_t keep_a = h ? r.y : r.x, keep_b = h ? r.w : r.z;
-        const uint32_t give_a = h ? r.x : r.y, give_b = h ? r.z : r.w;
-        const uint32_t recv_a = (uint32_t)__shfl_xor((int)give_a, 32);
-        const uint32_t recv_b = (uint32_t)__shfl_xor((int)give_b, 32);
-        if (4 * j + 0 < W) xw[4 * j + 0] = h ? recv_a : keep_a;
-        if (4 * j + 1 < W) xw[4 * j + 1] = h ? recv_b : keep_b;
-        if (4 * j + 2 < W) xw[4 * j + 2] = h ? keep_a : recv_a;
-        if (4 * j + 3 < W) xw[4 * j + 3] = h ? keep_b : recv_b;
+        uint32_t q4[4];
+        half_trade(r, h, q4);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (4 * j + q < W) xw[4 * j + q] = q4[q];
       }
     } else {
 #pragma unroll

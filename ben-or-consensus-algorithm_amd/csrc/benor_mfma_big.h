@@ -46,14 +46,7 @@ __device__ __forceinline__ void big_x_block(const uint32_t *keys, uint64_t trial
   const uint2 kk = lds_keys(keys);
   const uint4 r = philox4x32_10(kk.x, kk.y, make_uint4((uint32_t)trial, (uint32_t)(trial >> 32), 2u * j + h,
                                                        kStreamInit << 24));
-  const uint32_t keep_a = h ? r.y : r.x, keep_b = h ? r.w : r.z;
-  const uint32_t give_a = h ? r.x : r.y, give_b = h ? r.z : r.w;
-  const uint32_t recv_a = (uint32_t)__shfl_xor((int)give_a, 32);
-  const uint32_t recv_b = (uint32_t)__shfl_xor((int)give_b, 32);
-  xw[0] = h ? recv_a : keep_a;
-  xw[1] = h ? recv_b : keep_b;
-  xw[2] = h ? keep_a : recv_a;
-  xw[3] = h ? keep_b : recv_b;
+  half_trade(r, h, xw);
 }
 
 }  // namespace benor

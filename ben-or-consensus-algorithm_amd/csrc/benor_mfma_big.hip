@@ -111,14 +111,9 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_big_kernel(KParams p) {
         const uint2 kk = lds_keys(keys);
         const uint4 r = philox4x32_10(kk.x, kk.y,
                                       make_uint4((uint32_t)trial, (uint32_t)(trial >> 32), 2u * j + h, kStreamInit << 24));
-        const uint32_t keep_a = h ? r.y : r.x, keep_b = h ? r.w : r.z;
-        const uint32_t give_a = h ? r.x : r.y, give_b = h ? r.z : r.w;
-        const uint32_t recv_a = (uint32_t)__shfl_xor((int)give_a, 32);
-        const uint32_t recv_b = (uint32_t)__shfl_xor((int)give_b, 32);
-        X[(4u * j + 0u) * 64u + lane] = h ? recv_a : keep_a;
-        X[(4u * j + 1u) * 64u + lane] = h ? recv_b : keep_b;
-        X[(4u * j + 2u) * 64u + lane] = h ? keep_a : recv_a;
-        X[(4u * j + 3u) * 64u + lane] = h ? keep_b : recv_b;
+        uint32_t q4[4];
+        half_trade(r, h, q4);
+        for (uint32_t q = 0; q < 4u; ++q) X[(4u * j + q) * 64u + lane] = q4[q];
       }
     } else {
       for (uint32_t c = 0; c < W; ++c) {
