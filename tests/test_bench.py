@@ -94,6 +94,11 @@ def test_bench_single_gpu_line():
     assert c5b["kernels_per_launch"] and c5b["undecided_trials"] == 0 and 1.0 < c5b["mean_rounds"] < 1.05
     c1 = oc.pop("C1 N=5,F=1 network API")                 # configs[0]: one network, reference calls
     assert c1["reference_assertions_hold"] and 0 < c1["median_ms"] < 50
+    net = oc.pop("C4 N=1024,F=341 network API, mid-run /stop")   # one network through the drop-in API
+    assert net["stop inside round 1"]["stopped_nodes"] == 1 and net["stop inside round 1"]["seconds"] > 0
+    assert net["no stop (lockstep kernel)"]["stopped_nodes"] == 0
+    sweep = oc.pop("C5 sweep (2^30 trials, 224 cells)")          # configs[4] end to end, CSV checked
+    assert sweep["cells"] == 224 and sweep["trials"] > 2 ** 29 and sweep["csv_equals_results_r02_sweep_c5"] is True
     for k, v in oc.items():
         assert 0 < v["roofline"]["frac"] < 1.0 and v["roofline"]["bound"], k
     # N=256/F=85 and the headline run on the matrix cores (m odd, m > 2F): 2m terms per node-round
