@@ -144,6 +144,21 @@ __device__ __forceinline__ uint32_t coin_word(uint4 b, uint32_t round) {
   return j == 0u ? b.x : j == 1u ? b.y : j == 2u ? b.z : b.w;
 }
 
+// coin_word for a lane-varying round, as three v_bfi_b32 on VGPR masks: the ?:
+// chain compiles to v_cndmask_b32 with a VCC / SGPR-pair condition, ~24 cycles
+// per wave instruction on gfx950 against ~4 for v_bfi_b32
+// (profiles/r03-v7_valu_probe.txt).  The result is a VGPR.
+__device__ __forceinline__ uint32_t coin_word_v(uint4 b, uint32_t round) {
+  const uint32_t j = (round - 1u) & 3u;
+  uint32_t m0 = 0u - (j & 1u), m1 = 0u - (j >> 1);
+  asm volatile("" : "+v"(m0), "+v"(m1));
+  uint32_t lo, hi, r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(lo) : "v"(m0), "v"(b.y), "v"(b.x));
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(hi) : "v"(m0), "v"(b.w), "v"(b.z));
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m1), "v"(hi), "v"(lo));
+  return r;
+}
+
 // Coins of the tied receivers of one group (lanes = compact nodes 64 g + l).
 // The key words are laundered through an empty asm so that Philox's ten round
 // keys are not hoisted out of the round loop into permanently live SGPRs.

@@ -120,7 +120,7 @@ __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
       int8_t v;
       if (p.init_mode == BO_INIT_RANDOM) {      // word c >> 5 of stream 1 (oracle_random_init)
         const uint4 ir = philox4x32_10<false>(k0, k1, make_uint4(tlo, thi, c >> 7, kStreamInit << 24));
-        v = (int8_t)((coin_word(ir, ((c >> 5) & 3u) + 1u) >> (c & 31u)) & 1u);
+        v = (int8_t)((coin_word_v(ir, ((c >> 5) & 3u) + 1u) >> (c & 31u)) & 1u);
       } else {
         v = p.init_x[i];
       }

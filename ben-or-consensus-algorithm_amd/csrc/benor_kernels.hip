@@ -657,7 +657,7 @@ __global__ void __launch_bounds__(256) benor_event_kernel(KParams p) {
             c += (uint32_t)__builtin_popcountll(~p.faulty_mask[j] & below & all[j]);
           }
           const uint4 rr = philox4x32_10<false>(k0, k1, make_uint4(tlo, thi, c >> 5, ((k - 1u) >> 2) | (kStreamCoin << 24)));
-          nx = (int8_t)((coin_word(rr, k) >> (c & 31u)) & 1u);
+          nx = (int8_t)((coin_word_v(rr, k) >> (c & 31u)) & 1u);
         }
         L.xs[to] = nx;
         L.ks[to] = (int16_t)(k + 1u);

@@ -206,7 +206,7 @@ __global__ void __launch_bounds__(256) benor_lane_kernel(KParams p) {
         if (kWide) cw1 = coin_block(kk0, kk1, tlo, thi, 32u, r);
         cg = g1;
       }
-      const Plane cwr = (Plane)(coin_word(cw, r) | (kWide ? (uint64_t)coin_word(cw1, r) << 32 : 0ull));
+      const Plane cwr = (Plane)(coin_word_v(cw, r) | (kWide ? (uint64_t)coin_word_v(cw1, r) << 32 : 0ull));
       // P-phase (node.ts:88-113), per receiver: a = c0 - F - 1 (sign: not d0),
       // b = c1 - F - 1 (sign: not d1), a - b = c0 - c1 (sign: c1 > c0),
       // b - a (sign: c0 > c1)

@@ -124,7 +124,7 @@ __device__ uint32_t small_lane_trial(uint32_t k0, uint32_t k1, uint64_t tr, uint
       cw = coin_block<false>(k0, k1, tlo, thi, 0u, r);     // mul_lo/hi Philox on this divergent path
       cg = g1;
     }
-    const uint32_t cwr = coin_word(cw, r);
+    const uint32_t cwr = coin_word_v(cw, r);
     uint32_t nd0 = 0u, nd1 = 0u, gt1 = 0u, gt0 = 0u;
 #pragma unroll
     for (int c = MM - 1; c >= 0; --c) {                           // node.ts:88-113, per receiver
