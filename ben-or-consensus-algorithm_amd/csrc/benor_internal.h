@@ -109,7 +109,12 @@ struct KParams {
   // round r of the trials trial_begin + trial_list[i], i < *trial_list_len,
   // which tied in every round before r (x = their round r-1 coins); 0: round 1
   uint32_t cont_round;
+  // diagnostics (BENOR_TIMELINE=<file>, packed matrix-core kernel): per wave,
+  // kTimelineWords u64 -- wall-clock stamps of its phases and its batch counts
+  unsigned long long *timeline;
 };
+
+constexpr uint32_t kTimelineWords = 12;
 
 
 constexpr uint32_t kLiveReq = 2;                 // live mailbox: request bitset words (BO_MAX_N / 32)

@@ -241,18 +241,31 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
   const uint32_t ngroups = (trial_count + BATCH - 1u) / BATCH;
   uint32_t g = wave_id, len2 = 0u, len3 = 0u, lql = 0u;          // wave-uniform
   uint32_t h0[3] = {0u, 0u, 0u}, h1[3] = {0u, 0u, 0u};             // halts with 0 / 1 in rounds 1..3 (wave totals)
+  // diagnostics: [0] start, [1] fresh batches exhausted, [2] lists drained,
+  // [3] lane path done, [4] flushed; [5..10] batches: fresh, r2 full, r3 full,
+  // r2 partial, r3 partial, lane-path passes
+  unsigned long long *tl = p.timeline ? p.timeline + (size_t)wave_id * kTimelineWords : nullptr;
+  uint32_t nb[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+  bool fresh_done = false;
+  if (tl && lane == 0u) tl[0] = (unsigned long long)wall_clock64();
 
   for (;;) {
     // ---- the next batch: the deepest full list, else fresh round-1 trials
     // (batch g, g + waves_total, ...), else the partial lists
     uint32_t r, n;
     const uint32_t *src = nullptr;
-    if (R >= 3u && len3 >= BATCH) { r = 3u; n = BATCH; len3 -= n; src = list3 + len3; }
-    else if (R >= 2u && len2 >= BATCH) { r = 2u; n = BATCH; len2 -= n; src = list2 + len2; }
-    else if (g < ngroups) { r = 1u; n = trial_count - g * BATCH; n = n < BATCH ? n : BATCH; }
-    else if (len2) { r = 2u; n = len2; src = list2; len2 = 0u; }
-    else if (len3) { r = 3u; n = len3; src = list3; len3 = 0u; }
+    uint32_t kind;
+    if (R >= 3u && len3 >= BATCH) { r = 3u; n = BATCH; len3 -= n; src = list3 + len3; kind = 2u; }
+    else if (R >= 2u && len2 >= BATCH) { r = 2u; n = BATCH; len2 -= n; src = list2 + len2; kind = 1u; }
+    else if (g < ngroups) { r = 1u; n = trial_count - g * BATCH; n = n < BATCH ? n : BATCH; kind = 0u; }
+    else if (len2) { r = 2u; n = len2; src = list2; len2 = 0u; kind = 3u; }
+    else if (len3) { r = 3u; n = len3; src = list3; len3 = 0u; kind = 4u; }
     else break;
+    if (tl) {
+      if (kind >= 3u && !fresh_done && lane == 0u) tl[1] = (unsigned long long)wall_clock64();
+      fresh_done = fresh_done || kind >= 3u;
+      ++nb[kind];
+    }
     r = (uint32_t)__builtin_amdgcn_readfirstlane((int)r);
     n = (uint32_t)__builtin_amdgcn_readfirstlane((int)n);
 
@@ -380,10 +393,19 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
     while (lql >= 64u) {
       lql -= 64u;
       small_lane_path<MM>(keys, lq[lql + lane], fixed1, random_init, F, k_max, R, lhist, hist_len);
+      if (tl) ++nb[5];
     }
+  }
+  if (tl && lane == 0u) {
+    if (!fresh_done) tl[1] = (unsigned long long)wall_clock64();
+    tl[2] = (unsigned long long)wall_clock64();
   }
   // ---- the rest of the lane-path queue
   if (lane < lql) small_lane_path<MM>(keys, lq[lane], fixed1, random_init, F, k_max, R, lhist, hist_len);
+  if (tl && lane == 0u) {
+    if (lql) ++nb[5];
+    tl[3] = (unsigned long long)wall_clock64();
+  }
   // halts of the matrix-core rounds: lane 2q + v adds bin 3 (q + 1) + v
   {
     uint32_t c = 0u;
@@ -396,6 +418,10 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
   }
   __syncthreads();
   flush_hist(lhist, p);
+  if (tl && lane == 0u) {
+    tl[4] = (unsigned long long)wall_clock64();
+    for (int i = 0; i < 6; ++i) tl[5 + i] = nb[i];
+  }
 }
 
 template <int MM>

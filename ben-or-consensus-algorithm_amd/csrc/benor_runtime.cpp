@@ -545,6 +545,36 @@ uint64_t bo_plan_popc_words_per_node_round(const bo_plan *pl) {
   return counts * ((pl->kp.m + 31ull) / 32ull);
 }
 
+// Diagnostics (BENOR_TIMELINE=<file>): the packed matrix-core kernel stamps
+// each wave's phases; one CSV line per wave is appended to the file
+// (tools/timeline_report.py).  Synchronous; not for timing the launch itself.
+static hipError_t launch_with_timeline(benor::KParams kp, int grid, hipStream_t s, const char *path) {
+  const size_t words = (size_t)grid * benor::kWavesPerBlock * benor::kTimelineWords;
+  unsigned long long *d = nullptr;
+  hipError_t e = hipMalloc(&d, words * sizeof(unsigned long long));
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(d, 0, words * sizeof(unsigned long long), s);
+  kp.timeline = d;
+  if (e == hipSuccess) e = benor::launch_lockstep(kp, grid, s);
+  std::vector<unsigned long long> h(words);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e == hipSuccess) e = hipMemcpy(h.data(), d, words * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (e != hipSuccess) return e;
+  if (FILE *f = std::fopen(path, "a")) {
+    std::fprintf(f, "# launch m=%u trials=%llu grid=%d waves=%d\n", kp.m, (unsigned long long)kp.trial_count, grid,
+                 grid * benor::kWavesPerBlock);
+    for (size_t w = 0; w < (size_t)grid * benor::kWavesPerBlock; ++w) {
+      const unsigned long long *t = h.data() + w * benor::kTimelineWords;
+      std::fprintf(f, "%zu", w);
+      for (uint32_t i = 0; i < 11u; ++i) std::fprintf(f, ",%llu", t[i]);
+      std::fprintf(f, "\n");
+    }
+    std::fclose(f);
+  }
+  return hipSuccess;
+}
+
 static int plan_launch_impl(bo_plan *pl, uint64_t trial_begin, uint64_t trial_count, uint64_t *hist_dev,
                             bo_node_state *node_out, uint32_t *rounds_out, hipStream_t s) {
   if (trial_count == 0) return BO_OK;
@@ -657,7 +687,12 @@ static int plan_launch_impl(bo_plan *pl, uint64_t trial_begin, uint64_t trial_co
     kp.trial_begin = trial_begin + done;
     kp.trial_count = n;
     const int grid = benor::lockstep_grid(kp, pl->device);
-    HIP_TRY(benor::launch_lockstep(kp, grid, s));
+    const char *tl_path = kp.variant == 8 ? getenv("BENOR_TIMELINE") : nullptr;
+    if (tl_path) {
+      HIP_TRY(launch_with_timeline(kp, grid, s, tl_path));
+    } else {
+      HIP_TRY(benor::launch_lockstep(kp, grid, s));
+    }
     done += n;
   }
   return BO_OK;
