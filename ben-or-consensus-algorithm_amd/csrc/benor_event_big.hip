@@ -56,7 +56,23 @@ __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t lane) {   // v of `l
   return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
 }
 
-__device__ __forceinline__ uint32_t last_lane(uint64_t mask) { return 63u - (uint32_t)__builtin_clzll(mask); }
+__device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }   // v_min_u32
+__device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }   // v_max_u32
+
+// All-ones when x == 0 (else 0), and all-ones when (int)(a - b) < 0 (|a - b| <
+// 2^31) -- VALU arithmetic in asm, so the compiler cannot turn them back into
+// compares feeding v_cndmask_b32 (a VCC / SGPR-pair select, ~24 cycles per wave
+// instruction on gfx950 against 2-4 here).
+__device__ __forceinline__ uint32_t zero_mask(uint32_t x) {
+  uint32_t r;
+  asm("v_min_u32 %0, 1, %1\n\tv_add_u32 %0, -1, %0" : "=&v"(r) : "v"(x));
+  return r;
+}
+__device__ __forceinline__ uint32_t below_mask(uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_sub_u32 %0, %1, %2\n\tv_ashrrev_i32 %0, 31, %0" : "=&v"(r) : "v"(a), "v"(b));
+  return r;
+}
 
 struct BigState {
   uint64_t *ibox;     // [N][2] {c0, c1, len} per phase, bit 63 killed
@@ -221,17 +237,33 @@ __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
         pv = __hip_atomic_load(&pool[pk], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         tv = __hip_atomic_load(&pool[len - 1u - lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      // ---- the batch's messages: event i takes the message at its pick from
-      // the pool as the earlier events of the batch left it (overlay lookup)
-      uint32_t ovp = 0xFFFFFFFFu, ovv = 0u;     // overlay: lane j = event j's write
-      uint32_t mine = 0u;                       // lane i: the message event i delivers
-      for (uint32_t i = 0; i < (uint32_t)B; ++i) {
-        const uint32_t qpos = rl(pk, i), tpos = len - 1u - i;
-        const uint64_t h1 = __ballot(ovp == qpos), h2 = __ballot(ovp == tpos);
-        const uint32_t msg = h1 ? rl(ovv, last_lane(h1)) : rl(pv, i);
-        const uint32_t moved = h2 ? rl(ovv, last_lane(h2)) : rl(tv, i);
-        if (lane == i) { ovp = qpos; ovv = moved; mine = msg; }
+      // ---- the batch's messages.  Event i takes the message at q_i = pk and
+      // moves the one at t_i = len - 1 - i there (swap-remove).  As the batch's
+      // earlier events left the pool, position p holds the value moved by the
+      // last event j < i with q_j = p, else the pool's own word.  So per lane:
+      //   a = last j < i with q_j = q_i, b = last j < i with q_j = t_i (one scan
+      //   over the batch's picks, no cross-iteration dependency);
+      //   moved_i = moved_b (b exists) else pool[t_i] -- a chain i -> b -> ...
+      //   resolved to its root by pointer jumping (6 bpermute steps for 64);
+      //   msg_i = moved_a (a exists) else pool[q_i];
+      // and event i's write is the position's last one iff no later event
+      // of the batch picks q_i (nx = the first such j).
+      const uint32_t qi = pk, ti = len - 1u - lane;
+      uint32_t a1 = 0u, b1 = 0u, nx = 64u;      // a + 1, b + 1 (0: none)
+      for (uint32_t j = 0; j < (uint32_t)B; ++j) {
+        const uint32_t qj = rl(pk, j);
+        const uint32_t lt = below_mask(j, lane), gt = below_mask(lane, j);   // j < i, j > i
+        const uint32_t eq_q = zero_mask(qj ^ qi), eq_t = zero_mask(qj ^ ti);
+        a1 = umax(a1, eq_q & lt & (j + 1u));
+        b1 = umax(b1, eq_t & lt & (j + 1u));
+        nx = umin(nx, j | (~(eq_q & gt) & 64u));
       }
+      uint32_t root = b1 ? b1 - 1u : lane;
+      for (int step = 0; step < 6; ++step)
+        root = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(root << 2), (int)root);
+      const uint32_t ovv = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(root << 2), (int)tv);   // moved_i
+      const uint32_t via = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((a1 ? a1 - 1u : lane) << 2), (int)ovv);
+      const uint32_t mine = a1 ? via : pv;      // lane i: the message event i delivers
       // ---- POST /message (node.ts:45-158), all B deliveries at once: each
       // adds {len, c0 | c1} to its receiver's inbox slot unless the receiver is
       // killed (node.ts:45) or the round is beyond the oracle's window.  When
@@ -285,15 +317,9 @@ __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
           }
         }
       }
-      // ---- the batch's pool writes (the last write to each position wins)
-      {
-        bool live = lane < used && ovp < len - used;
-        for (uint32_t j = 1; j < used; ++j) {
-          const uint32_t v = rl(ovp, j);
-          live = live && !(j > lane && v == ovp);
-        }
-        if (live) pool[ovp] = ovv;
-      }
+      // ---- the batch's pool writes: each used event's, unless a later used
+      // event overwrites its position or the position was popped
+      if (lane < used && nx >= used && qi < len - used) pool[qi] = ovv;
       len -= used;
       rng += (uint64_t)used * kGamma;
       e += used;
