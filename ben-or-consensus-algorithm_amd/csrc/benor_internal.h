@@ -112,6 +112,9 @@ struct KParams {
   // diagnostics (BENOR_TIMELINE=<file>, packed matrix-core kernel): per wave,
   // kTimelineWords u64 -- wall-clock stamps of its phases and its batch counts
   unsigned long long *timeline;
+  // packed matrix-core kernel: tail batch with round-3 shadow slots (A/B knob
+  // BENOR_SMALL_SPEC=0 turns it off)
+  uint32_t small_spec;
 };
 
 constexpr uint32_t kTimelineWords = 12;

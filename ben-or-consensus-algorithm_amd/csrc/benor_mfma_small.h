@@ -267,7 +267,7 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
       // slots, slot s + SA runs round 3 of slot s's trial speculatively (used
       // only if slot s ties), and the slots left over take round-3 entries:
       // one batch instead of a round-2 and a round-3 partial batch.
-      if (kSmallSpecSlots<S> > 0u && R >= 3u && n <= 64u * kSmallSpecSlots<S>) {
+      if (kSmallSpecSlots<S> > 0u && R >= 3u && p.small_spec && n <= 64u * kSmallSpecSlots<S>) {
         spec = true;
         n3 = len3 < 64u * (S - 2u * kSmallSpecSlots<S>) ? len3 : 64u * (S - 2u * kSmallSpecSlots<S>);
         len3 -= n3;
