@@ -97,6 +97,9 @@ def test_bench_single_gpu_line():
     net = oc.pop("C4 N=1024,F=341 network API, mid-run /stop")   # one network through the drop-in API
     assert net["stop inside round 1"]["stopped_nodes"] == 1 and net["stop inside round 1"]["seconds"] > 0
     assert net["no stop (lockstep kernel)"]["stopped_nodes"] == 0
+    live = net["live start, /stop sent after it"]
+    assert live["stopped_nodes"] == 1 and live["stop_landed_at_delivery"] is not None
+    assert live["start_returned_after_s"] < live["seconds"]
     sweep = oc.pop("C5 sweep (2^30 trials, 224 cells)")          # configs[4] end to end, CSV checked
     assert sweep["cells"] == 224 and sweep["trials"] > 2 ** 29 and sweep["csv_equals_results_r02_sweep_c5"] is True
     for k, v in oc.items():
