@@ -82,6 +82,7 @@ struct BigState {
   uint64_t *killed;   // [64]
   uint64_t *decided;  // [64]
   uint64_t *comp;     // [4][64] completion of round k at k & 3
+  uint32_t *picks;    // [2048] a batch's pick positions, low 16 bits as a bitmap
 };
 
 }  // namespace
@@ -103,6 +104,8 @@ __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
   S.ks = reinterpret_cast<int16_t *>(S.comp + 4 * 64);
   S.cidx = reinterpret_cast<uint16_t *>(S.ks + ((N + 3u) & ~3u));
   S.xs = reinterpret_cast<int8_t *>(S.cidx + ((N + 3u) & ~3u));
+  S.picks = reinterpret_cast<uint32_t *>(S.xs + ((N + 15u) & ~15u));
+  for (uint32_t i = lane; i < 2048u; i += 64u) S.picks[i] = 0u;
   const uint64_t allw = lane < NWd ? (N >= 64u * (lane + 1u) ? ~0ull : (1ull << (N - 64u * lane)) - 1ull) : 0ull;
   const uint64_t wmask = NWd >= 64u ? ~0ull : ((1ull << NWd) - 1ull);   // lanes holding a bitset word
   const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
@@ -248,22 +251,39 @@ __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
       //   msg_i = moved_a (a exists) else pool[q_i];
       // and event i's write is the position's last one iff no later event
       // of the batch picks q_i (nx = the first such j).
+      // Usually no two picks of a batch share a position and no pick is one of
+      // the batch's tail positions (~64^2 / len): a 64 K-bit LDS bitmap of the
+      // picks' low 16 bits finds the batches that may have one (q-q or q-t key
+      // collisions, ~10 % at len ~ 7·10^5 with false positives), and only those
+      // run the scan.
       const uint32_t qi = pk, ti = len - 1u - lane;
       uint32_t a1 = 0u, b1 = 0u, nx = 64u;      // a + 1, b + 1 (0: none)
-      for (uint32_t j = 0; j < (uint32_t)B; ++j) {
-        const uint32_t qj = rl(pk, j);
-        const uint32_t lt = below_mask(j, lane), gt = below_mask(lane, j);   // j < i, j > i
-        const uint32_t eq_q = zero_mask(qj ^ qi), eq_t = zero_mask(qj ^ ti);
-        a1 = umax(a1, eq_q & lt & (j + 1u));
-        b1 = umax(b1, eq_t & lt & (j + 1u));
-        nx = umin(nx, j | (~(eq_q & gt) & 64u));
+      uint32_t ovv = tv, mine = pv;             // moved_i, and the message event i delivers
+      bool maybe = false;
+      if (lane < B) {
+        const uint32_t kq = qi & 0xFFFFu, kt = ti & 0xFFFFu;
+        const uint32_t old = atomicOr(&S.picks[kq >> 5], 1u << (kq & 31u));
+        maybe = (old >> (kq & 31u)) & 1u;
+        asm volatile("" ::: "memory");           // the read below after every lane's mark (in-order LDS)
+        maybe = maybe || ((S.picks[kt >> 5] >> (kt & 31u)) & 1u);
       }
-      uint32_t root = b1 ? b1 - 1u : lane;
-      for (int step = 0; step < 6; ++step)
-        root = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(root << 2), (int)root);
-      const uint32_t ovv = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(root << 2), (int)tv);   // moved_i
-      const uint32_t via = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((a1 ? a1 - 1u : lane) << 2), (int)ovv);
-      const uint32_t mine = a1 ? via : pv;      // lane i: the message event i delivers
+      if (__any(maybe)) {
+        for (uint32_t j = 0; j < (uint32_t)B; ++j) {
+          const uint32_t qj = rl(pk, j);
+          const uint32_t lt = below_mask(j, lane), gt = below_mask(lane, j);   // j < i, j > i
+          const uint32_t eq_q = zero_mask(qj ^ qi), eq_t = zero_mask(qj ^ ti);
+          a1 = umax(a1, eq_q & lt & (j + 1u));
+          b1 = umax(b1, eq_t & lt & (j + 1u));
+          nx = umin(nx, j | (~(eq_q & gt) & 64u));
+        }
+        uint32_t root = b1 ? b1 - 1u : lane;
+        for (int step = 0; step < 6; ++step)
+          root = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(root << 2), (int)root);
+        ovv = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(root << 2), (int)tv);
+        const uint32_t via = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((a1 ? a1 - 1u : lane) << 2), (int)ovv);
+        mine = a1 ? via : pv;
+      }
+      if (lane < B) S.picks[(qi & 0xFFFFu) >> 5] = 0u;   // the bitmap is empty again for the next batch
       // ---- POST /message (node.ts:45-158), all B deliveries at once: each
       // adds {len, c0 | c1} to its receiver's inbox slot unless the receiver is
       // killed (node.ts:45) or the round is beyond the oracle's window.  When
@@ -405,7 +425,7 @@ __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
 
 uint32_t event_big_lds_bytes(const KParams &p) {
   const uint32_t N = p.N;
-  return p.hist_bytes + 16u * N + 8u * 64u * 6u + 2u * ((N + 3u) & ~3u) * 2u + ((N + 15u) & ~15u);
+  return p.hist_bytes + 16u * N + 8u * 64u * 6u + 2u * ((N + 3u) & ~3u) * 2u + ((N + 15u) & ~15u) + 2048u * 4u;
 }
 
 hipError_t launch_event_big(const KParams &p, int grid, hipStream_t s) {
