@@ -83,6 +83,7 @@ struct BigState {
   uint64_t *decided;  // [64]
   uint64_t *comp;     // [4][64] completion of round k at k & 3
   uint32_t *picks;    // [2048] a batch's pick positions, low 16 bits as a bitmap
+  uint32_t *wrote;    // [2048] the positions a batch wrote back, likewise
 };
 
 }  // namespace
@@ -105,6 +106,7 @@ __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
   S.cidx = reinterpret_cast<uint16_t *>(S.ks + ((N + 3u) & ~3u));
   S.xs = reinterpret_cast<int8_t *>(S.cidx + ((N + 3u) & ~3u));
   S.picks = reinterpret_cast<uint32_t *>(S.xs + ((N + 15u) & ~15u));
+  S.wrote = S.picks + 2048;
   for (uint32_t i = lane; i < 2048u; i += 64u) S.picks[i] = 0u;
   const uint64_t allw = lane < NWd ? (N >= 64u * (lane + 1u) ? ~0ull : (1ull << (N - 64u * lane)) - 1ull) : 0ull;
   const uint64_t wmask = NWd >= 64u ? ~0ull : ((1ull << NWd) - 1ull);   // lanes holding a bitset word
@@ -168,6 +170,11 @@ __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
     __threadfence_block();
     uint32_t next = 0, cur = 1, R = 0, halted = 0, seen = 0;
     long long polled = wall_clock64() - (long long)kLivePollTicks;   // the first batch polls
+    // the next batch's picks and pool words, loaded while this batch resolves
+    // (valid when it starts at pf_e with pf_len messages and pf_b events)
+    uint32_t pf_pk = 0u, pf_pv = 0u, pf_tv = 0u, pf_len = 0u, wq = 0xFFFFFFFFu;
+    uint64_t pf_e = ~0ull, pf_b = 0ull;
+    for (uint32_t i = lane; i < 2048u; i += 64u) S.wrote[i] = 0u;
     bool overflow = false;
     uint64_t e = 0;
     auto advance = [&]() {                      // complete rounds: halting (node.ts:116-145 as DESIGN §2)
@@ -233,12 +240,55 @@ __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
         if (until < B) B = until;
       }
       uint32_t pk = 0, pv = 0, tv = 0;
-      if (lane < B) {
+      // agent-scope loads are L2-served (no stale L1 line after the last batch's stores)
+      auto load = [&](uint32_t i) { return __hip_atomic_load(&pool[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+      if (pf_e == e && pf_len == len && pf_b == B) {
+        // the previous batch ran to its end: its prefetch is this batch, except
+        // for the words that batch wrote after they were read (S.wrote marks
+        // them by their low 16 bits; a false match only reloads)
+        pk = pf_pk;
+        pv = pf_pv;
+        tv = pf_tv;
+        bool stale = false;
+        if (lane < B) {
+          const uint32_t kq = pk & 0xFFFFu, kt = (len - 1u - lane) & 0xFFFFu;
+          stale = ((S.wrote[kq >> 5] >> (kq & 31u)) & 1u) || ((S.wrote[kt >> 5] >> (kt & 31u)) & 1u);
+        }
+        if (stale) {
+          pv = load(pk);
+          tv = load(len - 1u - lane);
+        }
+      } else if (lane < B) {
         const uint64_t z = mix64(rng + (uint64_t)(lane + 1u) * kGamma);
         pk = (uint32_t)(((uint64_t)(uint32_t)(z >> 32) * (uint64_t)(len - lane)) >> 32);
-        // agent-scope loads are L2-served (no stale L1 line after the last batch's stores)
-        pv = __hip_atomic_load(&pool[pk], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        tv = __hip_atomic_load(&pool[len - 1u - lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pv = load(pk);
+        tv = load(len - 1u - lane);
+      }
+      if (wq != 0xFFFFFFFFu) S.wrote[(wq & 0xFFFFu) >> 5] = 0u;   // the previous batch's marks are spent
+      wq = 0xFFFFFFFFu;
+      // ---- prefetch: the next batch's picks and words, as if this batch runs to
+      // its end without a trigger (no scheduled stop at its end)
+      pf_e = ~0ull;
+      {
+        const uint32_t len2 = len - (uint32_t)B;
+        uint64_t B2 = len2 < 64u ? len2 : 64u;
+        bool ok = len2 > 0u;
+        if (next < p.ev_nstops) {
+          const uint64_t until2 = (p.ev_stops[next] >> 12) - (e + B);
+          if (until2 == 0u) ok = false;
+          else if (until2 < B2) B2 = until2;
+        }
+        if (ok) {
+          pf_e = e + B;
+          pf_len = len2;
+          pf_b = B2;
+          if (lane < B2) {
+            const uint64_t z = mix64(rng + (uint64_t)((uint32_t)B + lane + 1u) * kGamma);
+            pf_pk = (uint32_t)(((uint64_t)(uint32_t)(z >> 32) * (uint64_t)(len2 - lane)) >> 32);
+            pf_pv = load(pf_pk);
+            pf_tv = load(len2 - 1u - lane);
+          }
+        }
       }
       // ---- the batch's messages.  Event i takes the message at q_i = pk and
       // moves the one at t_i = len - 1 - i there (swap-remove).  As the batch's
@@ -339,7 +389,11 @@ __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
       }
       // ---- the batch's pool writes: each used event's, unless a later used
       // event overwrites its position or the position was popped
-      if (lane < used && nx >= used && qi < len - used) pool[qi] = ovv;
+      if (lane < used && nx >= used && qi < len - used) {
+        pool[qi] = ovv;
+        atomicOr(&S.wrote[(qi & 0xFFFFu) >> 5], 1u << (qi & 31u));   // for the next batch's prefetch
+        wq = qi;
+      }
       len -= used;
       rng += (uint64_t)used * kGamma;
       e += used;
@@ -425,7 +479,7 @@ __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
 
 uint32_t event_big_lds_bytes(const KParams &p) {
   const uint32_t N = p.N;
-  return p.hist_bytes + 16u * N + 8u * 64u * 6u + 2u * ((N + 3u) & ~3u) * 2u + ((N + 15u) & ~15u) + 2048u * 4u;
+  return p.hist_bytes + 16u * N + 8u * 64u * 6u + 2u * ((N + 3u) & ~3u) * 2u + ((N + 15u) & ~15u) + 2u * 2048u * 4u;
 }
 
 hipError_t launch_event_big(const KParams &p, int grid, hipStream_t s) {
