@@ -242,7 +242,7 @@ __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
       uint32_t pk = 0, pv = 0, tv = 0;
       // agent-scope loads are L2-served (no stale L1 line after the last batch's stores)
       auto load = [&](uint32_t i) { return __hip_atomic_load(&pool[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-      if (pf_e == e && pf_len == len && pf_b == B) {
+      if (p.ev_fast && pf_e == e && pf_len == len && pf_b == B) {
         // the previous batch ran to its end: its prefetch is this batch, except
         // for the words that batch wrote after they were read (S.wrote marks
         // them by their low 16 bits; a false match only reloads)
@@ -272,7 +272,7 @@ __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
       {
         const uint32_t len2 = len - (uint32_t)B;
         uint64_t B2 = len2 < 64u ? len2 : 64u;
-        bool ok = len2 > 0u;
+        bool ok = p.ev_fast && len2 > 0u;
         if (next < p.ev_nstops) {
           const uint64_t until2 = (p.ev_stops[next] >> 12) - (e + B);
           if (until2 == 0u) ok = false;
@@ -309,8 +309,8 @@ __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
       const uint32_t qi = pk, ti = len - 1u - lane;
       uint32_t a1 = 0u, b1 = 0u, nx = 64u;      // a + 1, b + 1 (0: none)
       uint32_t ovv = tv, mine = pv;             // moved_i, and the message event i delivers
-      bool maybe = false;
-      if (lane < B) {
+      bool maybe = !p.ev_fast;
+      if (p.ev_fast && lane < B) {
         const uint32_t kq = qi & 0xFFFFu, kt = ti & 0xFFFFu;
         const uint32_t old = atomicOr(&S.picks[kq >> 5], 1u << (kq & 31u));
         maybe = (old >> (kq & 31u)) & 1u;
@@ -333,7 +333,7 @@ __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
         const uint32_t via = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((a1 ? a1 - 1u : lane) << 2), (int)ovv);
         mine = a1 ? via : pv;
       }
-      if (lane < B) S.picks[(qi & 0xFFFFu) >> 5] = 0u;   // the bitmap is empty again for the next batch
+      if (p.ev_fast && lane < B) S.picks[(qi & 0xFFFFu) >> 5] = 0u;   // the bitmap is empty again for the next batch
       // ---- POST /message (node.ts:45-158), all B deliveries at once: each
       // adds {len, c0 | c1} to its receiver's inbox slot unless the receiver is
       // killed (node.ts:45) or the round is beyond the oracle's window.  When
@@ -391,8 +391,10 @@ __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
       // event overwrites its position or the position was popped
       if (lane < used && nx >= used && qi < len - used) {
         pool[qi] = ovv;
-        atomicOr(&S.wrote[(qi & 0xFFFFu) >> 5], 1u << (qi & 31u));   // for the next batch's prefetch
-        wq = qi;
+        if (p.ev_fast) {
+          atomicOr(&S.wrote[(qi & 0xFFFFu) >> 5], 1u << (qi & 31u));   // for the next batch's prefetch
+          wq = qi;
+        }
       }
       len -= used;
       rng += (uint64_t)used * kGamma;

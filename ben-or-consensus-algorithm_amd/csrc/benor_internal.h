@@ -115,6 +115,9 @@ struct KParams {
   // packed matrix-core kernel: tail batch with round-3 shadow slots (A/B knob
   // BENOR_SMALL_SPEC=0 turns it off)
   uint32_t small_spec;
+  // event level, big kernel: the collision bitmap and the next-batch prefetch
+  // (A/B knob BENOR_EVENT_FAST=0: every batch scans and loads its own words)
+  uint32_t ev_fast;
 };
 
 constexpr uint32_t kTimelineWords = 12;

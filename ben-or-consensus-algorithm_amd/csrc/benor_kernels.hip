@@ -739,6 +739,10 @@ void plan_geometry(KParams &p) {
     p.nblocks = 1;
     p.variant = 5;
     p.wave_bytes = 0;
+    {
+      const char *fast = getenv("BENOR_EVENT_FAST");
+      p.ev_fast = fast && fast[0] == '0' ? 0u : 1u;
+    }
     p.ev_cap = 4u * p.N * p.N + 64u;
     p.ev_stride = p.ev_cap;                          // u32 messages
     p.lds_bytes = event_big_lds_bytes(p);

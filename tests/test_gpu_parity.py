@@ -477,6 +477,28 @@ def test_event_mode_big_without_stop_equals_lockstep_kernel():
         np.testing.assert_array_equal(a, b)
 
 
+def test_event_mode_big_fast_paths_off_equal_on():
+    """BENOR_EVENT_FAST=0 (every batch scans its picks and loads its own pool
+    words) and the default (collision bitmap, next-batch prefetch) give the same
+    histograms and per-node states: the fast paths change no delivery."""
+    N, F = 1024, 341
+    fl = first_f(N, F)
+    m = N - F
+    vals = [0] * F + [1] * (m // 2) + [0] * (m // 2) + ["?"]
+    sched = [None] * N
+    sched[500] = 400_000
+    fast = benor.TrialsPlan(N, F, fl, seed=5, k_max=8, mode=EV, crash_at=sched, initial_values=vals).run(0, 3)
+    _, st_fast = benor.run_trial_states(N, F, fl, seed=5, trial=0, k_max=8, mode=EV, crash_at=sched)
+    os.environ["BENOR_EVENT_FAST"] = "0"
+    try:
+        slow = benor.TrialsPlan(N, F, fl, seed=5, k_max=8, mode=EV, crash_at=sched, initial_values=vals).run(0, 3)
+        _, st_slow = benor.run_trial_states(N, F, fl, seed=5, trial=0, k_max=8, mode=EV, crash_at=sched)
+    finally:
+        os.environ.pop("BENOR_EVENT_FAST", None)
+    np.testing.assert_array_equal(fast, slow)
+    assert st_fast == st_slow
+
+
 def test_event_mode_big_states_match_oracle():
     """Per-node states of one trial (bo_run_trial_states, the network API's
     launch) at N = 1024 with two scheduled stops in round 1."""
