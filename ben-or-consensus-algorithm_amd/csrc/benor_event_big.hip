@@ -25,12 +25,16 @@
 //     which a trigger changes).  Events go in batches of up to 64: lane i
 //     computes the pick of event e + i assuming no trigger (splitmix64 is a
 //     counter: state e + i is state e + (i + 1) * gamma) and loads both pool
-//     words the swap-remove touches, so one HBM round trip serves 64 events;
-//     the wave then applies them in order, resolving the batch's own earlier
-//     writes through a 64-entry overlay (lane j: position and value written by
-//     event j).  A trigger ends the batch: the overlay is written back, the
-//     triggered broadcast is appended, and the next batch starts after it.
-//     Batches also end before a scheduled stop.
+//     words the swap-remove touches, so one HBM round trip serves 64 events
+//     (and the next batch's words are loaded while this one resolves).  The
+//     batch's messages are resolved in parallel -- which earlier event of the
+//     batch last wrote a lane's pick or tail position, by a scan that an LDS
+//     bitmap of the picks skips in most batches, and pointer jumping along the
+//     swap-remove chains -- and its deliveries are applied at once unless an
+//     inbox reaches its quorum inside the batch (then the batch replays one
+//     delivery at a time up to that trigger).  A trigger ends the batch: the
+//     used events' writes go back, the triggered broadcast is appended, and
+//     the next batch starts after it.  Batches also end before a scheduled stop.
 //   * a live run (bo_consensus_start_live, any N) also polls a host-mapped
 //     mailbox between batches, about every 10 us of wall clock, for GET /stop
 //     requests served while it runs; a request is applied before the next
