@@ -112,9 +112,6 @@ struct KParams {
   // diagnostics (BENOR_TIMELINE=<file>, packed matrix-core kernel): per wave,
   // kTimelineWords u64 -- wall-clock stamps of its phases and its batch counts
   unsigned long long *timeline;
-  // packed matrix-core kernel: tail batch with round-3 shadow slots (A/B knob
-  // BENOR_SMALL_SPEC=0 turns it off)
-  uint32_t small_spec;
   // event level, big kernel: the collision bitmap and the next-batch prefetch
   // (A/B knob BENOR_EVENT_FAST=0: every batch scans and loads its own words)
   uint32_t ev_fast;
@@ -161,10 +158,6 @@ hipError_t launch_lane_m(const KParams &p, int grid_blocks, hipStream_t stream);
 template <int MM>
 hipError_t launch_mfma_small_m(const KParams &p, int grid_blocks, hipStream_t stream);
 constexpr uint32_t small_slots(uint32_t m) { return (32u / m) < 8u ? (32u / m) : 8u; }
-// Tail batch of the packed kernel: slots given to round-2 entries, each with a
-// round-3 shadow slot (S / 2; 0 when a batch has a single slot).
-template <uint32_t S>
-constexpr uint32_t kSmallSpecSlots = S / 2u;
 constexpr uint32_t kSmallMaxRound = 3;   // rounds on the matrix cores; a later tie -> the lane path
 // LDS words per wave: round-2 and round-3 lists (2 batches each), lane-path queue (a batch + 64)
 constexpr uint32_t small_wave_words(uint32_t m) { return 5u * 64u * small_slots(m) + 64u; }

@@ -804,8 +804,6 @@ void plan_geometry(KParams &p) {
       p.base_G = p.G;
       p.variant = 8;
       p.lds_bytes = p.hist_bytes + kWavesPerBlock * small_wave_words(p.m) * 4u;   // histogram, round lists
-      const char *spec = getenv("BENOR_SMALL_SPEC");
-      p.small_spec = spec && spec[0] == '0' ? 0u : 1u;
     }
     return;
   }

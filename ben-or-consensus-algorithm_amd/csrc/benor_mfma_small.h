@@ -252,28 +252,13 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
   for (;;) {
     // ---- the next batch: the deepest full list, else fresh round-1 trials
     // (batch g, g + waves_total, ...), else the partial lists
-    uint32_t r, n, n3 = 0u;
-    const uint32_t *src = nullptr, *src3 = nullptr;
+    uint32_t r, n;
+    const uint32_t *src = nullptr;
     uint32_t kind;
-    bool spec = false;                                  // the tail batch (below)
     if (R >= 3u && len3 >= BATCH) { r = 3u; n = BATCH; len3 -= n; src = list3 + len3; kind = 2u; }
     else if (R >= 2u && len2 >= BATCH) { r = 2u; n = BATCH; len2 -= n; src = list2 + len2; kind = 1u; }
     else if (g < ngroups) { r = 1u; n = trial_count - g * BATCH; n = n < BATCH ? n : BATCH; kind = 0u; }
-    else if (len2) {
-      r = 2u; n = len2; src = list2; len2 = 0u; kind = 3u;
-      // Tail batch: a trial that tied in round 1 has x = its round-1 coins for
-      // round 2 and, if round 2 ties too, x = its round-2 coins for round 3 --
-      // words 0 and 1 of one coin block.  So when the round-2 list fits SA
-      // slots, slot s + SA runs round 3 of slot s's trial speculatively (used
-      // only if slot s ties), and the slots left over take round-3 entries:
-      // one batch instead of a round-2 and a round-3 partial batch.
-      if (kSmallSpecSlots<S> > 0u && R >= 3u && p.small_spec && n <= 64u * kSmallSpecSlots<S>) {
-        spec = true;
-        n3 = len3 < 64u * (S - 2u * kSmallSpecSlots<S>) ? len3 : 64u * (S - 2u * kSmallSpecSlots<S>);
-        len3 -= n3;
-        src3 = list3 + len3;
-      }
-    }
+    else if (len2) { r = 2u; n = len2; src = list2; len2 = 0u; kind = 3u; }
     else if (len3) { r = 3u; n = len3; src = list3; len3 = 0u; kind = 4u; }
     else break;
     if (tl) {
@@ -298,11 +283,6 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
       const uint32_t e = s * 64u + lane;
       const uint32_t gb = g * BATCH + e;
       toff[s] = e < n ? (src ? src[e] : gb) : EMPTY;
-      if (spec) {                                       // A slots, their B shadows, round-3 entries
-        constexpr uint32_t SA = kSmallSpecSlots<S>;
-        const uint32_t ea = (s < SA ? s : s - SA) * 64u + lane, ec = (s - 2u * SA) * 64u + lane;
-        toff[s] = s < 2u * SA ? (ea < n ? src[ea] : EMPTY) : (ec < n3 ? src3[ec] : EMPTY);
-      }
       const uint64_t tr = tb + (toff[s] & 0x7FFFFFFFu);
       blk[s] = make_uint4((uint32_t)tr, (uint32_t)(tr >> 32), 0u, c3);
     }
@@ -312,8 +292,7 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
     uint32_t w = 0u;
 #pragma unroll
     for (uint32_t s = 0; s < S; ++s) {
-      const uint32_t ws = spec ? (s < kSmallSpecSlots<S> ? 0u : 1u) : wsel;   // spec: round 2 / round 3 coins
-      uint32_t x = ws == 0u ? blk[s].x : ws == 1u ? blk[s].y : ws == 2u ? blk[s].z : blk[s].w;
+      uint32_t x = wsel == 0u ? blk[s].x : wsel == 1u ? blk[s].y : wsel == 2u ? blk[s].z : blk[s].w;
       if (r == 1u) x = bsel(rmask, x, fixed1);
       uint32_t keep = (toff[s] >> 31) - 1u;               // ~0 unless the slot is EMPTY
       asm("" : "+v"(keep));                               // a mask, not a select
@@ -369,46 +348,6 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
     // lane path after round R; receivers not unanimous (impossible in
     // lockstep) -> the lane path.  (The ORs are < 2^31: 0 - o has bit 31 set
     // iff o != 0.)
-    if (spec) {
-      // A slot s: round 2 (halt, or tie -> its B slot s + SA, or odd -> rerun);
-      // B slot: round 3 of a tied A slot's trial; C slot: a round-3 entry.
-      // After round 3 a tie goes to the lane path (R = 3), as below.
-      constexpr uint32_t SA = kSmallSpecSlots<S>;
-      uint32_t c1a = 0u, c0a = 0u, c1b = 0u, c0b = 0u, tieA[SA > 0u ? SA : 1u];
-#pragma unroll
-      for (uint32_t s = 0; s < S; ++s) {
-        uint32_t valid = (toff[s] >> 31) ^ 1u;
-        if (s >= SA && s < 2u * SA) valid &= tieA[s - SA];
-        const uint32_t n1 = (0u - o1[s]) >> 31, n0 = (0u - o0[s]) >> 31, nq = (0u - oq[s]) >> 31;
-        const uint32_t h1v = valid & (n1 ^ 1u), h0v = valid & n1 & (n0 ^ 1u);
-        const uint32_t tie = valid & n1 & n0 & (nq ^ 1u), odd = valid & n1 & n0 & nq;
-        if (s < SA) { c1a += h1v; c0a += h0v; tieA[s] = tie; }
-        else { c1b += h1v; c0b += h0v; }
-        const uint32_t toq = s < SA ? 0u : tie;         // round-3 ties continue on the lane path
-        const uint64_t bt = ballot(toq != 0u);
-        if (toq) lq[lql + __builtin_amdgcn_mbcnt_hi((uint32_t)(bt >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bt, 0u))] = toff[s];
-        lql += (uint32_t)__popcll(bt);
-        const uint64_t bo = ballot(odd != 0u);          // impossible in lockstep: re-run from round 1
-        if (odd) lq[lql + __builtin_amdgcn_mbcnt_hi((uint32_t)(bo >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bo, 0u))] = toff[s] | 0x80000000u;
-        lql += (uint32_t)__popcll(bo);
-      }
-      uint32_t t1a = 0u, t0a = 0u, t1b = 0u, t0b = 0u;
-#pragma unroll
-      for (uint32_t b = 0; (1u << b) <= S; ++b) {
-        t1a += (uint32_t)__popcll(ballot(((c1a >> b) & 1u) != 0u)) << b;
-        t0a += (uint32_t)__popcll(ballot(((c0a >> b) & 1u) != 0u)) << b;
-        t1b += (uint32_t)__popcll(ballot(((c1b >> b) & 1u) != 0u)) << b;
-        t0b += (uint32_t)__popcll(ballot(((c0b >> b) & 1u) != 0u)) << b;
-      }
-      h1[1] += t1a; h0[1] += t0a;
-      h1[2] += t1b; h0[2] += t0b;
-      while (lql >= 64u) {
-        lql -= 64u;
-        small_lane_path<MM>(keys, lq[lql + lane], fixed1, random_init, F, k_max, R, lhist, hist_len);
-        if (tl) ++nb[5];
-      }
-      continue;
-    }
     const bool last = r >= R;
     uint32_t *dst = last ? lq : (r == 1u ? list2 : list3);
     uint32_t dlen = last ? lql : (r == 1u ? len2 : len3);

@@ -150,19 +150,6 @@ def test_mfma_small_equals_lane_kernel(N, F, T):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("N,F,k_max", [(10, 4, 16), (5, 1, 3), (12, 3, 4), (9, 2, 16)])
-def test_mfma_small_tail_batch_equals_without(monkeypatch, N, F, k_max):
-    """The tail batch (round 3 in shadow slots of the round-2 batch) against
-    BENOR_SMALL_SPEC=0 (separate round-2 and round-3 partial batches): the
-    same histogram, at k_max = 3 (round 3 is the last) and beyond."""
-    a = plan(N, F, True, seed=0x5EED ^ N, k_max=k_max)
-    ha = a.run(0, 700_001)
-    monkeypatch.setenv("BENOR_SMALL_SPEC", "0")
-    b = plan(N, F, True, seed=0x5EED ^ N, k_max=k_max)
-    np.testing.assert_array_equal(ha, b.run(0, 700_001))
-
-
-@pytest.mark.gpu
 @pytest.mark.parametrize("T", [300_000, 1_000_000])
 def test_short_launch_crossover_same_histogram(monkeypatch, T):
     """Under the default crossover (5*10^5 trials) a 3*10^5-trial launch of
