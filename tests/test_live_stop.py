@@ -208,3 +208,33 @@ def test_js_live_stop_replays_through_oracle(tmp_path):
                                             set(c["stops"]))
         for i in c["stops"]:
             assert r["states"][i]["killed"]
+
+
+@pytest.mark.gpu
+def test_live_edge_cases():
+    """A one-node network; a /stop posted twice and to a faulty node (both
+    no-ops beyond the first); a network dropped while its live run is in flight
+    (destroy waits for it); a second live start (refused, error 8)."""
+    # N = 1: the lone node decides its own value in round 1, all decided -> auto-stop
+    net = benor.Network(1, 0, [1], [False])
+    net.start_live(seed=1, k_max=16)
+    net.wait()
+    assert net.get_state(0) == {"killed": True, "x": 1, "decided": True, "k": 2}
+    # repeated and faulty-node stops
+    N, F, seed = 1024, 341, 66
+    faulty, init = shape(N, F, half(N - F))
+    net = benor.Network(N, F, init, faulty)
+    net.start_live(seed=seed, k_max=16)
+    net.stop_node(700)
+    net.stop_node(700)
+    net.stop_node(3)                                  # faulty from launch: already killed
+    with pytest.raises(benor.AlreadyStartedError):
+        net.start_live(seed=seed, k_max=16)
+    net.wait()
+    ev = net.live_stop_events()
+    assert ev[3] is None and sum(v is not None for v in ev) == (ev[700] is not None)
+    assert [net.get_state(i) for i in range(N)] == expected_live(N, F, faulty, init, seed, 16, ev, {3, 700})
+    # dropped mid-run: the handle's destructor waits for the kernel
+    other = benor.Network(N, F, init, faulty)
+    other.start_live(seed=seed + 1, k_max=16)
+    del other
