@@ -337,13 +337,14 @@ def event_network(benor, N=1024, F=341, stop_node=500, stop_after=300_000, seed=
         st = benor.getNodesState(N)
         out[label] = {"seconds": dt, "stopped_nodes": sum(1 for s in st[F:] if s["killed"])}
     # live start (bo_consensus_start_live): startConsensus returns at launch, the
-    # /stop is sent afterwards and lands in the running kernel; the run ends at
+    # /stop is sent 5 ms later and lands in the running kernel; the run ends at
     # getNodesState.  Reported: the wall time from the start to the final states
     # and where the stop landed (replayable as a schedule).
     benor.launchNetwork(N, F, init, faulty)
     t0 = time.perf_counter()
     benor.startConsensus(N, seed=seed, live=True)
     t_start = time.perf_counter() - t0
+    time.sleep(0.005)                                # the run is under way: the stop lands mid-round
     benor._current.stop_node(stop_node)
     st = benor.getNodesState(N)
     dt = time.perf_counter() - t0
