@@ -273,7 +273,11 @@ __global__ void __launch_bounds__(256) benor_mfma_kernel(KParams p) {
     if constexpr (SURE && W <= 4) {
       // Few products per tile (W): the sign packing of tile i - 1 is issued
       // among tile i's products, a few VALU per MFMA, so it runs in their
-      // shadow (two accumulators live).
+      // shadow (two accumulators live).  The wave raises its issue priority for
+      // the two product phases (back to 0 after the P-phase fold), so another
+      // wave's Philox / expansion VALU fills the matrix core's gaps rather than
+      // delaying its products: configs[2] -3 % (profiles/r04-o_setprio_ab.jsonl).
+      __builtin_amdgcn_s_setprio(1);
       mf_v16f racc[2];
 #pragma unroll
       for (int i = 0; i <= MT; ++i) {
@@ -364,6 +368,7 @@ __global__ void __launch_bounds__(256) benor_mfma_kernel(KParams p) {
           }
           __builtin_amdgcn_sched_barrier(0);
         }
+        __builtin_amdgcn_s_setprio(0);
       } else
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
