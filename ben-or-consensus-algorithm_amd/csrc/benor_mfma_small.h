@@ -305,6 +305,10 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
 #pragma unroll
     for (int v = 0; v < 4; ++v) bx[v] = Ex[v] | Ez[v] | (Ez[v] << 2);
 
+    // The products and their folds at raised issue priority (back to 0 for the
+    // outcome bookkeeping), so another wave's Philox fills the matrix core's gaps
+    // (steady state -1..-5 %, profiles/r04-q_small_setprio_ab.jsonl).
+    __builtin_amdgcn_s_setprio(1);
     // ---- R-phase: 8 (c1 - c0) per receiver row -> proposal nibbles (+6 / -6 / 0)
     mf_v4i bp;
     {
@@ -342,6 +346,7 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
       __builtin_amdgcn_sched_barrier(0);
     }
 
+    __builtin_amdgcn_s_setprio(0);
     // ---- per slot: every receiver decided 1 (node.ts:102-105) / decided 0
     // (node.ts:99-101) -> halted in round r (auto-stop, node.ts:116-145); every
     // receiver flipped its coin (node.ts:110-111) -> round r + 1's list, or the
