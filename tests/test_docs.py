@@ -1,0 +1,64 @@
+"""Documentation drift: every repo path the docs cite exists.
+
+The docs cite profiles, tools, sources and tests by path; a renamed or deleted
+file leaves a dangling reference that no other test sees.
+"""
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = "ben-or-consensus-algorithm_amd"
+DOCS = ["DESIGN.md", "README.md", "BASELINE.md", "INTEGRATION.md", "profiles/README.md"]
+# a backquoted path under one of the repo's own top-level directories
+CITED = re.compile(r"`((?:profiles|tools|tests|oracle|include|csrc|js|benor|results)/[^`\s:]+)")
+
+
+def cited_paths(doc):
+    text = open(os.path.join(ROOT, doc), encoding="utf-8").read()
+    out = set()
+    for m in CITED.finditer(text):
+        p = m.group(1).rstrip(".")
+        p = p.split("::")[0]
+        if any(c in p for c in "*<>{}") or p.endswith("/"):
+            continue                                   # globs, templates, directories
+        out.add(p)
+    return sorted(out)
+
+
+# r01-r03's one-off GPU wrappers, folded into tools/gpu.sh (profiles/README.md
+# says so); DESIGN.md still names the one behind each committed profile.
+RETIRED = {"tools/ab.sh", "tools/c5_breakdown.sh", "tools/gpu_c5_prof.sh", "tools/gpu_event_check.sh",
+           "tools/gpu_mfma_ab.sh", "tools/gpu_r02c.sh", "tools/gpu_r02d.sh", "tools/gpu_r02g.sh",
+           "tools/gpu_r02j.sh", "tools/gpu_trace_shapes.sh", "tools/prof_shape.sh", "tools/profile.sh",
+           "tools/summarize_profile.py", "tools/gpu_"}
+BUILT = {"oracle/_ref", "tools/mfma_fp4_layout_probe"}   # build outputs (git-ignored)
+
+
+def exists(p):
+    if p in RETIRED or p in BUILT:
+        return True
+    # profiles/README.md lists files relative to profiles/
+    for base in (ROOT, os.path.join(ROOT, PKG), os.path.join(ROOT, "profiles")):
+        full = os.path.join(base, p)
+        if os.path.exists(full):
+            return True
+        if p[-1] in "_-":                              # a family: `csrc/benor_w_`*.hip
+            d, stem = os.path.split(full)
+            if os.path.isdir(d) and any(f.startswith(stem) for f in os.listdir(d)):
+                return True
+    return False
+
+
+def test_retired_tools_are_gone_and_noted():
+    for p in RETIRED:
+        assert not os.path.exists(os.path.join(ROOT, p)), p
+    notes = open(os.path.join(ROOT, "profiles", "README.md"), encoding="utf-8").read()
+    assert "tools/gpu.sh" in notes and "replaced" in notes
+
+
+@pytest.mark.parametrize("doc", DOCS)
+def test_cited_paths_exist(doc):
+    missing = [p for p in cited_paths(doc) if not exists(p)]
+    assert not missing, f"{doc} cites paths that are not in the repo: {missing}"
