@@ -62,3 +62,12 @@ def test_retired_tools_are_gone_and_noted():
 def test_cited_paths_exist(doc):
     missing = [p for p in cited_paths(doc) if not exists(p)]
     assert not missing, f"{doc} cites paths that are not in the repo: {missing}"
+
+
+def test_profile_index_entries_exist():
+    """profiles/README.md names each session's files relative to profiles/."""
+    text = open(os.path.join(ROOT, "profiles", "README.md"), encoding="utf-8").read()
+    names = {m for m in re.findall(r"`(r0\d[^`\s]*)`", text) if not any(c in m for c in "*<>{}") and "-vN_" not in m}   # r01-vN_: a template
+    assert len(names) > 50
+    missing = sorted(n for n in names if not os.path.exists(os.path.join(ROOT, "profiles", n)))
+    assert not missing, f"profiles/README.md indexes files that are not in profiles/: {missing}"
