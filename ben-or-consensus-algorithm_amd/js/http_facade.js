@@ -15,7 +15,7 @@
 // node has received /start -- the point at which, in the reference, all live
 // nodes have broadcast their round-1 proposals.  Until then a started node
 // reports k = 1 (node.ts:172).  Messages POSTed from outside are acknowledged
-// and not simulated; as in the reference (node.ts:45,161), a killed node
+// and not simulated (why: DESIGN.md §2); as in the reference (node.ts:45,161), a killed node
 // never answers /message (the request stays open until the server closes).
 // The round loop runs once per network: the reference's round inboxes
 // (node.ts:29-30) outlive a run, so a later /start is acknowledged as the
