@@ -53,6 +53,15 @@ KERNEL_NAMES = {BO_KERNEL_NONE: "none", BO_KERNEL_BLOCKED: "blocked popcount", B
 BO_MAX_N = 4096
 BO_MAX_K = 1024
 
+# Environment knobs libbenor reads (csrc/benor_runtime.cpp kKnobs):
+# none is needed in production; each forces a choice the planner makes itself.
+# bench.py refuses to report while any is set.
+KNOBS = {
+    "BENOR_NO_MFMA": "validation", "BENOR_NO_MFMA_BIG": "validation", "BENOR_BIG_FORM": "validation",
+    "BENOR_COOP_BW": "validation", "BENOR_SMALL_MIN_TRIALS": "validation", "BENOR_BLOCKS_PER_CU": "tuning",
+    "BENOR_EVENT_LANES_PER_CU": "tuning", "BENOR_TEST_DEFER_SEG_CAP": "test", "BENOR_TIMELINE": "diagnostic",
+}
+
 BASE_NODE_PORT = 3000          # src/config.ts:1 (kept for the HTTP-shaped helpers)
 DEFAULT_K_MAX = 64             # round cap; the reference runs until /stop
 
@@ -298,22 +307,25 @@ def _net(N: int) -> Network:
 
 
 def startConsensus(N: int, seed: int | None = None, k_max: int = DEFAULT_K_MAX, stop_after=None,
-                   strict: bool = False, live: bool = False) -> None:
-    """src/nodes/consensus.ts:3-8: GET /start on every node, then the round
-    loop (node.ts:43-163) on the GPU until every live node decided or k_max.
-    stop_after: mid-run GET /stop schedule (Network.start).  live=True returns
-    once the kernel is launched (Network.start_live): stopConsensus / a node's
-    stop land in the running kernel, and getNodesState / getNodeState wait for
-    the run.  A second start on a network resolves as the reference's does
-    (every GET /start answers 200) but runs nothing: its inboxes persist
-    (node.ts:29-30), so no fresh consensus can follow; strict=True raises
-    Error instead."""
+                   strict: bool = False, live: bool | None = None, sync: bool = False) -> None:
+    """src/nodes/consensus.ts:3-8: GET /start on every node.  As the
+    reference's, it returns once the round loop (node.ts:43-163) is launched
+    on the GPU, before consensus finishes (Network.start_live): stopConsensus /
+    a node's stop land in the running kernel, and getNodesState / getNodeState
+    wait for the run.  sync=True returns after the run (every live node
+    decided, or k_max rounds; Network.start).  stop_after: a mid-run GET /stop
+    schedule given up front (Network.start; returns after the run).  A second
+    start on a network returns as the reference's does (every GET /start
+    answers 200) but runs nothing: its inboxes persist (node.ts:29-30), so no
+    fresh consensus can follow; strict=True raises instead."""
     if N == 0:
         return
     if live and stop_after:
         raise ValueError("stop_after and live are exclusive: a live run takes /stop as it comes")
+    if live and sync:
+        raise ValueError("live and sync are exclusive")
     try:
-        if live:
+        if not stop_after and not sync:
             _net(N).start_live(seed, k_max)
         else:
             _net(N).start(seed, k_max, stop_after)

@@ -84,6 +84,36 @@ __device__ __forceinline__ void philox4x32_10_multi(uint32_t k0, uint32_t k1, ui
   }
 }
 
+// Sequential word stream of Philox blocks (oracle orc_dstream): word i is
+// element i & 3 of block i >> 2 at counter {c0, c1, c2 | (i >> 2) << sh, c3}.
+// Random-delivery subsets (Floyd, stream 2, sh = 0) and the event level's
+// random /stop schedules (stream 4, sh = 12).
+struct DStream {
+  uint32_t k0, k1, c0, c1, c2, c3;
+  uint4 buf;
+  uint32_t widx;
+  uint32_t sh;           // block index position in c2: 0 (delivery stream), 12 (crash stream)
+  __device__ __forceinline__ uint32_t next() {
+    if ((widx & 3u) == 0u) buf = philox4x32_10(k0, k1, make_uint4(c0, c1, c2 | ((widx >> 2) << sh), c3));
+    const uint32_t j = widx & 3u;
+    ++widx;
+    return j == 0 ? buf.x : j == 1 ? buf.y : j == 2 ? buf.z : buf.w;
+  }
+  // uniform in [0, range): Lemire's multiply-shift with exact rejection
+  __device__ __forceinline__ uint32_t uniform(uint32_t range) {
+    uint64_t mm = (uint64_t)next() * range;
+    uint32_t l = (uint32_t)mm;
+    if (l < range) {
+      const uint32_t t = (0u - range) % range;
+      while (l < t) {
+        mm = (uint64_t)next() * range;
+        l = (uint32_t)mm;
+      }
+    }
+    return (uint32_t)(mm >> 32);
+  }
+};
+
 // One receiver's tally step: acc + popcount(word).  Opaque on purpose (see
 // the header comment): the per-receiver count must execute per receiver.
 __device__ __forceinline__ uint32_t tally(uint32_t word, uint32_t acc) {

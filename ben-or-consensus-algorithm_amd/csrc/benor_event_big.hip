@@ -88,6 +88,8 @@ struct BigState {
   uint64_t *comp;     // [4][64] completion of round k at k & 3
   uint32_t *picks;    // [2048] a batch's pick positions, low 16 bits as a bitmap
   uint32_t *wrote;    // [2048] the positions a batch wrote back, likewise
+  uint64_t *rstops;   // [ev_rstops] a random /stop schedule (event << 12 | node), ~0 once applied
+  uint64_t *rset;     // [64] its Floyd set over compact live indices
 };
 
 }  // namespace
@@ -111,6 +113,8 @@ __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
   S.xs = reinterpret_cast<int8_t *>(S.cidx + ((N + 3u) & ~3u));
   S.picks = reinterpret_cast<uint32_t *>(S.xs + ((N + 15u) & ~15u));
   S.wrote = S.picks + 2048;
+  S.rset = reinterpret_cast<uint64_t *>(S.wrote + 2048);
+  S.rstops = S.rset + 64;
   for (uint32_t i = lane; i < 2048u; i += 64u) S.picks[i] = 0u;
   const uint64_t allw = lane < NWd ? (N >= 64u * (lane + 1u) ? ~0ull : (1ull << (N - 64u * lane)) - 1ull) : 0ull;
   const uint64_t wmask = NWd >= 64u ? ~0ull : ((1ull << NWd) - 1ull);   // lanes holding a bitset word
@@ -171,8 +175,45 @@ __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
       const uint4 o = philox4x32_10<false>(k0, k1, make_uint4(tlo, thi, 0u, kStreamOrder << 24));
       rng = (((uint64_t)o.x << 32) | o.y) ^ 0xD1B54A32D192ED03ull;
     }
+    // ---- the /stop schedule: explicit (crash_at, sorted on the host, the same
+    // for every trial) or random per trial (crash_count, oracle event_trial):
+    // Floyd over compact live indices from Philox stream 4, then one uniform
+    // delivery count in [0, crash_window) per pick, in pick order.  next_key is
+    // the schedule's smallest unapplied (event << 12 | node), ~0 when none.
+    const uint32_t kr = p.ev_rstops;
+    if (kr) {
+      S.rset[lane] = 0ull;
+      __syncthreads();
+      if (lane == 0u) {
+        DStream ds;
+        ds.k0 = k0; ds.k1 = k1; ds.c0 = tlo; ds.c1 = thi; ds.c2 = 0u; ds.c3 = kStreamCrash << 24; ds.widx = 0;
+        ds.sh = 12u;
+        for (uint32_t j = m - kr, n = 0; j < m; ++j, ++n) {
+          const uint32_t tt = ds.uniform(j + 1u);
+          const uint32_t idx = ((S.rset[tt >> 6] >> (tt & 63u)) & 1ull) ? j : tt;
+          S.rset[idx >> 6] |= 1ull << (idx & 63u);
+          S.rstops[n] = idx;
+        }
+        for (uint32_t n = 0; n < kr; ++n) {
+          const uint32_t when = ds.uniform(p.crash_window);
+          S.rstops[n] = ((uint64_t)when << 12) | p.live_ids[(uint32_t)S.rstops[n]];
+        }
+      }
+      __syncthreads();
+    }
+    auto rstops_min = [&]() {                   // wave-uniform minimum of the random schedule
+      uint64_t v = ~0ull;
+      for (uint32_t i = lane; i < kr; i += 64u) v = v < S.rstops[i] ? v : S.rstops[i];
+      for (int off = 32; off >= 1; off >>= 1) {
+        const uint64_t o = __shfl_xor(v, off);
+        v = v < o ? v : o;
+      }
+      return v;
+    };
+    uint32_t next = 0;
+    uint64_t next_key = kr ? rstops_min() : (p.ev_nstops ? p.ev_stops[0] : ~0ull);
     __threadfence_block();
-    uint32_t next = 0, cur = 1, R = 0, halted = 0, seen = 0;
+    uint32_t cur = 1, R = 0, halted = 0, seen = 0;
     long long polled = wall_clock64() - (long long)kLivePollTicks;   // the first batch polls
     // the next batch's picks and pool words, loaded while this batch resolves
     // (valid when it starts at pf_e with pf_len messages and pf_b events)
@@ -192,15 +233,22 @@ __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
     while (!halted) {
       // ---- scheduled GET /stop (node.ts:191-194) before delivery e
       bool crashed = false;
-      while (next < p.ev_nstops && (p.ev_stops[next] >> 12) == e) {
-        const uint32_t i = (uint32_t)(p.ev_stops[next] & 4095u);
+      while ((next_key >> 12) == e) {
+        const uint32_t i = (uint32_t)(next_key & 4095u);
         if (lane == 0u) {
           S.killed[i >> 6] |= 1ull << (i & 63u);
           S.ibox[2u * i] |= kKilled;
           S.ibox[2u * i + 1u] |= kKilled;
         }
         crashed = true;
-        ++next;
+        if (kr) {
+          for (uint32_t j = lane; j < kr; j += 64u)
+            if (S.rstops[j] == next_key) S.rstops[j] = ~0ull;
+          next_key = rstops_min();
+        } else {
+          ++next;
+          next_key = next < p.ev_nstops ? p.ev_stops[next] : ~0ull;
+        }
       }
       // ---- live GET /stop requests (bo_consensus_start_live): every ~10 us the
       // wave reads the host-mapped mailbox; a new request lands before delivery e,
@@ -239,14 +287,14 @@ __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
       if (len == 0u) { halted = 3; break; }
       // ---- a batch of speculative events e .. e + B - 1
       uint64_t B = len < 64u ? len : 64u;
-      if (next < p.ev_nstops) {
-        const uint64_t until = (p.ev_stops[next] >> 12) - e;
+      if (next_key != ~0ull) {
+        const uint64_t until = (next_key >> 12) - e;
         if (until < B) B = until;
       }
       uint32_t pk = 0, pv = 0, tv = 0;
       // agent-scope loads are L2-served (no stale L1 line after the last batch's stores)
       auto load = [&](uint32_t i) { return __hip_atomic_load(&pool[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-      if (p.ev_fast && pf_e == e && pf_len == len && pf_b == B) {
+      if (pf_e == e && pf_len == len && pf_b == B) {
         // the previous batch ran to its end: its prefetch is this batch, except
         // for the words that batch wrote after they were read (S.wrote marks
         // them by their low 16 bits; a false match only reloads)
@@ -276,9 +324,9 @@ __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
       {
         const uint32_t len2 = len - (uint32_t)B;
         uint64_t B2 = len2 < 64u ? len2 : 64u;
-        bool ok = p.ev_fast && len2 > 0u;
-        if (next < p.ev_nstops) {
-          const uint64_t until2 = (p.ev_stops[next] >> 12) - (e + B);
+        bool ok = len2 > 0u;
+        if (next_key != ~0ull) {
+          const uint64_t until2 = (next_key >> 12) - (e + B);
           if (until2 == 0u) ok = false;
           else if (until2 < B2) B2 = until2;
         }
@@ -313,8 +361,8 @@ __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
       const uint32_t qi = pk, ti = len - 1u - lane;
       uint32_t a1 = 0u, b1 = 0u, nx = 64u;      // a + 1, b + 1 (0: none)
       uint32_t ovv = tv, mine = pv;             // moved_i, and the message event i delivers
-      bool maybe = !p.ev_fast;
-      if (p.ev_fast && lane < B) {
+      bool maybe = false;
+      if (lane < B) {
         const uint32_t kq = qi & 0xFFFFu, kt = ti & 0xFFFFu;
         const uint32_t old = atomicOr(&S.picks[kq >> 5], 1u << (kq & 31u));
         maybe = (old >> (kq & 31u)) & 1u;
@@ -337,7 +385,7 @@ __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
         const uint32_t via = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((a1 ? a1 - 1u : lane) << 2), (int)ovv);
         mine = a1 ? via : pv;
       }
-      if (p.ev_fast && lane < B) S.picks[(qi & 0xFFFFu) >> 5] = 0u;   // the bitmap is empty again for the next batch
+      if (lane < B) S.picks[(qi & 0xFFFFu) >> 5] = 0u;   // the bitmap is empty again for the next batch
       // ---- POST /message (node.ts:45-158), all B deliveries at once: each
       // adds {len, c0 | c1} to its receiver's inbox slot unless the receiver is
       // killed (node.ts:45) or the round is beyond the oracle's window.  When
@@ -395,10 +443,8 @@ __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
       // event overwrites its position or the position was popped
       if (lane < used && nx >= used && qi < len - used) {
         pool[qi] = ovv;
-        if (p.ev_fast) {
-          atomicOr(&S.wrote[(qi & 0xFFFFu) >> 5], 1u << (qi & 31u));   // for the next batch's prefetch
-          wq = qi;
-        }
+        atomicOr(&S.wrote[(qi & 0xFFFFu) >> 5], 1u << (qi & 31u));     // for the next batch's prefetch
+        wq = qi;
       }
       len -= used;
       rng += (uint64_t)used * kGamma;
@@ -485,7 +531,8 @@ __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
 
 uint32_t event_big_lds_bytes(const KParams &p) {
   const uint32_t N = p.N;
-  return p.hist_bytes + 16u * N + 8u * 64u * 6u + 2u * ((N + 3u) & ~3u) * 2u + ((N + 15u) & ~15u) + 2u * 2048u * 4u;
+  return p.hist_bytes + 16u * N + 8u * 64u * 6u + 2u * ((N + 3u) & ~3u) * 2u + ((N + 15u) & ~15u) + 2u * 2048u * 4u +
+         8u * 64u + 8u * p.ev_rstops;   // random /stop schedule: Floyd set, keys
 }
 
 hipError_t launch_event_big(const KParams &p, int grid, hipStream_t s) {

@@ -96,6 +96,9 @@ struct KParams {
   // as (event << 12 | node), ascending
   const uint64_t *ev_stops;
   uint32_t ev_nstops;
+  // event level, N > kMaxEventN: a random /stop schedule (crash_at NULL,
+  // crash_count > 0) drawn per trial on the device -- its length min(crash_count, m)
+  uint32_t ev_rstops;
   // live run (bo_consensus_start_live): the wave-per-trial event kernel at any
   // N, polling a host-mapped mailbox for GET /stop requests served while it
   // runs -- live_box[0] request sequence, [kLiveReq ..) requested-stop bits,
@@ -112,9 +115,6 @@ struct KParams {
   // diagnostics (BENOR_TIMELINE=<file>, packed matrix-core kernel): per wave,
   // kTimelineWords u64 -- wall-clock stamps of its phases and its batch counts
   unsigned long long *timeline;
-  // event level, big kernel: the collision bitmap and the next-batch prefetch
-  // (A/B knob BENOR_EVENT_FAST=0: every batch scans and loads its own words)
-  uint32_t ev_fast;
 };
 
 constexpr uint32_t kTimelineWords = 12;
@@ -130,6 +130,15 @@ static_assert(16u * kMfmaContRounds <= 64u, "deferral length words overflow thei
 
 constexpr uint64_t kDeferChunk = 1ull << 22;   // trials per matrix-core launch when trials can be deferred
 
+// Environment knobs (benor_runtime.cpp kKnobs: the only getenv in the library).
+// Each is documented in DESIGN.md §6 and mirrored by benor.KNOBS; none is
+// needed in production, every one of them only forces a choice the planner
+// makes by itself, for tests, tuning sweeps and diagnostics -- bench.py
+// refuses to report with any set.  knob() returns NULL when unset.
+const char *knob(const char *name);
+uint32_t knob_u32(const char *name, uint32_t dflt);
+bool knob_is(const char *name, const char *value);
+
 // Pick the tally block size G and fill nblocks / LDS sizes.
 void plan_geometry(KParams &p);
 
@@ -138,7 +147,6 @@ hipError_t launch_lockstep(const KParams &p, int grid_blocks, hipStream_t stream
 // Random delivery, Bernoulli + fix-up sampler (benor_random.hip, r04).
 uint32_t random_bern_rows(uint32_t m, uint32_t b);
 hipError_t launch_random_bern(const KParams &p, int grid_blocks, hipStream_t stream);
-bool random_bern_v1(const KParams &p);   // BENOR_RANDOM_V1=1: the r02 kernel (A/B knob)
 
 // Event level for kMaxEventN < N <= BO_MAX_N (benor_event_big.hip): one wave per trial.
 uint32_t event_big_lds_bytes(const KParams &p);

@@ -50,32 +50,6 @@ namespace benor {
 // out [word][lane] (any per-lane word index is bank-conflict free), then the
 // receiver's inbox is (sender plane AND delivery mask).  One receiver group
 // (64 receivers) at a time; this mode is bound by the subset's random draws.
-struct DStream {
-  uint32_t k0, k1, c0, c1, c2, c3;
-  uint4 buf;
-  uint32_t widx;
-  uint32_t sh;           // block index position in c2: 0 (delivery stream), 12 (crash stream)
-  __device__ __forceinline__ uint32_t next() {
-    if ((widx & 3u) == 0u) buf = philox4x32_10(k0, k1, make_uint4(c0, c1, c2 | ((widx >> 2) << sh), c3));
-    const uint32_t j = widx & 3u;
-    ++widx;
-    return j == 0 ? buf.x : j == 1 ? buf.y : j == 2 ? buf.z : buf.w;
-  }
-  // uniform in [0, range): Lemire's multiply-shift with exact rejection
-  __device__ __forceinline__ uint32_t uniform(uint32_t range) {
-    uint64_t mm = (uint64_t)next() * range;
-    uint32_t l = (uint32_t)mm;
-    if (l < range) {
-      const uint32_t t = (0u - range) % range;
-      while (l < t) {
-        mm = (uint64_t)next() * range;
-        l = (uint32_t)mm;
-      }
-    }
-    return (uint32_t)(mm >> 32);
-  }
-};
-
 // One Floyd step: sender t, else (t already in the subset) sender jj, joins
 // the lane's bitset ([word][lane] in LDS, `lb` = this lane's byte offset).
 // ds_or: LDS ops of a wave retire in order, so the next step's read sees this
@@ -98,140 +72,14 @@ __device__ __forceinline__ void floyd_insert(uint32_t lbase, uint32_t t, uint32_
   __hip_atomic_fetch_or(bitset_word(idx, lbase), 1u << (idx & 31u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 
-// Sampler (b) of oracle_delivery_mask: Bernoulli(a/16) mask, then exact
-// fix-up flips at uniform sender indices until the mask holds q senders.  The
-// mask words and the fix-up fields are taken in stream order; every lane runs
-// the same (wave-uniform) stream schedule, so Philox blocks are drawn once per
-// 4 words for the whole wave.  Writes the lane's mask into B ([word][lane]).
-//
-// The fix-up definition is sequential (each field sees the flips before it),
-// but a field's test depends on an earlier field only when both name the same
-// sender: the repeat then sees the bit already flipped (or still unwanted) and
-// is refused either way.  So fields go 4 at a time: the 4 mask words are read
-// back to back (one LDS round trip instead of 4), each field is tested against
-// them and refused when an earlier field of the batch named the same sender,
-// and the flips go out as ds_xor (LDS ops of a wave apply in issue order; a
-// refused field xors 0).  PER = floor(32/b) fields per stream word (b = 7..12).
-template <int PER, bool POW2>
-__device__ __forceinline__ void bernoulli_fixup(uint32_t *__restrict__ B, uint32_t m, uint32_t b, uint32_t rm,
-                                                uint32_t need, uint32_t blk0, uint32_t k0, uint32_t k1,
-                                                uint32_t tlo, uint32_t thi, uint32_t c2, uint32_t c3) {
-  constexpr int NF = 4 * PER;                        // fields per Philox block
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t lb = (uint32_t)(uintptr_t)(lds_u32 *)B + lane * 4u;   // LDS address of this lane's word 0
-  for (uint32_t blk = blk0;; ++blk) {
-    if (!__any(need != 0u)) break;
-    const uint4 bb = philox4x32_10(k0, k1, make_uint4(tlo, thi, c2 | blk, c3));
-    const uint32_t u4[4] = {bb.x, bb.y, bb.z, bb.w};
-#pragma unroll
-    for (int g = 0; g < NF; g += 4) {
-      uint32_t fb[4], cur[4];
-      lds_u32 *wp[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int f = g + j;                         // field f: word f / PER, bits (f % PER) * b
-        fb[j] = __builtin_amdgcn_ubfe(u4[f / PER], (uint32_t)(f % PER) * b, b);
-        // an index >= m (never when m = 2^b) reads word 0 and is refused below
-        wp[j] = bitset_word(POW2 ? fb[j] : (fb[j] < m ? fb[j] : 0u), lb);
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) cur[j] = *wp[j];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        bool ok = need != 0u && (POW2 || fb[j] < m) && __builtin_amdgcn_ubfe(cur[j], fb[j], 1u) == rm;
-#pragma unroll
-        for (int k = 0; k < j; ++k) ok = ok && fb[k] != fb[j];
-        if (ok) {
-          __hip_atomic_fetch_xor(wp[j], 1u << (fb[j] & 31u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-          --need;
-        }
-      }
-    }
-  }
-}
-
-// Mask generation for p = A/16, unrolled at compile time: NW = 4 - tz(A)
-// stream words per mask word, L = lcm(NW, 4) stream words (L/4 Philox blocks)
-// per super-block, bit = (u < A) combined from bit tz(A) up.
-template <int A>
-__device__ __forceinline__ uint32_t bernoulli_words(uint32_t *__restrict__ B, uint32_t m, uint32_t k0,
-                                                    uint32_t k1, uint32_t tlo, uint32_t thi, uint32_t c2,
-                                                    uint32_t c3, uint32_t &blocks) {
-  constexpr int TZ = __builtin_ctz(A), NW = 4 - TZ;
-  constexpr int L = NW == 3 ? 12 : 4, NB = L / 4, MW = L / NW;   // words, blocks, mask words per super-block
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t W32 = (m + 31u) >> 5;
-  uint32_t c = 0;
-  uint32_t blk = 0;
-  for (uint32_t w0 = 0; w0 < W32; w0 += MW) {
-    uint32_t u[L];
-#pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      if (j == 0 || w0 + (uint32_t)((4 * j) / NW) < W32) {    // blocks a partial super-block needs
-        const uint4 bb = philox4x32_10(k0, k1, make_uint4(tlo, thi, c2 | (blk + j), c3));
-        u[4 * j] = bb.x, u[4 * j + 1] = bb.y, u[4 * j + 2] = bb.z, u[4 * j + 3] = bb.w;
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < MW; ++t) {
-      const uint32_t w = w0 + (uint32_t)t;
-      if (w < W32) {
-        uint32_t r = ~u[t * NW];
-#pragma unroll
-        for (int i = TZ + 1; i < 4; ++i) r = ((A >> i) & 1) ? (~u[t * NW + i - TZ] | r) : (~u[t * NW + i - TZ] & r);
-        const uint32_t n = m - 32u * w;
-        if (n < 32u) r &= (1u << n) - 1u;
-        B[w * 64u + lane] = r;
-        c += (uint32_t)__builtin_popcount(r);
-      }
-    }
-    blk += NB;
-  }
-  blocks = (W32 * NW + 3u) >> 2;                     // blocks the mask used (the fix-up starts after them)
-  return c;
-}
-
-template <int... As>
-__device__ __forceinline__ uint32_t bernoulli_words_any(uint32_t a, uint32_t *__restrict__ B, uint32_t m,
-                                                        uint32_t k0, uint32_t k1, uint32_t tlo, uint32_t thi,
-                                                        uint32_t c2, uint32_t c3, uint32_t &blocks,
-                                                        std::integer_sequence<int, As...>) {
-  uint32_t c = 0;
-  (void)((a == (uint32_t)(As + 1) ? (c = bernoulli_words<As + 1>(B, m, k0, k1, tlo, thi, c2, c3, blocks), true)
-                                  : false) || ...);
-  return c;
-}
-
-__device__ __forceinline__ void bernoulli_mask(uint32_t *__restrict__ B, uint32_t m, uint32_t q, bool active,
-                                               uint32_t a, uint32_t b, uint32_t k0, uint32_t k1, uint32_t tlo,
-                                               uint32_t thi, uint32_t c2, uint32_t c3) {
-  uint32_t blk0 = 0;                                 // the fix-up starts at a fresh Philox block
-  const uint32_t c = bernoulli_words_any(a, B, m, k0, k1, tlo, thi, c2, c3, blk0, std::make_integer_sequence<int, 15>{});
-  const uint32_t rm = c > q ? 1u : 0u;               // 1: clear members, 0: set non-members
-  const uint32_t need = active ? (rm ? c - q : q - c) : 0u;
-  const bool pow2 = (1u << b) == m;
-  if (b <= 8u) {
-    if (pow2) bernoulli_fixup<4, true>(B, m, b, rm, need, blk0, k0, k1, tlo, thi, c2, c3);
-    else bernoulli_fixup<4, false>(B, m, b, rm, need, blk0, k0, k1, tlo, thi, c2, c3);
-  } else if (b <= 10u) {
-    if (pow2) bernoulli_fixup<3, true>(B, m, b, rm, need, blk0, k0, k1, tlo, thi, c2, c3);
-    else bernoulli_fixup<3, false>(B, m, b, rm, need, blk0, k0, k1, tlo, thi, c2, c3);
-  } else {
-    if (pow2) bernoulli_fixup<2, true>(B, m, b, rm, need, blk0, k0, k1, tlo, thi, c2, c3);
-    else bernoulli_fixup<2, false>(B, m, b, rm, need, blk0, k0, k1, tlo, thi, c2, c3);
-  }
-}
-
 __device__ __forceinline__ void random_tally(const uint4 *__restrict__ plane, uint32_t *__restrict__ B,
                                              uint32_t W, uint32_t m, uint32_t q, bool active, uint32_t k0,
                                              uint32_t k1, uint32_t tlo, uint32_t thi, uint32_t node, uint32_t r,
-                                             uint32_t phase, uint32_t rd_a, uint32_t rd_b, uint32_t &c0,
-                                             uint32_t &c1) {
+                                             uint32_t phase, uint32_t &c0, uint32_t &c1) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t e = m - q;
-  const bool bern = rd_a != 0u;
-  const bool deliver_T = bern || q <= e;
-  const uint32_t k = bern ? 0u : (deliver_T ? q : e);
+  const bool deliver_T = q <= e;
+  const uint32_t k = deliver_T ? q : e;
   // Floyd over [0, m): for jj = m-k .. m-1, t = uniform(jj + 1) (Lemire, exact).
   // Words come from Philox stream 2 in order (DStream above: word i is element
   // i & 3 of block i >> 2).  Fast path: one block = 4 draws, taken while the
@@ -240,7 +88,6 @@ __device__ __forceinline__ void random_tally(const uint4 *__restrict__ plane, ui
   // words, same result -- the oracle's definition).
   // delivery counter {tlo, thi, block | round << 16 | phase << 31, node | 2 << 24} (oracle_delivery_mask)
   const uint32_t c2 = ((r & 0x7FFFu) << 16) | ((phase & 1u) << 31), c3 = (node & 0xFFFu) | (kStreamDelivery << 24);
-  if (bern) bernoulli_mask(B, m, q, active, rd_a, rd_b, k0, k1, tlo, thi, c2, c3);
   const uint32_t lb = (uint32_t)(uintptr_t)(lds_u32 *)B + lane * 4u;   // LDS address of this lane's word 0
   uint32_t jj = m - k, widx = 0;
   for (;;) {
@@ -351,7 +198,7 @@ __global__ void __launch_bounds__(256) benor_random_kernel(KParams p) {
         const bool active = c < m;
         const uint32_t node = active ? p.live_ids[c] : 0u;
         uint32_t a0, a1;
-        random_tally(X, B, W, m, q, active, k0, k1, tlo, thi, node, r, 0u, p.rd_a, p.rd_b, a0, a1);
+        random_tally(X, B, W, m, q, active, k0, k1, tlo, thi, node, r, 0u, a0, a1);
         const uint64_t vm = group_mask(j, m);
         const uint64_t p0 = ballot(a0 > a1) & vm;
         const uint64_t p1 = ballot(a1 > a0) & vm;
@@ -363,7 +210,7 @@ __global__ void __launch_bounds__(256) benor_random_kernel(KParams p) {
         const bool active = c < m;
         const uint32_t node = active ? p.live_ids[c] : 0u;
         uint32_t a0, a1;
-        random_tally(P, B, W, m, q, active, k0, k1, tlo, thi, node, r, 1u, p.rd_a, p.rd_b, a0, a1);
+        random_tally(P, B, W, m, q, active, k0, k1, tlo, thi, node, r, 1u, a0, a1);
         const uint64_t vm = group_mask(j, m);
         const bool d0l = a0 > F, d1l = a1 > F;
         const uint64_t d0 = ballot(d0l) & vm;
@@ -689,6 +536,7 @@ __global__ void __launch_bounds__(256) benor_event_kernel(KParams p) {
     atomicAdd(&lhist[halted == 1 ? (R * 3u + v) : v], 1u);
     if (halted == 1 && v == 2u) atomicAdd(&lhist[p.hist_len - 1u], 1u);
     if (overflow && p.rounds_out) atomicOr(p.rounds_out, 0x80000000u);
+    if (overflow && p.overflow) atomicOr(p.overflow, 2u);   // bo_plan_check: the pool filled up
     if (p.node_out) {
       for (uint32_t i = 0; i < N; ++i) {
         const bool f = (p.faulty_mask[i >> 6] >> (i & 63u)) & 1ull;
@@ -739,10 +587,6 @@ void plan_geometry(KParams &p) {
     p.nblocks = 1;
     p.variant = 5;
     p.wave_bytes = 0;
-    {
-      const char *fast = getenv("BENOR_EVENT_FAST");
-      p.ev_fast = fast && fast[0] == '0' ? 0u : 1u;
-    }
     p.ev_cap = 4u * p.N * p.N + 64u;
     p.ev_stride = p.ev_cap;                          // u32 messages
     p.lds_bytes = event_big_lds_bytes(p);
@@ -778,8 +622,8 @@ void plan_geometry(KParams &p) {
       while ((1u << b) < p.m) ++b;
       p.rd_b = b;
     }
-    p.wave_bytes = 2u * W * 16u + 2u * W * 64u * 4u;   // X, P records + per-lane bitset
-    if (p.rd_a && !random_bern_v1(p)) {               // benor_random.hip: padded bitset rows
+    p.wave_bytes = 2u * W * 16u + 2u * W * 64u * 4u;   // X, P records + per-lane bitset (Floyd)
+    if (p.rd_a) {                                     // Bernoulli sampler (benor_random.hip): padded bitset rows
       p.rd_rows = random_bern_rows(p.m, p.rd_b);
       p.wave_bytes = 2u * W * 16u + p.rd_rows * 64u * 4u;
     }
@@ -798,8 +642,7 @@ void plan_geometry(KParams &p) {
     // trial can decide (m > F) and no "?" initial value (every vote count is
     // m).  The lane kernel planned above serves the state launches (network
     // API); the packed kernel re-runs its rare leftovers itself.
-    const char *no_mfma = getenv("BENOR_NO_MFMA");
-    if (p.m >= 2u && p.m <= kMaxSmallMfmaM && p.m > p.F && p.init_q == 0u && !(no_mfma && no_mfma[0] == '1')) {
+    if (p.m >= 2u && p.m <= kMaxSmallMfmaM && p.m > p.F && p.init_q == 0u && !knob_is("BENOR_NO_MFMA", "1")) {
       p.base_variant = p.variant;
       p.base_G = p.G;
       p.variant = 8;
@@ -845,10 +688,8 @@ void plan_geometry(KParams &p) {
   // LDS plan stays.
   const bool sure = (p.m & 1u) && !(p.init_q & 1u) && p.m > 2u * p.F;
   const bool can_halt = p.m > p.F && !(p.init_mode == BO_INIT_FIXED && p.init_tie);
-  const char *no_mfma = getenv("BENOR_NO_MFMA");
-  const char *no_big = getenv("BENOR_NO_MFMA_BIG");
-  const bool big_ok = !(no_big && no_big[0] == '1');
-  if (can_halt && (p.m <= kMaxMfmaM || big_ok) && !(no_mfma && no_mfma[0] == '1')) {
+  const bool big_ok = !knob_is("BENOR_NO_MFMA_BIG", "1");
+  if (can_halt && (p.m <= kMaxMfmaM || big_ok) && !knob_is("BENOR_NO_MFMA", "1")) {
     p.base_variant = p.variant;
     p.base_G = p.G;
     p.variant = 7;
@@ -920,8 +761,8 @@ hipError_t launch_lockstep(const KParams &p, int grid, hipStream_t s) {
     q.lds_bytes = q.hist_bytes + kWavesPerBlock * q.wave_bytes;
     return launch_lockstep(q, grid, s);
   }
-  if (p.variant == 2 && p.rd_a && p.rd_rows) return launch_random_bern(p, grid, s);
-  if (p.variant == 2) {
+  if (p.variant == 2 && p.rd_a) return launch_random_bern(p, grid, s);
+  if (p.variant == 2) {                      // Floyd sampler
     if (p.lds_bytes > 64u * 1024u) {
       hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&benor_random_kernel),
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds_bytes);
@@ -957,26 +798,14 @@ uint64_t defer_units(const KParams &p, int grid) {
   return mfma_big_coop(p) ? (uint64_t)grid : (uint64_t)grid * block_waves(p);
 }
 
-bool random_bern_v1(const KParams &p) {
-  (void)p;
-  const char *ev = getenv("BENOR_RANDOM_V1");
-  return ev && ev[0] == '1';
-}
-
 // A packed-shape launch runs on the lane kernel when it writes per-node
 // state (network API) or is short: below ~10^6 trials the packed kernel's
 // partial round lists at the end of each wave outweigh its per-trial gain
 // (DESIGN §4.2).
-// BENOR_SMALL_MIN_TRIALS overrides the crossover.
+// BENOR_SMALL_MIN_TRIALS overrides the crossover (validation knob).
 bool small_on_lane(const KParams &p) {
   if (p.node_out || p.rounds_out) return true;
-  if (const char *ev = getenv("BENOR_SMALL_FORM")) {   // A/B knob: packed / lane
-    if (strcmp(ev, "lane") == 0) return true;
-    if (strcmp(ev, "packed") == 0) return false;
-  }
-  uint64_t min_trials = kSmallMinTrials;
-  if (const char *ev = getenv("BENOR_SMALL_MIN_TRIALS")) min_trials = strtoull(ev, nullptr, 10);
-  return p.trial_count < min_trials;
+  return p.trial_count < knob_u32("BENOR_SMALL_MIN_TRIALS", (uint32_t)kSmallMinTrials);
 }
 
 int lockstep_grid(const KParams &p, int device) {
@@ -1010,8 +839,8 @@ int lockstep_grid(const KParams &p, int device) {
     if (cap > 4u) cap = 4u;
     if (per_cu > cap) per_cu = cap;
     if (per_cu < 1u) per_cu = 1u;
-    if (const char *ev = getenv("BENOR_BLOCKS_PER_CU")) {   // tuning knob
-      const uint64_t v = strtoull(ev, nullptr, 10);
+    {                                        // tuning knob
+      const uint64_t v = knob_u32("BENOR_BLOCKS_PER_CU", 0u);
       if (v >= 1u && v <= lds_groups_per_cu(p.lds_bytes)) per_cu = v;
     }
     uint64_t grid = (uint64_t)cus * per_cu;
@@ -1053,8 +882,8 @@ int lockstep_grid(const KParams &p, int device) {
     const uint64_t v = want < 2u ? 2u : want;
     if (v < per_cu) per_cu = v;
   }
-  if (const char *ev = getenv("BENOR_BLOCKS_PER_CU")) {   // tuning knob (tools/lane_grid_sweep.py)
-    const uint64_t v = strtoull(ev, nullptr, 10);
+  {                                          // tuning knob (tools/lane_grid_sweep.py)
+    const uint64_t v = knob_u32("BENOR_BLOCKS_PER_CU", 0u);
     if (v >= 1u && v < per_cu) per_cu = v;
   }
   uint64_t grid = (uint64_t)cus * per_cu;

@@ -389,13 +389,11 @@ static hipError_t launch_big_nt(const KParams &p, int grid, hipStream_t s) {
 // per-wave form's long group tail), 10^6 x1.17; N=4096 F=1365 (W=43) x1.06-1.10;
 // N=3000 F=1400 (W=25) x1.06; N=2048 F=682 (W=22) x1.09; N=1500 F=200 (W=21)
 // x1.01; N=2049 F=1024 (W=17, KIND 2) x0.93.  BENOR_BIG_FORM=wave / coop
-// overrides the choice.
+// forces one (validation knob: tests run both forms at every W).
 bool mfma_big_coop(const KParams &p) {
   if (p.variant != 7 || p.W <= 16u || p.node_out || p.rounds_out) return false;
-  if (const char *ev = getenv("BENOR_BIG_FORM")) {
-    if (strcmp(ev, "wave") == 0) return false;
-    if (strcmp(ev, "coop") == 0) return true;
-  }
+  if (knob_is("BENOR_BIG_FORM", "wave")) return false;
+  if (knob_is("BENOR_BIG_FORM", "coop")) return true;
   return p.W >= kCoopMinW;
 }
 

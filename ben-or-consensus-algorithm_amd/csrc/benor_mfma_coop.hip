@@ -32,7 +32,6 @@
 // blockIdx.x * defer_seg_cap), appended to the compact list by wave 0.
 #include "benor_mfma_big.h"
 
-#include <cstdlib>
 #include <type_traits>
 
 namespace benor {
@@ -44,13 +43,14 @@ namespace benor {
 __device__ __forceinline__ mf_v4i as_votes(uint32_t w) { return expand_votes(w); }
 __device__ __forceinline__ mf_v4i as_votes(mf_v4i v) { return v; }
 
-// CB: each tile's first product takes the phase's bias as its C operand (no
+// Each tile's first product takes the phase's bias as its C operand (no
 // accumulator zeroing, no bias add per result) -- in the P-phase for blocks
-// without the last tile, whose dead rows need NaN.
-// PF: the next group's /start words are written right after this group's
-// P-phase products (X is free once the R-phase barrier has passed), so the
-// P-phase barrier also publishes them and a group needs two barriers, not three.
-template <int KIND, int NT, int BW, bool CB, bool EXP, bool PF>
+// without the last tile, whose dead rows need NaN (r03: +2-4 % against zeroed
+// accumulators; profiles/r03-s3k_coop_exp_inproc.jsonl).
+// The next group's /start words are written right after this group's P-phase
+// products (X is free once the R-phase barrier has passed), so the P-phase
+// barrier also publishes them and a group needs two barriers, not three.
+template <int KIND, int NT, int BW, bool EXP>
 __global__ void __launch_bounds__(64 * BW) benor_mfma_coop_kernel(KParams p) {
   using XW = std::conditional_t<EXP, mf_v4i, uint32_t>;
   constexpr uint32_t XS = EXP ? 4u : 1u;      // dwords per plane word
@@ -144,18 +144,12 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_coop_kernel(KParams p) {
       }
     }
   };
-  if constexpr (PF) {
-    if (blockIdx.x < ngroups) start_x(blockIdx.x);
-    __syncthreads();
-  }
+  if (blockIdx.x < ngroups) start_x(blockIdx.x);
+  __syncthreads();
   for (uint32_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
     const uint32_t t = (g << 5) + (lane & 31u);
     const bool valid = t < trial_count;
     const uint32_t toff = cont ? (valid ? p.trial_list[t] : 0u) : t;   // the trial's offset in the launch
-    if constexpr (!PF) {
-      start_x(g);
-      __syncthreads();
-    }
 
     // ---- R-phase: this wave's tile blocks; proposals to LDS as sign bits
     // (1 = proposal 0), packed as in benor_mfma_big.hip
@@ -164,8 +158,7 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_coop_kernel(KParams p) {
       const uint32_t i = b * (uint32_t)NT;
       mf_v16f acc[NT];
       XW wcur = XR[lane];                      // chunk c + 1's word read among chunk c's products
-      uint32_t c0 = 0;
-      if constexpr (CB) {                      // chunk 0 with C = the bias (W >= 17)
+      {                                        // chunk 0 with C = the bias (W >= 17)
         const XW wnext = XR[64u + lane];
         const mf_v4i bx = as_votes(wcur);
 #pragma unroll
@@ -174,12 +167,8 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_coop_kernel(KParams p) {
           acc[u] = mfma_count<4>(ones, bx, cb_r);
         }
         wcur = wnext;
-        c0 = 1;
-      } else {
-#pragma unroll
-        for (int u = 0; u < NT; ++u) acc[u] = mf_v16f{};
       }
-      for (uint32_t c = c0; c < W; ++c) {
+      for (uint32_t c = 1; c < W; ++c) {
         const XW wnext = XR[(c + 1u < W ? c + 1u : c) * 64u + lane];
         const mf_v4i bx = as_votes(wcur);
 #pragma unroll
@@ -191,12 +180,6 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_coop_kernel(KParams p) {
 #pragma unroll
         for (int k = 0; k < NT; ++k) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
         wcur = wnext;
-      }
-      if constexpr (!CB) {
-#pragma unroll
-        for (int u = 0; u < NT; ++u)
-#pragma unroll
-          for (int j = 0; j < 16; ++j) acc[u][j] += bias_r;
       }
 #pragma unroll
       for (int q = 0; q < NT / 2; ++q) {      // tile pair (i + 2q, i + 2q + 1) -> proposal word (i >> 1) + q
@@ -223,7 +206,7 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_coop_kernel(KParams p) {
     for (uint32_t b = wv; b < NB; b += BW) {
       const uint32_t i = b * (uint32_t)NT;
       const float nanf = __builtin_nanf("");
-      const bool cbb = CB && i + (uint32_t)NT < MT;   // every tile of the block has 32 live rows
+      const bool cbb = i + (uint32_t)NT < MT;   // every tile of the block has 32 live rows
       mf_v16f acc[NT];
       XW wcur = PR[lane];
       uint32_t k0 = 0;
@@ -277,9 +260,7 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_coop_kernel(KParams p) {
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    if constexpr (PF) {
-      if (g + gridDim.x < ngroups) start_x(g + gridDim.x);
-    }
+    if (g + gridDim.x < ngroups) start_x(g + gridDim.x);
     // this wave's columns: some receiver decided 1 / 0 (KIND 0, 1, 2: acc < 0
     // <=> decided 1), a "?" proposal or an undecided receiver (defer)
     {
@@ -345,14 +326,8 @@ __global__ void __launch_bounds__(64 * BW) benor_mfma_coop_kernel(KParams p) {
   flush_hist(lhist, p);
 }
 
-// Receiver tiles per block: big_nt(W) (BENOR_COOP_NT=4 / 8 overrides).
-static uint32_t coop_nt(const KParams &p) {
-  if (const char *ev = getenv("BENOR_COOP_NT")) {
-    const int v = atoi(ev);
-    if (v == 4 || v == 8) return (uint32_t)v;
-  }
-  return big_nt(p.W);
-}
+// Receiver tiles per block: big_nt(W).
+static uint32_t coop_nt(const KParams &p) { return big_nt(p.W); }
 
 static uint32_t coop_lds_bytes(const KParams &p, bool exp) {
   const uint32_t NT = coop_nt(p);
@@ -363,36 +338,26 @@ static uint32_t coop_lds_bytes(const KParams &p, bool exp) {
 // serves only four products: x1.04 at N=1600 F=100, N=1700 F=300 and N=2048
 // F=682; eight-tile blocks (W >= 28) measured within -2..+1 % either way, so
 // they keep the packed words (profiles/r03-s3k_coop_exp_inproc.jsonl).
-// BENOR_COOP_EXP=0 / 1 overrides (1: whenever the planes fit one
-// workgroup's LDS, W = 64: 132 KB).
-static bool coop_exp(const KParams &p) {
-  const bool fits = coop_lds_bytes(p, true) <= 160u * 1024u;
-  if (const char *ev = getenv("BENOR_COOP_EXP")) {
-    if (ev[0] == '0') return false;
-    if (ev[0] == '1') return fits;
-  }
-  return fits && coop_nt(p) == 4u;
-}
+static bool coop_exp(const KParams &p) { return coop_lds_bytes(p, true) <= 160u * 1024u && coop_nt(p) == 4u; }
 
 uint32_t mfma_coop_lds_bytes(const KParams &p) { return coop_lds_bytes(p, coop_exp(p)); }
 
 // Waves per workgroup: 8 with eight-tile blocks (W >= 28: N=4096 F=1365 x1.04
 // over 4 waves, F=0 equal), else 4 (W = 22..27: 8 waves x0.85-0.86, their
 // four-tile blocks leave more registers and the CU takes more groups).
-// BENOR_COOP_BW=4 / 8 overrides.
+// BENOR_COOP_BW=4 / 8 forces one (validation knob: tests run both forms at
+// every W, knob_value in benor_runtime.cpp).
 uint32_t mfma_coop_block_waves(const KParams &p) {
-  if (const char *ev = getenv("BENOR_COOP_BW")) {
-    const int v = atoi(ev);
-    if (v == 4 || v == 8) return (uint32_t)v;
-  }
+  const uint32_t v = knob_u32("BENOR_COOP_BW", 0u);
+  if (v == 4u || v == 8u) return v;
   return big_nt(p.W) == 8u ? 8u : 4u;
 }
 
 template <int KIND, int NT, int BW>
 static int coop_occupancy(const KParams &p) {
   int n = 0;
-  const void *fn = coop_exp(p) ? reinterpret_cast<const void *>(&benor_mfma_coop_kernel<KIND, NT, BW, true, true, true>)
-                               : reinterpret_cast<const void *>(&benor_mfma_coop_kernel<KIND, NT, BW, true, false, true>);
+  const void *fn = coop_exp(p) ? reinterpret_cast<const void *>(&benor_mfma_coop_kernel<KIND, NT, BW, true>)
+                               : reinterpret_cast<const void *>(&benor_mfma_coop_kernel<KIND, NT, BW, false>);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, 64 * BW, mfma_coop_lds_bytes(p)) != hipSuccess)
     n = 1;
   const int lds_fit = (int)lds_groups_per_cu(mfma_coop_lds_bytes(p));
@@ -411,31 +376,21 @@ int mfma_coop_blocks_per_cu(const KParams &p) {
   return k == 0 ? coop_occupancy<0, 4, 4>(p) : k == 1 ? coop_occupancy<1, 4, 4>(p) : coop_occupancy<2, 4, 4>(p);
 }
 
-template <int KIND, int NT, int BW, bool CB, bool EXP, bool PF>
-static hipError_t launch_coop_cb(const KParams &p, int grid, hipStream_t s) {
+template <int KIND, int NT, int BW, bool EXP>
+static hipError_t launch_coop_exp(const KParams &p, int grid, hipStream_t s) {
   const uint32_t lds = coop_lds_bytes(p, EXP);
   if (lds > 64u * 1024u) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&benor_mfma_coop_kernel<KIND, NT, BW, CB, EXP, PF>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&benor_mfma_coop_kernel<KIND, NT, BW, EXP>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((benor_mfma_coop_kernel<KIND, NT, BW, CB, EXP, PF>), dim3(grid), dim3(64 * BW), lds, s, p);
+  hipLaunchKernelGGL((benor_mfma_coop_kernel<KIND, NT, BW, EXP>), dim3(grid), dim3(64 * BW), lds, s, p);
   return hipGetLastError();
 }
 
-// BENOR_COOP_CBIAS=0: accumulators zeroed and the bias added per result (A/B).
 template <int KIND, int NT, int BW>
 static hipError_t launch_coop(const KParams &p, int grid, hipStream_t s) {
-  const char *ev = getenv("BENOR_COOP_CBIAS");
-  const bool cb = !(ev && ev[0] == '0');
-  const char *pv = getenv("BENOR_COOP_PF");        // BENOR_COOP_PF=0: three barriers per group (A/B)
-  const bool pf = !(pv && pv[0] == '0');
-  if (!cb) return coop_exp(p) ? launch_coop_cb<KIND, NT, BW, false, true, false>(p, grid, s)
-                              : launch_coop_cb<KIND, NT, BW, false, false, false>(p, grid, s);
-  if (coop_exp(p)) return pf ? launch_coop_cb<KIND, NT, BW, true, true, true>(p, grid, s)
-                             : launch_coop_cb<KIND, NT, BW, true, true, false>(p, grid, s);
-  return pf ? launch_coop_cb<KIND, NT, BW, true, false, true>(p, grid, s)
-            : launch_coop_cb<KIND, NT, BW, true, false, false>(p, grid, s);
+  return coop_exp(p) ? launch_coop_exp<KIND, NT, BW, true>(p, grid, s) : launch_coop_exp<KIND, NT, BW, false>(p, grid, s);
 }
 
 template <int KIND, int NT>

@@ -434,7 +434,8 @@ hipError_t launch_nw_b(const KParams &p, int grid, hipStream_t s) {
 
 template <int NW>
 hipError_t launch_nw(const KParams &p, int grid, hipStream_t s) {
-  switch (p.rd_b) {   // m in (128, 4096]: b = ceil(log2 m) in 8..12
+  switch (p.rd_b) {   // m in [128, 4096]: b = ceil(log2 m) in 7..12 (b = 7 only at m = 128, q = 64)
+    case 7: return launch_nw_b<NW, 7>(p, grid, s);
     case 8: return launch_nw_b<NW, 8>(p, grid, s);
     case 9: return launch_nw_b<NW, 9>(p, grid, s);
     case 10: return launch_nw_b<NW, 10>(p, grid, s);
@@ -451,7 +452,7 @@ uint32_t random_bern_rows(uint32_t m, uint32_t b) {
 }
 
 hipError_t launch_random_bern(const KParams &p, int grid, hipStream_t s) {
-  if (p.rd_a == 0u || p.rd_b < 8u || p.rd_b > 12u || p.rd_rows < random_bern_rows(p.m, p.rd_b))
+  if (p.rd_a == 0u || p.rd_b < 7u || p.rd_b > 12u || p.rd_rows < random_bern_rows(p.m, p.rd_b))
     return hipErrorInvalidValue;
   const uint32_t tz = (uint32_t)__builtin_ctz(p.rd_a);
   switch (4u - tz) {

@@ -62,6 +62,47 @@ __global__ void add_bin_kernel(unsigned long long *hist, uint32_t bin, unsigned 
 
 }  // namespace
 
+namespace benor {
+// Every environment knob the library reads.  Production needs none: each
+// forces a choice the planner makes by itself (DESIGN.md §6 "knobs").
+//   validation: run another product kernel or form on the same trials, so
+//     tests can check each against the others and the oracle;
+//   tuning: grid shape only (every test checks that the histogram does not
+//     depend on it);
+//   test: provoke an error path;  diagnostic: instrumented launches.
+struct KnobSpec {
+  const char *name, *kind;
+};
+constexpr KnobSpec kKnobs[] = {
+    {"BENOR_NO_MFMA", "validation"},            // "1": popcount kernels instead of the matrix-core ones
+    {"BENOR_NO_MFMA_BIG", "validation"},        // "1": popcount kernels for m > 1024
+    {"BENOR_BIG_FORM", "validation"},           // "wave" / "coop": big-network matrix-core form
+    {"BENOR_COOP_BW", "validation"},            // 4 / 8: waves per cooperative workgroup
+    {"BENOR_SMALL_MIN_TRIALS", "validation"},   // packed matrix-core kernel from this launch size
+    {"BENOR_BLOCKS_PER_CU", "tuning"},          // workgroups per CU (grid)
+    {"BENOR_EVENT_LANES_PER_CU", "tuning"},     // event level, N <= 256: lanes per CU
+    {"BENOR_TEST_DEFER_SEG_CAP", "test"},       // deferral segment capacity below the sizing rule
+    {"BENOR_TIMELINE", "diagnostic"},           // packed matrix-core kernel: per-wave phase stamps to a file
+};
+
+const char *knob(const char *name) {
+  for (const KnobSpec &k : kKnobs)
+    if (std::strcmp(k.name, name) == 0) return std::getenv(name);
+  std::fprintf(stderr, "libbenor: knob %s is not registered in kKnobs\n", name);
+  std::abort();
+}
+
+uint32_t knob_u32(const char *name, uint32_t dflt) {
+  const char *v = knob(name);
+  return v && *v ? (uint32_t)std::strtoul(v, nullptr, 10) : dflt;
+}
+
+bool knob_is(const char *name, const char *value) {
+  const char *v = knob(name);
+  return v && std::strcmp(v, value) == 0;
+}
+}  // namespace benor
+
 // One simulated network.  `mu` guards the node states: bo_consensus_start may
 // run on a worker thread (the N-API addon's napi_async_work) while the caller's
 // thread serves /stop, /getState and /status.  The kernel runs without the
@@ -340,9 +381,6 @@ static int plan_host(const bo_trials_cfg *cfg, std::vector<uint32_t> &live, std:
   if (cfg->k_max < 1 || cfg->k_max > BO_MAX_K) return fail(BO_ERR_INVALID_ARGUMENT, "k_max must be in [1, 1024]");
   if (cfg->mode != BO_MODE_LOCKSTEP && cfg->mode != BO_MODE_RANDOM_DELIVERY && cfg->mode != BO_MODE_EVENT)
     return fail(BO_ERR_UNSUPPORTED, "unknown delivery mode");
-  if (cfg->mode == BO_MODE_EVENT && cfg->N > benor::kMaxEventN && !cfg->crash_at && cfg->crash_count > 0)
-    return fail(BO_ERR_UNSUPPORTED, "event mode: a random /stop schedule (crash_count) needs N <= 256; "
-                                    "give crash_at for larger networks");
   if (cfg->init_mode != BO_INIT_RANDOM && cfg->init_mode != BO_INIT_FIXED)
     return fail(BO_ERR_INVALID_ARGUMENT, "unknown init_mode");
   if (!cfg->faulty) return fail(BO_ERR_INVALID_ARGUMENT, "faulty is NULL");
@@ -371,6 +409,8 @@ static int plan_host(const bo_trials_cfg *cfg, std::vector<uint32_t> &live, std:
   kp.q = cfg->N - cfg->F;
   kp.crash_count = cfg->crash_count;
   kp.crash_window = cfg->crash_window;
+  if (cfg->mode == BO_MODE_EVENT && !cfg->crash_at && cfg->crash_count > 0 && cfg->crash_window > 0)
+    kp.ev_rstops = std::min<uint32_t>(cfg->crash_count, m);   // per-trial random /stop schedule
   kp.live = live_run && cfg->mode == BO_MODE_EVENT ? 1u : 0u;
   for (uint32_t i = 0; i < cfg->N && i < 4u * 64u; ++i)
     if (cfg->faulty[i]) kp.faulty_mask[i >> 6] |= 1ull << (i & 63u);
@@ -396,6 +436,13 @@ static int plan_host(const bo_trials_cfg *cfg, std::vector<uint32_t> &live, std:
   return BO_OK;
 }
 
+// BO_KERNEL_* of a plan: its variant, except the wave-per-trial event kernel
+// (variant 5: N > 256 or a live run), which is the event-level family too.
+static int kernel_family(const benor::KParams &kp) {
+  if (kp.m == 0) return BO_KERNEL_NONE;
+  return kp.variant == 5u ? BO_KERNEL_EVENT : (int)kp.variant;
+}
+
 int bo_kernel_for(const bo_trials_cfg *cfg, int *kernel_out) {
   if (!kernel_out) return fail(BO_ERR_INVALID_ARGUMENT, "NULL argument");
   std::vector<uint32_t> live;
@@ -403,7 +450,7 @@ int bo_kernel_for(const bo_trials_cfg *cfg, int *kernel_out) {
   benor::KParams kp;
   const int rc = plan_host(cfg, live, plane, kp);
   if (rc) return rc;
-  *kernel_out = kp.m == 0 ? BO_KERNEL_NONE : (int)kp.variant;
+  *kernel_out = kernel_family(kp);
   return BO_OK;
 }
 
@@ -484,8 +531,7 @@ static int plan_create_impl(const bo_trials_cfg *cfg, bo_plan **out, bool live_r
       // accesses, so fewer lanes whose slices stay cache-resident beat full
       // occupancy: 512 per CU for slices up to 4 KiB (N <= 12), else 256
       // (tools/ev_sweep.sh, BENOR_EVENT_LANES_PER_CU overrides).
-      uint64_t per_cu = stride_bytes <= 4096u ? 512u : 256u;
-      if (const char *ev = getenv("BENOR_EVENT_LANES_PER_CU")) per_cu = strtoull(ev, nullptr, 10);
+      uint64_t per_cu = benor::knob_u32("BENOR_EVENT_LANES_PER_CU", stride_bytes <= 4096u ? 512u : 256u);
       if (per_cu < 256u) per_cu = 256u;
       uint64_t lanes = (uint64_t)cus * per_cu;
       const uint64_t fit = (4ull << 30) / stride_bytes;
@@ -529,7 +575,7 @@ uint32_t bo_plan_live_nodes(const bo_plan *pl) { return pl ? pl->kp.m : 0u; }
 
 int bo_plan_kernel(const bo_plan *pl) {
   if (!pl) return -BO_ERR_INVALID_ARGUMENT;
-  return pl->kp.m == 0 ? BO_KERNEL_NONE : (int)pl->kp.variant;
+  return kernel_family(pl->kp);
 }
 
 // Lockstep: the R-phase needs c1 only (c0 = M - c1, M binary votes,
@@ -612,8 +658,7 @@ static int plan_launch_impl(bo_plan *pl, uint64_t trial_begin, uint64_t trial_co
     // deferral atomic and histogram flush (~12 ns each; N=256 F=0:
     // round 2 took 31 us for ~5 us of products).  The cooperative form's grid
     // is already one workgroup per group.
-    const char *full_ev = getenv("BENOR_CONT_FULL_GRID");   // A/B knob: every pass on the round-1 grid
-    const bool shrink = !benor::mfma_big_coop(kp) && !(full_ev && full_ev[0] == '1');
+    const bool shrink = !benor::mfma_big_coop(kp);
     auto pass_grid = [&](uint32_t r) {
       if (!shrink || r < 2u) return grid;
       const int g = grid >> (2u * (r - 1u));
@@ -636,8 +681,7 @@ static int plan_launch_impl(bo_plan *pl, uint64_t trial_begin, uint64_t trial_co
     const uint64_t words = 2u * cap + 64u + seg_words;                  // two lists, three lengths, segments
     // Test knob: a smaller segment capacity than the sizing rule's, so that a
     // GPU test can see the overflow reported (tests/test_mfma.py).
-    const char *cap_ev = getenv("BENOR_TEST_DEFER_SEG_CAP");
-    const uint32_t test_seg_cap = cap_ev ? (uint32_t)strtoul(cap_ev, nullptr, 10) : 0u;
+    const uint32_t test_seg_cap = benor::knob_u32("BENOR_TEST_DEFER_SEG_CAP", 0u);
     if (pl->defer_words < words) {
       if (pl->d_defer) (void)hipFree(pl->d_defer);
       pl->d_defer = nullptr;
@@ -687,7 +731,7 @@ static int plan_launch_impl(bo_plan *pl, uint64_t trial_begin, uint64_t trial_co
     kp.trial_begin = trial_begin + done;
     kp.trial_count = n;
     const int grid = benor::lockstep_grid(kp, pl->device);
-    const char *tl_path = kp.variant == 8 ? getenv("BENOR_TIMELINE") : nullptr;
+    const char *tl_path = kp.variant == 8 ? benor::knob("BENOR_TIMELINE") : nullptr;
     if (tl_path) {
       HIP_TRY(launch_with_timeline(kp, grid, s, tl_path));
     } else {
@@ -704,6 +748,11 @@ int bo_plan_launch(bo_plan *pl, uint64_t trial_begin, uint64_t trial_count, uint
                           reinterpret_cast<hipStream_t>(stream));
 }
 
+namespace {
+int plan_flag_read(bo_plan *pl, hipStream_t s, uint32_t &v);
+int plan_flag_error(uint32_t v);
+}  // namespace
+
 int bo_plan_run(bo_plan *pl, uint64_t trial_begin, uint64_t trial_count, uint64_t *hist_host) {
   if (!pl || !hist_host) return fail(BO_ERR_INVALID_ARGUMENT, "NULL argument");
   const uint32_t H = bo_hist_len(pl->cfg.k_max);
@@ -717,24 +766,57 @@ int bo_plan_run(bo_plan *pl, uint64_t trial_begin, uint64_t trial_count, uint64_
   (void)hipFree(d);
   if (e != hipSuccess) return hip_fail(e, "bo_plan_run");
   if (rc) return rc;
-  rc = bo_plan_check(pl);
+  uint32_t flag = 0;
+  rc = plan_flag_read(pl, nullptr, flag);   // the launches went to the null stream
+  if (!rc) rc = plan_flag_error(flag);
   if (rc) return rc;
   for (uint32_t i = 0; i < H; ++i) hist_host[i] += h[i];
   return BO_OK;
 }
 
-int bo_plan_check(bo_plan *pl) {
-  if (!pl) return fail(BO_ERR_INVALID_ARGUMENT, "NULL argument");
+namespace {
+// The plan's invariant flag, read with a copy ordered on `s` (the stream its
+// launches went to) on the plan's device: waits for that stream only, not for
+// other plans', torch's or a live run's work (bo_plan_run, bo_consensus_wait).
+// Cleared when set.
+int plan_flag_read(bo_plan *pl, hipStream_t s, uint32_t &v) {
+  v = 0;
   if (!pl->d_flag) return BO_OK;
-  HIP_TRY(hipDeviceSynchronize());
-  uint32_t v = 0;
-  HIP_TRY(hipMemcpy(&v, pl->d_flag, sizeof v, hipMemcpyDeviceToHost));
+  int cur = 0;
+  HIP_TRY(hipGetDevice(&cur));
+  if (cur != pl->device) HIP_TRY(hipSetDevice(pl->device));
+  hipError_t e = hipMemcpyAsync(&v, pl->d_flag, sizeof v, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e == hipSuccess && v) e = hipMemsetAsync(pl->d_flag, 0, sizeof v, s);
+  if (e == hipSuccess && v) e = hipStreamSynchronize(s);
+  if (cur != pl->device) (void)hipSetDevice(cur);
+  if (e != hipSuccess) return hip_fail(e, "plan flag read");
+  return BO_OK;
+}
+
+int plan_flag_error(uint32_t v) {
   if (!v) return BO_OK;
-  HIP_TRY(hipMemset(pl->d_flag, 0, sizeof v));
   if (v & 1u)
     return fail(BO_ERR_INTERNAL, "a matrix-core launch deferred more trials than its segment holds: "
                                  "its histogram is incomplete (deferral segment sizing)");
   return fail(BO_ERR_INTERNAL, "an event-level message pool filled up: the affected trials stopped early");
+}
+}  // namespace
+
+// Standalone check after bo_plan_launch on streams the library does not know:
+// the whole plan device is synchronised first.
+int bo_plan_check(bo_plan *pl) {
+  if (!pl) return fail(BO_ERR_INVALID_ARGUMENT, "NULL argument");
+  if (!pl->d_flag) return BO_OK;
+  int cur = 0;
+  HIP_TRY(hipGetDevice(&cur));
+  if (cur != pl->device) HIP_TRY(hipSetDevice(pl->device));
+  const hipError_t e = hipDeviceSynchronize();
+  if (cur != pl->device) (void)hipSetDevice(cur);
+  if (e != hipSuccess) return hip_fail(e, "bo_plan_check");
+  uint32_t v = 0;
+  const int rc = plan_flag_read(pl, nullptr, v);
+  return rc ? rc : plan_flag_error(v);
 }
 
 int bo_run_trials(const bo_trials_cfg *cfg, uint64_t trial_begin, uint64_t trial_count, uint64_t *hist_host) {
@@ -951,7 +1033,9 @@ int bo_consensus_wait(bo_network *net) {
   hipError_t e = hipStreamSynchronize(lr->s);
   if (e == hipSuccess) e = hipMemcpy(states.data(), lr->d_st, sizeof(bo_node_state) * N, hipMemcpyDeviceToHost);
   if (e == hipSuccess) e = hipMemcpy(&rounds, lr->d_r, sizeof(uint32_t), hipMemcpyDeviceToHost);
-  int rc = e != hipSuccess ? hip_fail(e, "bo_consensus_wait") : bo_plan_check(lr->pl);
+  uint32_t flag = 0;
+  int rc = e != hipSuccess ? hip_fail(e, "bo_consensus_wait") : plan_flag_read(lr->pl, lr->s, flag);
+  if (!rc) rc = plan_flag_error(flag);
   if (!rc && (rounds & 0x80000000u))
     rc = fail(BO_ERR_INTERNAL, "event-level message pool filled up: the run stopped early");
   {

@@ -45,20 +45,23 @@ function stopSchedule(N, stopAfter) {
 async function launchNetwork(N, F, initialValues, faultyList, options = {}) {
   const basePort = options.basePort !== undefined ? options.basePort : BASE_NODE_PORT;
   const kMax = options.kMax !== undefined ? options.kMax : 64;
-  // options.stopAfter: GET /stop requests that land during the run, as delivery
-  // counts per node (array of N, null = never; bo_consensus_start_sched).  The
-  // run is one kernel, so a /stop request arriving over HTTP while it is in
-  // flight is ordered after it; a scheduled one lands mid-round.
-  // options.live: the run starts when every running node has served /start
-  // and /start answers at once (node.ts:167-188 answers before consensus
-  // finishes); a GET /stop served over HTTP while it runs lands in the kernel
+  // The run starts when every running node has served /start, and /start
+  // answers at once (node.ts:167-188 answers before consensus finishes); a
+  // GET /stop served over HTTP while it runs lands in the kernel
   // (bo_consensus_start_live), and /getState shows the final states once the
-  // run has ended.
+  // run has ended -- the reference's callers poll it.
+  // options.sync: /start answers once the run has finished; a /stop arriving
+  // over HTTP while it is in flight is ordered after it.
+  // options.stopAfter: GET /stop requests that land during the run, as delivery
+  // counts per node (array of N, null = never; bo_consensus_start_sched), given
+  // up front; /start answers at the end of the run, as with sync.
   let sched;
   if (options.stopAfter !== undefined && options.stopAfter !== null) {
     if (options.live) throw new RangeError('stopAfter and live are exclusive: a live run takes /stop as it comes');
     sched = stopSchedule(N, options.stopAfter);
   }
+  if (options.live && options.sync) throw new RangeError('live and sync are exclusive');
+  const live = sched === undefined && !options.sync;
   const handle = addon.networkCreate(N, F, initialValues, faultyList);   // launchNodes.ts:10-13 errors
   const net = {
     handle, N, started: new Array(N).fill(false), running: null, ran: false, seed: options.seed,
@@ -71,9 +74,9 @@ async function launchNetwork(N, F, initialValues, faultyList, options = {}) {
   };
 
   function maybeRun() {
-    if (net.running || net.ran) return options.live ? null : net.running;
-    const live = runningNodes();
-    if (live.length === 0 || !live.every((i) => net.started[i])) return null;
+    if (net.running || net.ran) return live ? null : net.running;
+    const run = runningNodes();
+    if (run.length === 0 || !run.every((i) => net.started[i])) return null;
     let seed = net.seed;
     if (seed === undefined) {
       seed = (BigInt(Math.floor(Math.random() * 2 ** 32)) << 32n) | BigInt(Math.floor(Math.random() * 2 ** 32));
@@ -82,7 +85,7 @@ async function launchNetwork(N, F, initialValues, faultyList, options = {}) {
       net.ran = true;
       net.running = null;
     };
-    if (options.live) {
+    if (live) {
       try {
         addon.networkStartLive(handle, BigInt(seed), kMax);
       } catch (e) {

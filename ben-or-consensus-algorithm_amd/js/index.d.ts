@@ -37,16 +37,23 @@ export interface StartOptions {
   kMax?: number;
   /** GET /stop requests landing mid-run (node.ts:191-194): per node, the number of
    * POST /message deliveries (network-wide, seeded order) after which it is stopped;
-   * an array of N entries (null = never) or {nodeId: deliveries}.  Event-level kernels, N <= 4096. */
+   * an array of N entries (null = never) or {nodeId: deliveries}.  Event-level kernels,
+   * N <= 4096.  Resolves at the end of the run. */
   stopAfter?: (number | null)[] | { [nodeId: number]: number };
   /** Reject a second start on one network (libbenor error 8) instead of resolving as a no-op. */
   strict?: boolean;
-  /** Resolve once the kernel is launched (GET /start answers before consensus finishes);
-   * stopNode / stopConsensus then land in the running kernel, getNodesState / getNodeState /
-   * waitConsensus wait for the run.  Exclusive with stopAfter. */
+  /** Resolve once the run has finished (every live node decided, or kMax rounds); a stop
+   * sent meanwhile is ordered after the run.  Default: resolve once the kernel is launched,
+   * as the reference's startConsensus does (consensus.ts:3-8). */
+  sync?: boolean;
+  /** The default (launch, resolve, let stops land in the running kernel); exclusive with
+   * stopAfter and sync. */
   live?: boolean;
 }
 
+/** Resolves once the round loop is launched (before consensus finishes, like GET /start);
+ * stopNode / stopConsensus then land in the running kernel, and getNodesState / getNodeState /
+ * waitConsensus wait for the run.  {sync: true}: resolves after the run. */
 export declare function startConsensus(N: number, options?: StartOptions): Promise<void>;
 export declare function stopConsensus(N: number): Promise<void>;
 export declare function stopNode(nodeId: number): Promise<void>;
@@ -55,9 +62,9 @@ export declare function getNodesState(N: number): Promise<NodeState[]>;
 export declare function getNodeStatus(nodeId: number): Promise<{ status: 200 | 500; body: "live" | "faulty" }>;
 export declare function reachedFinality(states: NodeState[]): boolean;
 export declare function delay(ms: number): Promise<void>;
-/** End of a live run (startConsensus(N, {live: true})); resolves at once otherwise. */
+/** End of a run started by the default startConsensus; resolves at once otherwise. */
 export declare function waitConsensus(N: number): Promise<void>;
-/** After a live run: per node, the delivery count at which its /stop landed (null = none);
+/** After a run started by the default startConsensus: per node, the delivery count at which its /stop landed (null = none);
  * as stopAfter on a fresh network with the same seed it reproduces the run. */
 export declare function liveStopEvents(N: number): Promise<(number | null)[]>;
 
@@ -72,7 +79,7 @@ export interface TrialsConfig {
   kMax?: number;
   trialBegin?: bigint | number;
   trialCount?: bigint | number;
-  /** 0 lockstep (default), 1 random delivery (f <= F), 2 event level (N <= 4096; crashCount needs N <= 256) */
+  /** 0 lockstep (default), 1 random delivery (f <= F), 2 event level (N <= 4096) */
   mode?: 0 | 1 | 2;
   /** event mode: deliveries after which node i is stopped (null = never) */
   crashAt?: (number | null)[];

@@ -61,19 +61,22 @@ function randomSeed() {
   return (hi << 32n) | lo;
 }
 
-// Resolves once the round loop has run to completion (all live nodes decided,
-// or kMax rounds).  The reference resolves before consensus finishes and the
-// callers poll getNodesState; polling here sees the final states at once.
-// options.stopAfter: GET /stop requests that land while consensus runs
-// (node.ts:191-194) -- an array of N delivery counts or an object
-// {nodeId: deliveries}; a node is stopped after that many POST /message have
-// been handled network-wide (seeded delivery order, the event-level kernel,
-// N <= 4096).
-// options.live: resolve as soon as the kernel is launched, as the reference's
-// GET /start answers before consensus finishes; stopConsensus / stopNode then
-// land in the running kernel (bo_consensus_start_live), and getNodesState /
-// getNodeState / waitConsensus wait for the run to end.  liveStopEvents(N)
-// gives the delivery count at which each /stop landed (replayable as stopAfter).
+// As the reference's (consensus.ts:3-8): resolves once every running node has
+// served GET /start, i.e. as soon as the round loop is launched
+// (bo_consensus_start_live), before consensus finishes (node.ts:167-188
+// answers right after the round-1 broadcasts).  A stopConsensus / stopNode sent
+// afterwards lands in the running kernel before its next delivery (node.ts:45,
+// :191-194); getNodesState / getNodeState / waitConsensus wait for the run to
+// end, so the reference's start-then-poll callers see final states.
+// liveStopEvents(N) gives the delivery count at which each /stop landed
+// (replayable as stopAfter on a fresh network with the same seed).
+// options.sync: resolve when the round loop has run to completion (every live
+// node decided, or kMax rounds); a /stop sent while it runs is ordered after it.
+// options.stopAfter: GET /stop requests that land while consensus runs, given
+// up front -- an array of N delivery counts or an object {nodeId: deliveries};
+// a node is stopped after that many POST /message have been handled
+// network-wide (seeded delivery order, the event-level kernel, N <= 4096).
+// Resolves at the end of the run, like sync.
 // A second start on the same network resolves, as the reference's GET /start
 // answers 200, but runs nothing: its round inboxes outlive a run (node.ts:29-30),
 // so no fresh consensus can follow (options.strict: reject with libbenor error 8).
@@ -86,12 +89,16 @@ async function startConsensus(N, options = {}) {
     if (options.live) throw new RangeError('stopAfter and live are exclusive: a live run takes /stop as it comes');
     sched = stopSchedule(N, options.stopAfter);
   }
+  if (options.live && options.sync) throw new RangeError('live and sync are exclusive');
+  const live = sched === undefined && !options.sync;
   const cur = net(N);
   try {
-    if (options.live) {
+    if (live) {
       addon.networkStartLive(cur.handle, seed, kMax);
+      // kept until the network is replaced: every reader waits for it, and a
+      // failed run fails every later read rather than serving pre-run states
       cur.running = addon.networkWait(cur.handle);
-      cur.running.catch(() => {});   // surfaced by the next settle()
+      cur.running.catch(() => {});
       return;
     }
     await addon.networkStart(cur.handle, seed, kMax, sched);
@@ -100,13 +107,11 @@ async function startConsensus(N, options = {}) {
   }
 }
 
-// The end of a live run (a no-op otherwise).
+// The end of a live run (a no-op otherwise).  Concurrent readers all wait for
+// the same run (the reference's getNodesState is Promise.all over
+// getNodeState, __test__/tests/utils.ts:14-20).
 async function settle(cur) {
-  if (cur.running) {
-    const p = cur.running;
-    cur.running = null;
-    await p;
-  }
+  if (cur.running) await cur.running;
 }
 
 async function waitConsensus(N) {

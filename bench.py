@@ -21,11 +21,15 @@ roofline: of the kernel the plan picked, from the average kernel duration
          (HIP events on the launch stream).  The bench shape runs the
          matrix-core kernel: algorithmic e2m1 FLOP/s -- every
          live receiver sums the m live votes in each phase, 4m FLOP per live
-         node-round -- against the dense FP4 peak (~10 PFLOP/s).  With
-         BENOR_NO_MFMA=1 it runs the popcount W kernel: tally popcount words
-         per live node-round (2 or 3 * ceil(m/32), 44 at the bench shape;
-         DESIGN.md §4) against the v_bcnt_u32_b32 issue peak (256 CU x 4 SIMD
-         x 16 lanes x 2.4 GHz = 39.3 T words/s).
+         node-round -- against the dense FP4 peak (~10 PFLOP/s).  A --N/--F
+         shape the matrix cores do not take runs a popcount kernel: tally
+         popcount words per live node-round (2 or 3 * ceil(m/32); DESIGN.md
+         §4) against the v_bcnt_u32_b32 issue peak (256 CU x 4 SIMD x 16
+         lanes x 2.4 GHz = 39.3 T words/s).
+Environment: every BENOR_* variable set is recorded in the line ("env"); a
+         libbenor knob (benor.KNOBS: forced kernels, grids, test paths) makes
+         bench.py refuse to run -- a figure is only reported for the kernels
+         the planner picks by itself.
 cpu_baseline: the oracle's bit-plane restatement (oracle/benor_oracle.c,
          OpenMP over trials) on a bounded sample, rank 0 at N = 1 only, on
          every host thread and on one core.
@@ -329,27 +333,27 @@ def event_network(benor, N=1024, F=341, stop_node=500, stop_after=300_000, seed=
     init = [0] * F + [1] * (m // 2) + [0] * (m // 2) + ["?"] * (m % 2)
     faulty = [i < F for i in range(N)]
     out = {}
-    for label, sched in (("no stop (lockstep kernel)", None), ("stop inside round 1", {stop_node: stop_after})):
+    for label, sched in (("no stop, sync start (lockstep kernel)", None), ("stop inside round 1", {stop_node: stop_after})):
         benor.launchNetwork(N, F, init, faulty)
         t0 = time.perf_counter()
-        benor.startConsensus(N, seed=seed, stop_after=sched)
+        benor.startConsensus(N, seed=seed, stop_after=sched, sync=sched is None)
         dt = time.perf_counter() - t0
         st = benor.getNodesState(N)
         out[label] = {"seconds": dt, "stopped_nodes": sum(1 for s in st[F:] if s["killed"])}
-    # live start (bo_consensus_start_live): startConsensus returns at launch, the
-    # /stop is sent 5 ms later and lands in the running kernel; the run ends at
-    # getNodesState.  Reported: the wall time from the start to the final states
-    # and where the stop landed (replayable as a schedule).
+    # the default start (bo_consensus_start_live): startConsensus returns at
+    # launch, the /stop is sent 5 ms later and lands in the running kernel; the
+    # run ends at getNodesState.  Reported: the wall time from the start to the
+    # final states and where the stop landed (replayable as a schedule).
     benor.launchNetwork(N, F, init, faulty)
     t0 = time.perf_counter()
-    benor.startConsensus(N, seed=seed, live=True)
+    benor.startConsensus(N, seed=seed)
     t_start = time.perf_counter() - t0
     time.sleep(0.005)                                # the run is under way: the stop lands mid-round
     benor._current.stop_node(stop_node)
     st = benor.getNodesState(N)
     dt = time.perf_counter() - t0
     landed = benor._current.live_stop_events()[stop_node]
-    out["live start, /stop sent after it"] = {"seconds": dt, "start_returned_after_s": t_start,
+    out["default (live) start, /stop sent after it"] = {"seconds": dt, "start_returned_after_s": t_start,
                                                "stop_landed_at_delivery": landed,
                                                "stopped_nodes": sum(1 for s in st[F:] if s["killed"])}
     return {"N": N, "F": F, "initial_values": "half 1, half 0, one '?' (every R-phase ties)", **out}
@@ -359,20 +363,24 @@ def network_latency(benor, reps=200):
     """BASELINE configs[0]: one start.ts-style network (N=5, F=1, node 4 faulty,
     initial values [1,1,1,0,0], benorconsensus.test.ts:179-223) through the
     reference's own calls -- launchNetwork + startConsensus + getNodesState --
-    on the GPU; median and p90 wall time over `reps` networks."""
-    times = []
-    for rep in range(reps + 5):
-        t0 = time.perf_counter()
-        benor.launchNetwork(5, 1, [1, 1, 1, 0, 0], [False, False, False, False, True])
-        benor.startConsensus(5, seed=rep)
-        states = benor.getNodesState(5)
-        dt = time.perf_counter() - t0
-        if rep >= 5:
-            times.append(dt * 1e3)
-    times.sort()
-    ok = all(s["decided"] and s["x"] == 1 and s["k"] <= 2 for s in states[:4])
-    return {"networks": reps, "median_ms": times[len(times) // 2], "p90_ms": times[int(len(times) * 0.9)],
-            "reference_assertions_hold": ok}
+    on the GPU; median and p90 wall time over `reps` networks, for the default
+    start (resolves at launch, getNodesState waits for the run) and the sync one."""
+    out = {"networks": reps}
+    for label, kw in (("default", {}), ("sync", {"sync": True})):
+        times = []
+        for rep in range(reps + 5):
+            t0 = time.perf_counter()
+            benor.launchNetwork(5, 1, [1, 1, 1, 0, 0], [False, False, False, False, True])
+            benor.startConsensus(5, seed=rep, **kw)
+            states = benor.getNodesState(5)
+            dt = time.perf_counter() - t0
+            if rep >= 5:
+                times.append(dt * 1e3)
+        times.sort()
+        ok = all(s["decided"] and s["x"] == 1 and s["k"] <= 2 for s in states[:4])
+        out[label] = {"median_ms": times[len(times) // 2], "p90_ms": times[int(len(times) * 0.9)],
+                      "reference_assertions_hold": ok}
+    return out
 
 
 def cpu_baseline(N, F, k_max, seed, budget_s):
@@ -429,6 +437,13 @@ def main():
     import benor
     from benor.parallel import merge_histogram
 
+    env = {k: v for k, v in sorted(os.environ.items()) if k.startswith("BENOR_")}
+    forced = sorted(k for k in env if k in benor.KNOBS)
+    if forced:
+        print(f"bench.py: libbenor knobs set ({', '.join(forced)}): they force kernels, grids or test paths "
+              f"(benor.KNOBS); refusing to report a figure for anything but the planner's own choice",
+              file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # one process per GPU; BENOR_DIST_BACKEND=gloo rehearses several ranks on one GPU
@@ -576,6 +591,7 @@ def main():
         "all_node_rounds_per_s": rounds * N / elapsed,
         "trials_per_s": total_trials / elapsed,
         "agreement_violations": int(h[-1]),
+        "env": env,
     }
     if world == 1 and not args.no_other_configs:
         out["other_configs"] = other_configs(benor, torch, k_max, args.seed)

@@ -234,7 +234,7 @@ enum {
   BO_KERNEL_BLOCKED = 0,
   BO_KERNEL_W = 1,
   BO_KERNEL_RANDOM = 2,
-  BO_KERNEL_EVENT = 4,
+  BO_KERNEL_EVENT = 4,  /* event level: one lane per trial (N <= 256), one wave per trial (N > 256, live runs) */
   BO_KERNEL_LANE = 6,
   BO_KERNEL_MFMA = 7,
   BO_KERNEL_MFMA_SMALL = 8 /* packed matrix-core kernel: 2 <= m <= 32, m > F, no "?" initial value;

@@ -25,13 +25,13 @@ async function expectStatus(faultyArray) {   // :59-74
   }
 }
 
-// live: startConsensus resolves once the kernel is launched, as the reference's
-// does before consensus finishes (consensus.ts:3-8); the polling below is then
-// what the reference's suite relies on
-async function runToFinality(faultyArray, initialValues, live = false) {   // :138-160
+// The default startConsensus resolves once the kernel is launched, as the
+// reference's does before consensus finishes (consensus.ts:3-8); the polling
+// below is then what the reference's suite relies on.  sync: resolve after the run.
+async function runToFinality(faultyArray, initialValues, sync = false) {   // :138-160
   const servers = await b.launchNetwork(faultyArray.length, faultyArray.filter((e) => e === true).length,
     initialValues, faultyArray);
-  await b.startConsensus(faultyArray.length, { seed: 0x5EEDn, live });
+  await b.startConsensus(faultyArray.length, sync ? { seed: 0x5EEDn, sync: true } : { seed: 0x5EEDn });
   const time = Date.now();
   let states = await b.getNodesState(faultyArray.length);
   while (Date.now() - time < 2000 && !b.reachedFinality(states)) {
@@ -73,9 +73,9 @@ const finality = [
     [0, 0, 1, 1, 1, 0, 0, 1, 1], 'agree'],                                                         // :227-286
   ['No Faulty Nodes', [false, false, false, false, false], [0, 1, 0, 1, 1], 'x1'],                // :351-393
 ];
-for (const [name, fa, init, kind, live] of finality.flatMap((c) => [[...c, false], [...c, true]])) {
-  it(`Finality is reached - ${name}${live ? ' (live start)' : ''}`, 'gpu', async () => {
-    const { servers, states } = await runToFinality(fa, init, live);
+for (const [name, fa, init, kind, sync] of finality.flatMap((c) => [[...c, false], [...c, true]])) {
+  it(`Finality is reached - ${name}${sync ? ' (sync start)' : ''}`, 'gpu', async () => {
+    const { servers, states } = await runToFinality(fa, init, sync);
     checkFaultyNull(fa, states);
     const vals = [];
     states.forEach((s, i) => {
@@ -89,10 +89,10 @@ for (const [name, fa, init, kind, live] of finality.flatMap((c) => [[...c, false
   });
 }
 
-for (const live of [false, true]) {
-  it(`Finality is reached - Exceeding Fault Tolerance${live ? ' (live start)' : ''}`, 'gpu', async () => {   // :292-345
+for (const sync of [false, true]) {
+  it(`Finality is reached - Exceeding Fault Tolerance${sync ? ' (sync start)' : ''}`, 'gpu', async () => {   // :292-345
     const fa = [true, true, true, true, true, false, false, false, false, false];
-    const { servers, states } = await runToFinality(fa, [0, 0, 1, 1, 1, 0, 0, 1, 1, 0], live);
+    const { servers, states } = await runToFinality(fa, [0, 0, 1, 1, 1, 0, 0, 1, 1, 0], sync);
     checkFaultyNull(fa, states);
     states.forEach((s, i) => {
       if (fa[i]) return;
@@ -102,9 +102,27 @@ for (const live of [false, true]) {
   });
 }
 
-it('live start and a stop schedule are exclusive', 'setup', async () => {
+it('live start excludes a stop schedule and sync', 'setup', async () => {
   await b.launchNetwork(3, 0, [1, 1, 1], [false, false, false]);
   await assert.rejects(b.startConsensus(3, { live: true, stopAfter: [null, 5, null] }), RangeError);
+  await assert.rejects(b.startConsensus(3, { live: true, sync: true }), RangeError);
+});
+
+// __test__/tests/utils.ts:14-20 reads the states as Promise.all over GET
+// /getState: every concurrent read after the default start waits for the run
+it('Concurrent getNodeState reads after a default start all see the final states', 'gpu', async () => {
+  const N = 1024, F = 341;
+  const fa = Array.from({ length: N }, (_, i) => i < F);
+  const init = Array.from({ length: N }, (_, i) => (i < F ? 0 : (i % 3 === 0 ? 0 : 1)));
+  const servers = await b.launchNetwork(N, F, init, fa);
+  await b.startConsensus(N, { seed: 0xC0FFEEn });
+  const states = await Promise.all(Array.from({ length: N }, (_, i) => b.getNodeState(i)));
+  states.forEach((s, i) => {
+    if (fa[i]) { assert.strictEqual(s.decided, null); return; }
+    assert.strictEqual(s.decided, true); assert.strictEqual(s.x, 1); assert.strictEqual(s.k, 2);
+  });
+  assert.deepStrictEqual(await b.getNodesState(N), states);
+  await b.stopConsensus(N); await closeAllServers(servers);
 });
 
 it('Finality is reached - Randomized', 'gpu', async () => {   // :399-450

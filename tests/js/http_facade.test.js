@@ -45,9 +45,9 @@ const closeAll = (servers) => Promise.all(servers.map((s) => new Promise((r) => 
 const tests = [];
 const it = (name, group, fn) => tests.push({ name, group, fn });
 
-async function withNet(fa, init, fn, live = false) {
+async function withNet(fa, init, fn, sync = false) {
   const servers = await facade.launchNetwork(fa.length, fa.filter((e) => e === true).length, init, fa,
-    { basePort: BASE, seed: 0x5EEDn, live });
+    { basePort: BASE, seed: 0x5EEDn, sync });
   try { await fn(servers); } finally { await stopConsensus(fa.length); await closeAll(servers); }
 }
 
@@ -80,9 +80,11 @@ it('setup: getState JSON and /stop', 'setup', async () => {
   });
 });
 
-it('setup: live start and a stop schedule are exclusive', 'setup', async () => {
+it('setup: live start excludes a stop schedule and sync', 'setup', async () => {
   await assert.rejects(facade.launchNetwork(3, 0, [1, 1, 1], [false, false, false],
     { basePort: BASE, live: true, stopAfter: [null, 5, null] }), RangeError);
+  await assert.rejects(facade.launchNetwork(3, 0, [1, 1, 1], [false, false, false],
+    { basePort: BASE, live: true, sync: true }), RangeError);
 });
 
 const finality = [
@@ -93,11 +95,11 @@ const finality = [
   ['No Faulty Nodes', [false, false, false, false, false], [0, 1, 0, 1, 1], 'x1'],
   ['One node', [false], [1], 'x1'],
 ];
-// live: /start answers once the kernel is launched (node.ts:167-188 answers
-// before consensus finishes) and the caller polls /getState, as the reference
-// suite does (benorconsensus.test.ts)
-for (const [name, fa, init, kind, live] of finality.flatMap((c) => [[...c, false], [...c, true]])) {
-  it(`Finality over HTTP - ${name}${live ? ' (live start)' : ''}`, 'gpu', async () => {
+// By default /start answers once the kernel is launched (node.ts:167-188
+// answers before consensus finishes) and the caller polls /getState, as the
+// reference suite does (benorconsensus.test.ts); sync: /start answers after the run
+for (const [name, fa, init, kind, sync] of finality.flatMap((c) => [[...c, false], [...c, true]])) {
+  it(`Finality over HTTP - ${name}${sync ? ' (sync start)' : ''}`, 'gpu', async () => {
     await withNet(fa, init, async () => {
       await startConsensus(fa.length);
       const t = Date.now();
@@ -112,7 +114,7 @@ for (const [name, fa, init, kind, live] of finality.flatMap((c) => [[...c, false
         vals.push(s.x);
       });
       if (kind === 'agree') assert.ok(vals.every((v) => v === vals[0]));
-    }, live);
+    }, sync);
   });
 }
 
@@ -140,7 +142,10 @@ it('Finality over HTTP - Randomized', 'gpu', async () => {
 it('A second round of /start runs nothing new (inboxes persist, node.ts:29-30)', 'gpu', async () => {
   await withNet([false, false, false, false, true], [1, 1, 1, 0, 0], async () => {
     await startConsensus(5);
-    const a = await getNodesState(5);
+    const t = Date.now();
+    let a = await getNodesState(5);
+    while (Date.now() - t < 2000 && !reachedFinality(a)) { await delay(20); a = await getNodesState(5); }
+    assert.ok(reachedFinality(a));
     await startConsensus(5);
     assert.strictEqual((await get(BASE, '/start')).status, 200);
     assert.deepStrictEqual(await getNodesState(5), a);

@@ -65,6 +65,19 @@ def test_bench_refuses_world_mismatch():
     assert r.returncode == 2 and "WORLD_SIZE=1" in r.stderr
 
 
+@pytest.mark.parametrize("knob", ["BENOR_NO_MFMA", "BENOR_BLOCKS_PER_CU", "BENOR_TIMELINE"])
+def test_bench_refuses_libbenor_knobs(knob):
+    """A knob that forces a kernel, a grid or a test path makes bench.py exit
+    before any GPU work: a figure is only reported for the
+    planner's own kernels."""
+    env = dict(os.environ, **{knob: "1"})
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "1", "--warmup", "0"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2 and knob in r.stderr and "refusing" in r.stderr
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
 def _run_bench(args, env_extra=None, launcher=None, timeout=300):
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", **(env_extra or {}))
     env.pop("WORLD_SIZE", None)
@@ -93,11 +106,12 @@ def test_bench_single_gpu_line():
     assert c5a["mean_rounds"] == 1.0 and "kernels_per_launch" not in c5a
     assert c5b["kernels_per_launch"] and c5b["undecided_trials"] == 0 and 1.0 < c5b["mean_rounds"] < 1.05
     c1 = oc.pop("C1 N=5,F=1 network API")                 # configs[0]: one network, reference calls
-    assert c1["reference_assertions_hold"] and 0 < c1["median_ms"] < 50
+    for leg in ("default", "sync"):
+        assert c1[leg]["reference_assertions_hold"] and 0 < c1[leg]["median_ms"] < 50
     net = oc.pop("C4 N=1024,F=341 network API, mid-run /stop")   # one network through the drop-in API
     assert net["stop inside round 1"]["stopped_nodes"] == 1 and net["stop inside round 1"]["seconds"] > 0
-    assert net["no stop (lockstep kernel)"]["stopped_nodes"] == 0
-    live = net["live start, /stop sent after it"]
+    assert net["no stop, sync start (lockstep kernel)"]["stopped_nodes"] == 0
+    live = net["default (live) start, /stop sent after it"]
     assert live["stopped_nodes"] == 1 and live["stop_landed_at_delivery"] is not None
     assert live["start_returned_after_s"] < live["seconds"]
     sweep = oc.pop("C5 sweep (2^30 trials, 224 cells)")          # configs[4] end to end, CSV checked

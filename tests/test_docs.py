@@ -71,3 +71,40 @@ def test_profile_index_entries_exist():
     assert len(names) > 50
     missing = sorted(n for n in names if not os.path.exists(os.path.join(ROOT, "profiles", n)))
     assert not missing, f"profiles/README.md indexes files that are not in profiles/: {missing}"
+
+
+# ------------------------------------------------- environment knobs
+CSRC = os.path.join(ROOT, PKG, "csrc")
+
+
+def _csrc_text():
+    out = {}
+    for f in sorted(os.listdir(CSRC)):
+        if f.endswith((".hip", ".h", ".cpp", ".c")):
+            out[f] = open(os.path.join(CSRC, f), encoding="utf-8").read()
+    return out
+
+
+def test_one_getenv_and_every_knob_registered():
+    """The library reads the environment in one place (benor::knob, over the
+    kKnobs table); every knob a source names is registered there, mirrored by
+    benor.KNOBS and documented in DESIGN.md; no dropped A/B knob survives."""
+    import benor
+
+    src = _csrc_text()
+    getenv = [(f, n) for f, t in src.items() for n in re.findall(r"\bgetenv\s*\(", t)]
+    assert [f for f, _ in getenv] == ["benor_runtime.cpp"], getenv
+    rt = src["benor_runtime.cpp"]
+    table = rt[rt.index("constexpr KnobSpec kKnobs[]"):]
+    table = table[:table.index("};")]
+    registered = dict(re.findall(r'\{"(BENOR_[A-Z0-9_]+)",\s*"(\w+)"\}', table))
+    used = {n for t in src.values() for n in re.findall(r'knob(?:_u32|_is)?\("(BENOR_[A-Z0-9_]+)"', t)}
+    assert used <= set(registered), used - set(registered)
+    assert set(registered) <= used, set(registered) - used          # no registered knob left unused
+    assert registered == benor.KNOBS
+    design = open(os.path.join(ROOT, "DESIGN.md"), encoding="utf-8").read()
+    for name in registered:
+        assert f"`{name}`" in design, name
+    for dropped in ("BENOR_RANDOM_V1", "BENOR_COOP_PF", "BENOR_COOP_EXP", "BENOR_COOP_CBIAS", "BENOR_COOP_NT",
+                    "BENOR_CONT_FULL_GRID", "BENOR_SMALL_FORM", "BENOR_EVENT_FAST"):
+        assert all(dropped not in t for t in src.values()), dropped

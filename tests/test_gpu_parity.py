@@ -168,8 +168,8 @@ def test_second_start_is_a_no_op():
 
 
 def test_stop_during_run_is_kept():
-    """A /stop served while the kernel runs (another thread) is ordered after
-    the run: the node keeps its final state and stays killed.  N=2048 with
+    """A /stop served while a sync start's kernel runs (another thread) is
+    ordered after the run: the node keeps its final state and stays killed.  N=2048 with
     F=1024 never decides (m <= 2F), so the run lasts k_max = 1024 rounds."""
     import threading
 
@@ -177,7 +177,7 @@ def test_stop_during_run_is_kept():
     init = [i % 2 for i in range(N)]
     benor.launchNetwork(N, F, init, [i < F for i in range(N)])
     net = benor._current
-    t = threading.Thread(target=lambda: benor.startConsensus(N, seed=9, k_max=K))
+    t = threading.Thread(target=lambda: benor.startConsensus(N, seed=9, k_max=K, sync=True))
     t.start()
     net.stop_node(1500)
     t.join()
@@ -345,10 +345,10 @@ def test_random_delivery_matches_oracle(N, F, f, trials):
 
 # Bernoulli + fix-up sampler (k >= 64, 8k > m): every comparator width (a odd,
 # a = 2 mod 4, a = 4 mod 8, a = 8: 4, 3, 2, 1 stream words per mask word), every
-# index-field width class (b = 7..12: 4, 3 or 2 fields per word) and m = 2^b
-# (no range check) against the oracle.
+# index-field width class (b = 7..12: 4, 3 or 2 fields per word; b = 7 only at
+# m = 128, q = 64) and m = 2^b (no range check) against the oracle.
 @pytest.mark.parametrize("m,q", [(256, 170), (200, 120), (512, 380), (700, 315), (1024, 683), (1500, 1003),
-                                 (3000, 1790), (2048, 1229), (256, 66)])
+                                 (3000, 1790), (2048, 1229), (256, 66), (128, 64)])
 def test_random_delivery_bernoulli_sampler_shapes(m, q):
     ab = oracle.delivery_bernoulli(m, q)
     assert ab is not None
@@ -418,26 +418,25 @@ def test_event_mode_without_stop_equals_lockstep_kernel():
         np.testing.assert_array_equal(a, b)
 
 
-@pytest.mark.parametrize("N,F,f,T,init", [(1024, 341, 0, 3000, None), (1024, 341, 100, 2000, None),
-                                          (600, 200, 37, 2000, "q"), (4096, 1365, 0, 64, None),
-                                          (3000, 1210, 0, 100, None), (257, 80, 1, 4000, "q")])
-def test_random_delivery_r04_kernel_equals_r02_kernel(N, F, f, T, init):
-    """The r04 Bernoulli kernel (benor_random.hip: uniform Philox rounds hoisted,
-    ds_mskor_rtn fix-up with speculative batches and undo, padded bitset rows)
-    gives the r02 kernel's histograms bit for bit (BENOR_RANDOM_V1=1 selects the
-    r02 kernel), on random and fixed initial values with "?" inputs."""
+@pytest.mark.parametrize("N,F,f,T,init", [(1024, 341, 0, 400, None), (1024, 341, 100, 300, None),
+                                          (600, 200, 37, 600, "q"), (4096, 1365, 0, 24, None),
+                                          (3000, 1210, 0, 40, None), (257, 80, 1, 2000, "q")])
+def test_random_delivery_bernoulli_kernel_matches_oracle(N, F, f, T, init):
+    """The Bernoulli-sampler kernel (benor_random.hip: uniform Philox rounds
+    hoisted, ds_mskor_rtn fix-up with speculative batches and undo, padded
+    bitset rows) against oracle_delivery_mask's sequential definition, on
+    random and fixed initial values with "?" inputs.  (Until r04 this compared
+    it with the r02 kernel, which r05 deleted.)"""
     fl = first_f(N, f)
     vals = None
     if init == "q":
         rng = np.random.default_rng(N)
         vals = ["?" if rng.random() < 0.1 else int(rng.integers(0, 2)) for _ in range(N)]
-    new = benor.TrialsPlan(N, F, fl, seed=0xA5A5 ^ N, k_max=12, mode=RD, initial_values=vals)
-    os.environ["BENOR_RANDOM_V1"] = "1"
-    try:
-        old = benor.TrialsPlan(N, F, fl, seed=0xA5A5 ^ N, k_max=12, mode=RD, initial_values=vals)
-    finally:
-        os.environ.pop("BENOR_RANDOM_V1", None)
-    np.testing.assert_array_equal(new.run(99, T), old.run(99, T))
+    plan = benor.TrialsPlan(N, F, fl, seed=0xA5A5 ^ N, k_max=12, mode=RD, initial_values=vals)
+    assert plan.kernel == benor.BO_KERNEL_RANDOM
+    ref = oracle.run_trials(N, F, fl, seed=0xA5A5 ^ N, trial_begin=99, trial_count=T, k_max=12,
+                            mode=oracle.MODE_RANDOM_DELIVERY, initial_values=vals)
+    np.testing.assert_array_equal(plan.run(99, T), ref.hist)
 
 
 # ------------------------------------- event level above N = 256 (benor_event_big.hip)
@@ -466,6 +465,26 @@ def test_event_mode_big_matches_oracle(N, F, trials, stops, init):
     np.testing.assert_array_equal(got, ref.hist)
 
 
+@pytest.mark.parametrize("N,F,cc,cw,trials", [(1024, 341, 1, 1_400_000, 3), (1024, 341, 3, 3_000_000, 3),
+                                              (1024, 341, 5, 800_000, 2), (4096, 1365, 2, 23_000_000, 2),
+                                              (4096, 1365, 5, 30_000_000, 1), (300, 99, 4, 180_000, 4)])
+def test_event_mode_big_random_stops_match_oracle(N, F, cc, cw, trials):
+    """A random /stop schedule (crash_count nodes at uniform delivery counts in
+    [0, crash_window), drawn per trial from Philox stream 4) at the configs[3]
+    and configs[4] shapes: the wave-per-trial kernel draws it on the device
+    (Floyd picks, then one delivery count per pick) and its histograms equal
+    oracle (iii) event_trials bit for bit.  Windows of about one to two rounds
+    of deliveries put the stops inside rounds 1 and 2."""
+    fl = first_f(N, F)
+    seed = 0x5707 ^ N ^ (cc << 20)
+    plan = benor.TrialsPlan(N, F, fl, seed=seed, k_max=8, mode=EV, crash_count=cc, crash_window=cw)
+    assert plan.kernel == benor.BO_KERNEL_EVENT
+    got = plan.run(11, trials)
+    ref, _ = oracle.event_trials(N, F, fl, seed=seed, trial_begin=11, trial_count=trials, k_max=8,
+                                 crash_count=cc, crash_window=cw)
+    np.testing.assert_array_equal(got, ref.hist)
+
+
 def test_event_mode_big_without_stop_equals_lockstep_kernel():
     """Without a /stop every phase completes with the whole live set, so the
     delivery order cannot change a tally: the big event kernel's histogram is
@@ -475,28 +494,6 @@ def test_event_mode_big_without_stop_equals_lockstep_kernel():
         a = benor.TrialsPlan(N, F, fl, seed=9, k_max=16, mode=EV).run(0, 40)
         b = benor.TrialsPlan(N, F, fl, seed=9, k_max=16).run(0, 40)
         np.testing.assert_array_equal(a, b)
-
-
-def test_event_mode_big_fast_paths_off_equal_on():
-    """BENOR_EVENT_FAST=0 (every batch scans its picks and loads its own pool
-    words) and the default (collision bitmap, next-batch prefetch) give the same
-    histograms and per-node states: the fast paths change no delivery."""
-    N, F = 1024, 341
-    fl = first_f(N, F)
-    m = N - F
-    vals = [0] * F + [1] * (m // 2) + [0] * (m // 2) + ["?"]
-    sched = [None] * N
-    sched[500] = 400_000
-    fast = benor.TrialsPlan(N, F, fl, seed=5, k_max=8, mode=EV, crash_at=sched, initial_values=vals).run(0, 3)
-    _, st_fast = benor.run_trial_states(N, F, fl, seed=5, trial=0, k_max=8, mode=EV, crash_at=sched)
-    os.environ["BENOR_EVENT_FAST"] = "0"
-    try:
-        slow = benor.TrialsPlan(N, F, fl, seed=5, k_max=8, mode=EV, crash_at=sched, initial_values=vals).run(0, 3)
-        _, st_slow = benor.run_trial_states(N, F, fl, seed=5, trial=0, k_max=8, mode=EV, crash_at=sched)
-    finally:
-        os.environ.pop("BENOR_EVENT_FAST", None)
-    np.testing.assert_array_equal(fast, slow)
-    assert st_fast == st_slow
 
 
 def test_event_mode_big_states_match_oracle():

@@ -97,9 +97,11 @@ def oracle_states(c):
 
 
 def test_schedule_validation():
-    # a random /stop schedule (batch API crash_count) needs the one-lane event kernel: N <= 256
-    with pytest.raises(RuntimeError, match="libbenor error 7"):
-        benor.TrialsPlan(300, 0, [False] * 300, mode=benor.BO_MODE_EVENT, crash_count=3, crash_window=100)
+    # a random /stop schedule (batch API crash_count) runs at every N since r05 (the
+    # wave-per-trial kernel draws it per trial); planned on the host, no device needed
+    for N in (300, 1024, 4096):
+        assert benor.kernel_for(N, N // 3, [i < N // 3 for i in range(N)], mode=benor.BO_MODE_EVENT,
+                                crash_count=3, crash_window=100) == benor.BO_KERNEL_EVENT
     benor.launchNetwork(5, 1, [1, 1, 1, 0, 0], [False, False, False, False, True])
     L = benor.lib()
     sched = (benor.ctypes.c_uint32 * 3)(1, 2, 3)
@@ -132,7 +134,8 @@ def test_network_api_stop_schedule_matches_oracle(idx):
 
 @pytest.mark.gpu
 def test_no_schedule_is_the_lockstep_start():
-    """An all-NEVER schedule is bo_consensus_start (lockstep kernel)."""
+    """An all-NEVER schedule is bo_consensus_start (lockstep kernel), and the
+    default start (event-level kernel, no stop sent) gives the same states."""
     c, _ = cases()[4]
     benor.launchNetwork(c["N"], c["F"], c["init"], c["faulty"])
     benor.startConsensus(c["N"], seed=c["seed"], k_max=c["k_max"], stop_after=[None] * c["N"])
