@@ -136,16 +136,35 @@ struct bo_plan {
   int device = 0;
 };
 
-// A live run (bo_consensus_start_live): the event-level kernel runs on its own
-// stream while the caller serves /stop, /getState and /status; GET /stop
-// requests reach the running kernel through a host-mapped mailbox.
-struct bo_live {
-  bo_plan *pl = nullptr;
+namespace {
+// The resources of one live run, kept for the next one (r05: the default
+// startConsensus is a live run, and a network of the reference's size spent
+// 0.8 ms of its 0.83 ms creating a stream, pinning a mailbox and allocating
+// and freeing ten device buffers).  A slot is one device's stream, a
+// host-mapped mailbox for BO_MAX_N nodes and one device buffer that grows to
+// the largest run it served; slots are handed out under a lock and returned
+// by bo_consensus_wait.  Never freed (process lifetime, like StateScratch).
+struct LiveSlot {
+  int device = -1;
   hipStream_t s = nullptr;
   uint32_t *box = nullptr;             // host-mapped mailbox (benor::kLiveReq / kLiveEv layout)
-  bo_node_state *d_st = nullptr;
-  uint64_t *d_h = nullptr;
-  uint32_t *d_r = nullptr;
+  uint32_t *dbox = nullptr;            // its device address
+  unsigned char *d = nullptr;          // flag | states | hist | rounds | live ids | init plane | init x | pool
+  size_t bytes = 0;
+  std::vector<unsigned char> h;        // host staging of the buffer's head
+};
+std::mutex g_slots_mu;
+std::vector<LiveSlot *> g_free_slots;
+}  // namespace
+
+// A live run (bo_consensus_start_live): the event-level kernel runs on its
+// slot's stream while the caller serves /stop, /getState and /status; GET
+// /stop requests reach the running kernel through the slot's mailbox.
+struct bo_live {
+  LiveSlot *slot = nullptr;
+  bo_plan pl;                          // device tables: views into the slot's buffer
+  uint32_t *box = nullptr;             // slot->box
+  size_t o_st = 0, o_r = 0;            // offsets of the states and the round word
   std::vector<uint32_t> active;
 };
 
@@ -951,40 +970,108 @@ int bo_run_trial_states(const bo_trials_cfg *cfg, uint64_t trial, bo_node_state 
 
 // ------------------------------------------------------------ live runs
 namespace {
+LiveSlot *slot_acquire(int dev) {
+  {
+    std::lock_guard<std::mutex> g(g_slots_mu);
+    for (size_t i = 0; i < g_free_slots.size(); ++i)
+      if (g_free_slots[i]->device == dev) {
+        LiveSlot *sl = g_free_slots[i];
+        g_free_slots.erase(g_free_slots.begin() + (long)i);
+        return sl;
+      }
+  }
+  auto *sl = new LiveSlot();
+  sl->device = dev;
+  const size_t box_bytes = sizeof(uint32_t) * (benor::kLiveEv + BO_MAX_N);
+  if (hipStreamCreateWithFlags(&sl->s, hipStreamNonBlocking) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void **>(&sl->box), box_bytes, hipHostMallocMapped | hipHostMallocCoherent) !=
+          hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void **>(&sl->dbox), sl->box, 0) != hipSuccess) {
+    if (sl->box) (void)hipHostFree(sl->box);
+    if (sl->s) (void)hipStreamDestroy(sl->s);
+    delete sl;
+    return nullptr;
+  }
+  return sl;
+}
+
+void slot_release(LiveSlot *sl) {
+  if (!sl) return;
+  std::lock_guard<std::mutex> g(g_slots_mu);
+  g_free_slots.push_back(sl);
+}
+
 void live_free(bo_live *lr) {
   if (!lr) return;
-  if (lr->s) (void)hipStreamSynchronize(lr->s);
-  if (lr->d_st) (void)hipFree(lr->d_st);
-  if (lr->d_h) (void)hipFree(lr->d_h);
-  if (lr->d_r) (void)hipFree(lr->d_r);
-  if (lr->box) (void)hipHostFree(lr->box);
-  if (lr->s) (void)hipStreamDestroy(lr->s);
-  if (lr->pl) bo_plan_destroy(lr->pl);
+  if (lr->slot) {
+    (void)hipStreamSynchronize(lr->slot->s);   // the kernel no longer reads the mailbox or the buffer
+    slot_release(lr->slot);
+  }
   delete lr;
 }
 
-// Plan, mailbox, state buffers and the launch on the run's own stream.
+size_t align_up(size_t v, size_t a) { return (v + a - 1u) & ~(a - 1u); }
+
+// Plan (host), slot, one upload and the launch on the slot's stream.
 int live_launch(bo_live *lr, const bo_trials_cfg *cfg) {
-  int rc = plan_create_impl(cfg, &lr->pl, true);
+  std::vector<uint32_t> live;
+  std::vector<uint4> plane;
+  benor::KParams kp;
+  int rc = plan_host(cfg, live, plane, kp, true);
   if (rc) return rc;
-  const uint32_t N = cfg->N, H = bo_hist_len(cfg->k_max);
-  HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&lr->box), sizeof(uint32_t) * (benor::kLiveEv + N),
-                        hipHostMallocMapped | hipHostMallocCoherent));
-  std::memset(lr->box, 0, sizeof(uint32_t) * benor::kLiveEv);
-  for (uint32_t i = 0; i < N; ++i) lr->box[benor::kLiveEv + i] = 0xFFFFFFFFu;
-  uint32_t *dbox = nullptr;
-  HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&dbox), lr->box, 0));
-  lr->pl->kp.live_box = dbox;
+  int dev = 0;
+  rc = check_device(&dev);
+  if (rc) return rc;
+  LiveSlot *sl = slot_acquire(dev);
+  if (!sl) return fail(BO_ERR_HIP, "live run: stream / mailbox allocation failed");
+  lr->slot = sl;
+  lr->box = sl->box;
+  const uint32_t N = cfg->N, H = bo_hist_len(cfg->k_max), m = kp.m;
+  // layout: flag | states [N] | hist [H] u64 | rounds | live [m] | init [W] uint4 | init x [N] | pool
+  const size_t o_st = 16u, o_h = align_up(o_st + sizeof(bo_node_state) * N, 16u);
+  const size_t o_r = o_h + sizeof(uint64_t) * H, o_live = align_up(o_r + 4u, 16u);
+  const size_t o_init = align_up(o_live + sizeof(uint32_t) * m, 16u);
+  const size_t o_ix = o_init + sizeof(uint4) * plane.size();
+  const size_t o_pool = align_up(o_ix + N, 256u);
+  const size_t bytes = o_pool + (size_t)kp.ev_stride * 4u;
+  if (sl->bytes < bytes) {
+    if (sl->d) (void)hipFree(sl->d);
+    sl->d = nullptr;
+    sl->bytes = 0;
+    HIP_TRY(hipMalloc(&sl->d, bytes));
+    sl->bytes = bytes;
+  }
+  sl->h.assign(o_pool, 0);
   std::vector<bo_node_state> st;
   initial_states(cfg, st);
-  HIP_TRY(hipMalloc(&lr->d_st, sizeof(bo_node_state) * N));
-  HIP_TRY(hipMalloc(&lr->d_h, sizeof(uint64_t) * H));
-  HIP_TRY(hipMalloc(&lr->d_r, sizeof(uint32_t)));
-  HIP_TRY(hipMemcpy(lr->d_st, st.data(), sizeof(bo_node_state) * N, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemset(lr->d_h, 0, sizeof(uint64_t) * H));
-  HIP_TRY(hipMemset(lr->d_r, 0, sizeof(uint32_t)));
-  HIP_TRY(hipStreamCreateWithFlags(&lr->s, hipStreamNonBlocking));
-  return plan_launch_impl(lr->pl, 0, 1, lr->d_h, lr->d_st, lr->d_r, lr->s);
+  std::memcpy(sl->h.data() + o_st, st.data(), sizeof(bo_node_state) * N);
+  if (m) std::memcpy(sl->h.data() + o_live, live.data(), sizeof(uint32_t) * m);
+  if (!plane.empty()) std::memcpy(sl->h.data() + o_init, plane.data(), sizeof(uint4) * plane.size());
+  if (cfg->init_mode == BO_INIT_FIXED) std::memcpy(sl->h.data() + o_ix, cfg->init, N);
+  // the mailbox: no request, no stop landed (the previous run's kernel has ended)
+  std::memset(sl->box, 0, sizeof(uint32_t) * benor::kLiveEv);
+  for (uint32_t i = 0; i < N; ++i) sl->box[benor::kLiveEv + i] = 0xFFFFFFFFu;
+  HIP_TRY(hipMemcpyAsync(sl->d, sl->h.data(), o_pool, hipMemcpyHostToDevice, sl->s));
+  bo_plan &pl = lr->pl;
+  pl.cfg = *cfg;
+  pl.cfg.faulty = nullptr;
+  pl.cfg.init = nullptr;
+  pl.cfg.crash_at = nullptr;
+  pl.device = dev;
+  pl.live_ids = live;
+  pl.kp = kp;
+  pl.d_flag = reinterpret_cast<uint32_t *>(sl->d);
+  pl.kp.live_ids = reinterpret_cast<uint32_t *>(sl->d + o_live);
+  pl.kp.init_plane = reinterpret_cast<uint4 *>(sl->d + o_init);
+  pl.kp.init_x = reinterpret_cast<int8_t *>(sl->d + o_ix);
+  pl.kp.scratch = reinterpret_cast<uint32_t *>(sl->d + o_pool);
+  pl.kp.ev_lanes = 1u;                           // one trial
+  pl.kp.live_box = sl->dbox;
+  lr->o_st = o_st;
+  lr->o_r = o_r;
+  return plan_launch_impl(&pl, 0, 1, reinterpret_cast<uint64_t *>(sl->d + o_h),
+                          reinterpret_cast<bo_node_state *>(sl->d + o_st), reinterpret_cast<uint32_t *>(sl->d + o_r),
+                          sl->s);
 }
 }  // namespace
 
@@ -1028,14 +1115,22 @@ int bo_consensus_wait(bo_network *net) {
   }
   if (!lr) return BO_OK;
   const uint32_t N = net->N;
+  LiveSlot *sl = lr->slot;
+  // one stream-ordered read-back of flag | states | hist | rounds
+  std::vector<unsigned char> head(lr->o_r + 4u);
+  hipError_t e = hipMemcpyAsync(head.data(), sl->d, head.size(), hipMemcpyDeviceToHost, sl->s);
+  if (e == hipSuccess) e = hipStreamSynchronize(sl->s);
   std::vector<bo_node_state> states(N);
-  uint32_t rounds = 0;
-  hipError_t e = hipStreamSynchronize(lr->s);
-  if (e == hipSuccess) e = hipMemcpy(states.data(), lr->d_st, sizeof(bo_node_state) * N, hipMemcpyDeviceToHost);
-  if (e == hipSuccess) e = hipMemcpy(&rounds, lr->d_r, sizeof(uint32_t), hipMemcpyDeviceToHost);
-  uint32_t flag = 0;
-  int rc = e != hipSuccess ? hip_fail(e, "bo_consensus_wait") : plan_flag_read(lr->pl, lr->s, flag);
-  if (!rc) rc = plan_flag_error(flag);
+  uint32_t rounds = 0, flag = 0;
+  int rc = BO_OK;
+  if (e != hipSuccess) {
+    rc = hip_fail(e, "bo_consensus_wait");
+  } else {
+    std::memcpy(&flag, head.data(), 4u);
+    std::memcpy(states.data(), head.data() + lr->o_st, sizeof(bo_node_state) * N);
+    std::memcpy(&rounds, head.data() + lr->o_r, 4u);
+    rc = plan_flag_error(flag);
+  }
   if (!rc && (rounds & 0x80000000u))
     rc = fail(BO_ERR_INTERNAL, "event-level message pool filled up: the run stopped early");
   {

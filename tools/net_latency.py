@@ -1,9 +1,11 @@
 """Latency of the reference's own usage pattern on the GPU (BASELINE configs[0]
 shape): launchNetwork(N, F, ...) + startConsensus(N) + getNodesState(N) for one
 network, as __test__/tests/benorconsensus.test.ts and src/start.ts drive it.
-Prints one JSON line per N with the median and p90 wall time in ms.
+Prints one JSON line per (N, start) with the median and p90 wall time in ms:
+the default start (resolves at launch, getNodesState waits for the run) and
+the sync one.
 
-    python tools/net_latency.py [--reps 200]
+    python tools/net_latency.py [--reps 200] [--max-n 1024]
 """
 import argparse
 import json
@@ -18,25 +20,30 @@ sys.path.insert(0, os.path.join(ROOT, "ben-or-consensus-algorithm_amd"))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=200)
+    ap.add_argument("--max-n", type=int, default=1024)
     a = ap.parse_args()
     import benor
 
     for N, F in [(5, 1), (10, 4), (10, 5), (100, 33), (1024, 341)]:
+        if N > a.max_n:
+            continue
         faulty = [i < F for i in range(N)]
         init = [(i * 7 + 3) % 2 for i in range(N)]
-        times = []
-        for rep in range(a.reps + 5):
-            t0 = time.perf_counter()
-            benor.launchNetwork(N, F, init, faulty)
-            benor.startConsensus(N, seed=rep)
-            states = benor.getNodesState(N)
-            dt = time.perf_counter() - t0
-            if rep >= 5:
-                times.append(dt * 1e3)
-        times.sort()
-        decided = sum(1 for s in states if s["decided"])
-        print(json.dumps({"N": N, "F": F, "reps": a.reps, "median_ms": times[len(times) // 2],
-                          "p90_ms": times[int(len(times) * 0.9)], "last_decided_nodes": decided}), flush=True)
+        for start, kw in (("default", {}), ("sync", {"sync": True})):
+            times = []
+            reps = a.reps if N < 1024 or start == "sync" else max(5, a.reps // 20)
+            for rep in range(reps + 5):
+                t0 = time.perf_counter()
+                benor.launchNetwork(N, F, init, faulty)
+                benor.startConsensus(N, seed=rep, **kw)
+                states = benor.getNodesState(N)
+                dt = time.perf_counter() - t0
+                if rep >= 5:
+                    times.append(dt * 1e3)
+            times.sort()
+            decided = sum(1 for s in states if s["decided"])
+            print(json.dumps({"N": N, "F": F, "start": start, "reps": reps, "median_ms": times[len(times) // 2],
+                              "p90_ms": times[int(len(times) * 0.9)], "last_decided_nodes": decided}), flush=True)
 
 
 if __name__ == "__main__":
