@@ -189,6 +189,19 @@ __device__ __forceinline__ uint32_t coin_word_v(uint4 b, uint32_t round) {
   return r;
 }
 
+// Random initial values of a network of at most 32 live nodes (one word per
+// trial, bit c = compact node c): word t & 3 of the Philox block
+// ctr = {q_lo, q_hi, 1 << 31, kStreamInit << 24}, q = t >> 2, so four
+// consecutive trials share a block (oracle_random_init, r05).  Networks of
+// more than 32 live nodes take words c >> 5 of the trial's own blocks.
+constexpr uint32_t kInitShared = 1u << 31;
+__device__ __forceinline__ uint4 init_block_small(uint32_t k0, uint32_t k1, uint64_t q) {
+  return philox4x32_10<false>(k0, k1, make_uint4((uint32_t)q, (uint32_t)(q >> 32), kInitShared, kStreamInit << 24));
+}
+__device__ __forceinline__ uint32_t init_word_small(uint32_t k0, uint32_t k1, uint64_t t) {
+  return coin_word_v(init_block_small(k0, k1, t >> 2), (uint32_t)(t & 3u) + 1u);
+}
+
 // Coins of the tied receivers of one group (lanes = compact nodes 64 g + l).
 // The key words are laundered through an empty asm so that Philox's ten round
 // keys are not hoisted out of the round loop into permanently live SGPRs.

@@ -147,9 +147,13 @@ __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
     for (uint32_t c = lane; c < m; c += 64u) {
       const uint32_t i = p.live_ids[c];
       int8_t v;
-      if (p.init_mode == BO_INIT_RANDOM) {      // word c >> 5 of stream 1 (oracle_random_init)
-        const uint4 ir = philox4x32_10<false>(k0, k1, make_uint4(tlo, thi, c >> 7, kStreamInit << 24));
-        v = (int8_t)((coin_word_v(ir, ((c >> 5) & 3u) + 1u) >> (c & 31u)) & 1u);
+      if (p.init_mode == BO_INIT_RANDOM) {      // oracle_random_init: m <= 32 a block per four trials,
+        if (m <= 32u) {                         // else word c >> 5 of the trial's stream 1
+          v = (int8_t)((init_word_small(k0, k1, trial) >> c) & 1u);
+        } else {
+          const uint4 ir = philox4x32_10<false>(k0, k1, make_uint4(tlo, thi, c >> 7, kStreamInit << 24));
+          v = (int8_t)((coin_word_v(ir, ((c >> 5) & 3u) + 1u) >> (c & 31u)) & 1u);
+        }
       } else {
         v = p.init_x[i];
       }

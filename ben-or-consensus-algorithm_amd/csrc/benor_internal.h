@@ -167,8 +167,15 @@ template <int MM>
 hipError_t launch_mfma_small_m(const KParams &p, int grid_blocks, hipStream_t stream);
 constexpr uint32_t small_slots(uint32_t m) { return (32u / m) < 8u ? (32u / m) : 8u; }
 constexpr uint32_t kSmallMaxRound = 3;   // rounds on the matrix cores; a later tie -> the lane path
-// LDS words per wave: round-2 and round-3 lists (2 batches each), lane-path queue (a batch + 64)
-constexpr uint32_t small_wave_words(uint32_t m) { return 5u * 64u * small_slots(m) + 64u; }
+// Shared-init Philox passes of a fresh batch: its 64 S trials (from any start
+// offset mod 4) use at most 16 S + 1 blocks of stream 1, drawn 64 per pass.
+constexpr uint32_t small_init_passes(uint32_t m) { return (16u * small_slots(m) + 1u + 63u) / 64u; }
+// LDS words per wave: round-2 and round-3 lists (2 batches each), the round-3
+// list's carried x words (2 batches), the lane-path queue (a batch + 64), the
+// fresh batch's init blocks (4 words per block)
+constexpr uint32_t small_wave_words(uint32_t m) {
+  return 7u * 64u * small_slots(m) + 64u + 256u * small_init_passes(m);
+}
 constexpr uint64_t kSmallMinTrials = 500000;    // shorter packed-shape launches run on the lane kernel
 bool small_on_lane(const KParams &p);
 

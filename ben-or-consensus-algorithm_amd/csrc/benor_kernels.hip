@@ -175,7 +175,9 @@ __global__ void __launch_bounds__(256) benor_random_kernel(KParams p) {
     if (p.init_mode == BO_INIT_RANDOM) {           // /start (node.ts:167-188)
       const uint32_t nph = (W + 1u) >> 1;
       if (lane < nph) {
-        const uint4 r = philox4x32_10(k0, k1, make_uint4(tlo, thi, lane, kStreamInit << 24));
+        uint4 r;
+        if (m <= 32u) r = make_uint4(init_word_small(k0, k1, trial), 0u, 0u, 0u);   // shared block (m <= 32)
+        else r = philox4x32_10(k0, k1, make_uint4(tlo, thi, lane, kStreamInit << 24));
         const uint32_t w0 = 2u * lane, w1 = w0 + 1u;
         const uint64_t v0 = group_mask(w0, m), v1 = group_mask(w1, m);
         const uint64_t x1a = ((uint64_t)r.y << 32 | r.x) & v0;
@@ -385,10 +387,16 @@ __global__ void __launch_bounds__(256) benor_event_kernel(KParams p) {
       const uint32_t i = p.live_ids[c];
       int8_t v;
       if (p.init_mode == BO_INIT_RANDOM) {
-        if ((c & 127u) == 0u) ir = philox4x32_10<false>(k0, k1, make_uint4(tlo, thi, c >> 7, kStreamInit << 24));
-        const uint32_t j = (c >> 5) & 3u;
-        const uint32_t w = j == 0u ? ir.x : j == 1u ? ir.y : j == 2u ? ir.z : ir.w;
-        v = (int8_t)((w >> (c & 31u)) & 1u);
+        if (m <= 32u) {                              // the shared block of four trials (oracle_random_init)
+          if (c == 0u) ir = init_block_small(k0, k1, trial >> 2);
+          const uint32_t w = coin_word_v(ir, (uint32_t)(trial & 3u) + 1u);
+          v = (int8_t)((w >> c) & 1u);
+        } else {
+          if ((c & 127u) == 0u) ir = philox4x32_10<false>(k0, k1, make_uint4(tlo, thi, c >> 7, kStreamInit << 24));
+          const uint32_t j = (c >> 5) & 3u;
+          const uint32_t w = j == 0u ? ir.x : j == 1u ? ir.y : j == 2u ? ir.z : ir.w;
+          v = (int8_t)((w >> (c & 31u)) & 1u);
+        }
       } else {
         v = p.init_x[i];
       }

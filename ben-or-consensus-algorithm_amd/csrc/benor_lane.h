@@ -23,7 +23,8 @@
 // Trials come from a per-wave queue exactly as in the packed design they
 // replace: the wave's j-th trial is global trial gw + j * waves_total, so any
 // launch split covers each trial id once.  The queue's Philox work -- the
-// random initial values (one or two words) and, for m <= 32, the coin block of
+// random initial values (one word of a block four trials share for m <= 32,
+// two words of the trial's own block above) and, for m <= 32, the coin block of
 // rounds 1-4 (benor_device.h coin_block) -- is drawn 64 trials per pass into
 // an LDS ring; a lane that finishes its trial takes the next queue entry.
 // Coins are needed only after a tied R-phase (all proposals "?", node.ts:63-69,
@@ -112,8 +113,12 @@ __global__ void __launch_bounds__(256) benor_lane_kernel(KParams p) {
           uint32_t kk0 = k0, kk1 = k1;
           asm volatile("" : "+s"(kk0), "+s"(kk1));
           if (random_init) {
-            const uint4 w = philox4x32_10(kk0, kk1, make_uint4((uint32_t)tr, (uint32_t)(tr >> 32), 0u, kStreamInit << 24));
-            iring[j & 127u] = make_uint2(w.x, w.y);
+            if constexpr (kWide) {
+              const uint4 w = philox4x32_10(kk0, kk1, make_uint4((uint32_t)tr, (uint32_t)(tr >> 32), 0u, kStreamInit << 24));
+              iring[j & 127u] = make_uint2(w.x, w.y);
+            } else {                                               // m <= 32: the shared-block word
+              iring[j & 127u] = make_uint2(init_word_small(kk0, kk1, tr), 0u);
+            }
           }
           if (KIND == 0 && !kWide) cring[j & 127u] = coin_block(kk0, kk1, (uint32_t)tr, (uint32_t)(tr >> 32), 0u, 1u);
         }

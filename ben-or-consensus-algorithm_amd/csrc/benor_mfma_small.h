@@ -159,8 +159,7 @@ __device__ void small_lane_path(const uint32_t *keys, uint32_t e, uint32_t fixed
   uint32_t bin;
   if (e >> 31) {
     uint32_t x = fixed1;
-    if (random_init)
-      x = philox4x32_10<false>(k2.x, k2.y, make_uint4((uint32_t)tr, (uint32_t)(tr >> 32), 0u, kStreamInit << 24)).x & LIVE;
+    if (random_init) x = init_word_small(k2.x, k2.y, tr) & LIVE;
     bin = small_lane_trial<MM>(k2.x, k2.y, tr, x, F, k_max, 0u, make_uint4(0u, 0u, 0u, 0u), 0u);
   } else {
     const uint4 cw = coin_block<false>(k2.x, k2.y, (uint32_t)tr, (uint32_t)(tr >> 32), 0u, 1u);
@@ -185,10 +184,14 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
   uint32_t *lhist = reinterpret_cast<uint32_t *>(smem);
   uint32_t *keys = reinterpret_cast<uint32_t *>(smem + p.hist_bytes - kParamBytes);
   // The wave's LDS slice: the round-2 and round-3 lists (2 BATCH each: a list
-  // is drained once it holds a batch, and one batch adds at most BATCH) and
-  // the lane-path queue (drained 64 at a time).
+  // is drained once it holds a batch, and one batch adds at most BATCH), the
+  // round-3 entries' x words (their round-2 coins, carried from the round-2
+  // batch that drew their coin block), the lane-path queue (drained 64 at a
+  // time) and a fresh batch's init blocks.
+  constexpr uint32_t NP = small_init_passes(MM);
   uint32_t *list2 = reinterpret_cast<uint32_t *>(smem + p.hist_bytes) + wv * small_wave_words(MM);
-  uint32_t *list3 = list2 + 2u * BATCH, *lq = list2 + 4u * BATCH;
+  uint32_t *list3 = list2 + 2u * BATCH, *list3w = list2 + 4u * BATCH, *lq = list2 + 6u * BATCH;
+  uint32_t *initw = lq + BATCH + 64u;                     // [NP * 64] uint4 blocks
   for (uint32_t i = threadIdx.x; i < hist_len; i += blockDim.x) lhist[i] = 0u;
   if (threadIdx.x == 0) {
     keys[0] = (uint32_t)p.seed;
@@ -200,7 +203,6 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
 
   const bool random_init = p.init_mode == BO_INIT_RANDOM;
   const uint32_t fixed1 = random_init ? 0u : (p.init_plane[0].z & LIVE);
-  const uint32_t rmask = random_init ? ~0u : 0u;         // round-1 x: the Philox word, or the fixed plane
   const uint32_t F = p.F, k_max = p.k_max;
   const uint32_t R = k_max < kSmallMaxRound ? k_max : kSmallMaxRound;   // last matrix-core round
 
@@ -271,32 +273,75 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
 
     // ---- slot s of this lane takes batch entry 64 s + lane; its x word is
     // the initial values (round 1, node.ts:167-188) or, after r - 1 ties, the
-    // coins of round r - 1 (node.ts:110-111): one Philox block per slot, the S
-    // chains advanced together (philox4x32_10_multi).
+    // coins of round r - 1 (node.ts:110-111).
+    //   round 1: four consecutive trials share a Philox block of stream 1
+    //     (init_word_small): the batch's <= 16 S + 1 blocks are drawn
+    //     lane-parallel (NP per lane, chains advanced together) into LDS, block
+    //     i at words 4i .. 4i + 3, so entry e's word sits at o + e (o = the
+    //     batch's first trial mod 4);
+    //   round 2: the slot's coin block of rounds 1-4 (word 0 = round-1 coins),
+    //     one per slot, the S chains advanced together; word 1 (round-2 coins)
+    //     goes with a trial that ties again to the round-3 list;
+    //   round 3: the carried word, no Philox.
     const uint2 kk = lds_keys(keys);
     const uint64_t tb = lds_u64(keys + 2);
-    uint32_t toff[S];
-    uint4 blk[S];
-    const uint32_t c3 = r == 1u ? (kStreamInit << 24) : (((r - 2u) >> 2) | (kStreamCoin << 24));
-#pragma unroll
-    for (uint32_t s = 0; s < S; ++s) {
-      const uint32_t e = s * 64u + lane;
-      const uint32_t gb = g * BATCH + e;
-      toff[s] = e < n ? (src ? src[e] : gb) : EMPTY;
-      const uint64_t tr = tb + (toff[s] & 0x7FFFFFFFu);
-      blk[s] = make_uint4((uint32_t)tr, (uint32_t)(tr >> 32), 0u, c3);
-    }
-    if (r == 1u) g += waves_total;
-    philox4x32_10_multi<S>(kk.x, kk.y, blk);
-    const uint32_t wsel = r == 1u ? 0u : ((r - 2u) & 3u);        // wave-uniform word of the block
+    uint32_t toff[S], cw1[S];
     uint32_t w = 0u;
+    if (r == 1u) {
+      const uint64_t t0 = tb + (uint64_t)g * BATCH;       // the batch's first trial
+      const uint32_t o = (uint32_t)t0 & 3u;
+      if (random_init) {
+        const uint64_t q0 = t0 >> 2;
+        uint4 blk[NP];
 #pragma unroll
-    for (uint32_t s = 0; s < S; ++s) {
-      uint32_t x = wsel == 0u ? blk[s].x : wsel == 1u ? blk[s].y : wsel == 2u ? blk[s].z : blk[s].w;
-      if (r == 1u) x = bsel(rmask, x, fixed1);
-      uint32_t keep = (toff[s] >> 31) - 1u;               // ~0 unless the slot is EMPTY
-      asm("" : "+v"(keep));                               // a mask, not a select
-      w |= (x & LIVE & keep) << (s * MM);
+        for (uint32_t i = 0; i < NP; ++i) {
+          const uint64_t q = q0 + lane + 64u * i;
+          blk[i] = make_uint4((uint32_t)q, (uint32_t)(q >> 32), kInitShared, kStreamInit << 24);
+        }
+        philox4x32_10_multi<NP>(kk.x, kk.y, blk);
+        uint4 *iw4 = reinterpret_cast<uint4 *>(initw);
+#pragma unroll
+        for (uint32_t i = 0; i < NP; ++i) iw4[lane + 64u * i] = blk[i];
+        asm volatile("" ::: "memory");                    // the reads below after every lane's write (in-order LDS)
+      }
+#pragma unroll
+      for (uint32_t s = 0; s < S; ++s) {
+        const uint32_t e = s * 64u + lane;
+        toff[s] = e < n ? g * BATCH + e : EMPTY;
+        const uint32_t x = random_init ? initw[o + e] : fixed1;
+        uint32_t keep = (toff[s] >> 31) - 1u;             // ~0 unless the slot is EMPTY
+        asm("" : "+v"(keep));                             // a mask, not a select
+        w |= (x & LIVE & keep) << (s * MM);
+      }
+      g += waves_total;
+    } else if (r == 2u) {
+      uint4 blk[S];
+#pragma unroll
+      for (uint32_t s = 0; s < S; ++s) {
+        const uint32_t e = s * 64u + lane;
+        toff[s] = e < n ? src[e] : EMPTY;
+        const uint64_t tr = tb + (toff[s] & 0x7FFFFFFFu);
+        blk[s] = make_uint4((uint32_t)tr, (uint32_t)(tr >> 32), 0u, kStreamCoin << 24);
+      }
+      philox4x32_10_multi<S>(kk.x, kk.y, blk);
+#pragma unroll
+      for (uint32_t s = 0; s < S; ++s) {
+        cw1[s] = blk[s].y;
+        uint32_t keep = (toff[s] >> 31) - 1u;
+        asm("" : "+v"(keep));
+        w |= (blk[s].x & LIVE & keep) << (s * MM);
+      }
+    } else {
+      const uint32_t *srcw = list3w + (src - list3);       // the carried words, same index
+#pragma unroll
+      for (uint32_t s = 0; s < S; ++s) {
+        const uint32_t e = s * 64u + lane;
+        toff[s] = e < n ? src[e] : EMPTY;
+        const uint32_t x = e < n ? srcw[e] : 0u;
+        uint32_t keep = (toff[s] >> 31) - 1u;
+        asm("" : "+v"(keep));
+        w |= (x & LIVE & keep) << (s * MM);
+      }
     }
     // B: +1.0 (0x2) where x = 1, -1.0 (0xA) where x = 0, 0 on unused positions
     const mf_v4i Ez = small_expand(used_mask & ~w);
@@ -356,6 +401,7 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
     const bool last = r >= R;
     uint32_t *dst = last ? lq : (r == 1u ? list2 : list3);
     uint32_t dlen = last ? lql : (r == 1u ? len2 : len3);
+    const bool carry = !last && r == 2u;                  // round-3 entries take their round-2 coins along
     uint32_t c1 = 0u, c0 = 0u, odd_any = 0u;
 #pragma unroll
     for (uint32_t s = 0; s < S; ++s) {
@@ -366,7 +412,11 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
       const uint32_t tie = valid & n1 & n0 & (nq ^ 1u);
       odd_any |= valid & n1 & n0 & nq;
       const uint64_t bt = ballot(tie != 0u);
-      if (tie) dst[dlen + __builtin_amdgcn_mbcnt_hi((uint32_t)(bt >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bt, 0u))] = toff[s];
+      if (tie) {
+        const uint32_t at = dlen + __builtin_amdgcn_mbcnt_hi((uint32_t)(bt >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bt, 0u));
+        dst[at] = toff[s];
+        if (carry) list3w[at] = cw1[s];
+      }
       dlen += (uint32_t)__popcll(bt);
     }
     if (last) lql = dlen;

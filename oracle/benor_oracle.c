@@ -29,9 +29,13 @@
  *       c >> 5, ((r-1) >> 2) | 0<<24}): one block per 32 nodes and 4 rounds;
  *       x = coin, the reference's `Math.random() > 0.5 ? 0 : 1` (node.ts:111)
  *       with P(1) = 1/2.
- *   random initial value of the c-th live node (ascending node id):
- *       bit (c & 31) of word c>>5, word j = philox(ctr {trial_lo, trial_hi,
- *       j>>2, 1<<24})[j & 3].
+ *   random initial value of the c-th live node (ascending node id), m live
+ *       nodes:
+ *       m <= 32 (one word per trial, r05): bit c of word trial & 3 of
+ *       philox(ctr {q_lo, q_hi, 1<<31, 1<<24}), q = trial >> 2 -- four
+ *       consecutive trials share one block;
+ *       m > 32: bit (c & 31) of word c>>5, word j = philox(ctr {trial_lo,
+ *       trial_hi, j>>2, 1<<24})[j & 3].
  *   halting: the network stops after the round in which every live node has
  *       decided (the reference's all-decided auto-stop, node.ts:116-145,
  *       without its F>0 `decided:null` defect), else after k_max rounds.
@@ -90,8 +94,15 @@ int oracle_coin(uint64_t seed, uint64_t trial, uint32_t c, uint32_t round) {
     return (int)((w >> (c & 31u)) & 1u);
 }
 
-/* Random initial value (0/1) of the c-th live node. */
-int oracle_random_init(uint64_t seed, uint64_t trial, uint32_t c) {
+/* Random initial value (0/1) of the c-th live node of a network of m live
+ * nodes.  A network of at most 32 live nodes needs one 32-bit word per trial,
+ * so four consecutive trials share a Philox block (ctr[2] bit 31 marks the
+ * shared form); larger networks take words c >> 5 of their own blocks. */
+int oracle_random_init(uint64_t seed, uint64_t trial, uint32_t c, uint32_t m) {
+    if (m <= 32u) {
+        uint32_t w = orc_philox_word(seed, trial >> 2, 1u << 31, ORC_STREAM_INIT << 24, (int)(trial & 3u));
+        return (int)((w >> c) & 1u);
+    }
     uint32_t j = c >> 5;
     uint32_t w = orc_philox_word(seed, trial, j >> 2, ORC_STREAM_INIT << 24, (int)(j & 3));
     return (int)((w >> (c & 31)) & 1u);
@@ -445,7 +456,7 @@ static void run_one(const orc_trials_cfg *cfg, const uint32_t *live_ids, uint32_
     /* initial planes (compact live order) */
     for (uint32_t w = 0; w < W; ++w) { x0[w] = x1[w] = 0; dec[w] = 0; }
     for (uint32_t c = 0; c < m; ++c) {
-        int v = cfg->init_mode == 1 ? cfg->init[live_ids[c]] : oracle_random_init(cfg->seed, trial, c);
+        int v = cfg->init_mode == 1 ? cfg->init[live_ids[c]] : oracle_random_init(cfg->seed, trial, c, m);
         if (v == 0) x0[c >> 6] |= 1ull << (c & 63);
         else if (v == 1) x1[c >> 6] |= 1ull << (c & 63);
         if (node_out) node_out[live_ids[c]].x = (int8_t)v;
@@ -663,7 +674,7 @@ static uint32_t event_trial(const orc_event_cfg *cfg, uint64_t trial, orc_node_s
     }
     for (uint32_t c = 0; c < m; ++c) {
         const uint32_t i = live_ids[c];
-        st[i].x = (int8_t)(cfg->init_mode == 1 ? cfg->init[i] : oracle_random_init(cfg->seed, trial, c));
+        st[i].x = (int8_t)(cfg->init_mode == 1 ? cfg->init[i] : oracle_random_init(cfg->seed, trial, c, m));
     }
     /* crash schedule */
     uint32_t *crash_at = (uint32_t *)malloc(sizeof(uint32_t) * N);

@@ -47,7 +47,7 @@ def lib():
         L.oracle_philox4x32_10.argtypes = [ctypes.POINTER(ctypes.c_uint32)] * 3
         L.oracle_coin.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32]
         L.oracle_coin.restype = ctypes.c_int
-        L.oracle_random_init.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32]
+        L.oracle_random_init.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32]
         L.oracle_random_init.restype = ctypes.c_int
         L.oracle_validate.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                                       ctypes.POINTER(ctypes.c_uint8)]
@@ -87,8 +87,10 @@ def coin(seed: int, trial: int, c: int, rnd: int) -> int:
     return lib().oracle_coin(seed, trial, c, rnd)
 
 
-def random_init(seed: int, trial: int, c: int) -> int:
-    return lib().oracle_random_init(seed, trial, c)
+def random_init(seed: int, trial: int, c: int, m: int) -> int:
+    """Random initial value of the c-th live node of an m-live-node network
+    (m <= 32: four consecutive trials share one Philox block)."""
+    return lib().oracle_random_init(seed, trial, c, m)
 
 
 VAL_CODE = {0: 0, 1: 1, "?": 2}

@@ -45,6 +45,28 @@ def test_coin_definition():
     assert abs(sum(bits) / len(bits) - 0.5) < 0.01
 
 
+def test_random_init_definition():
+    """Random initial values: a network of m <= 32 live
+    nodes takes bit c of word t & 3 of Philox(ctr {t >> 2, 1 << 31, 1 << 24}),
+    so trials 4q .. 4q + 3 are the four words of one block; larger networks
+    take bit c & 31 of word c >> 5 of the trial's own blocks
+    (ctr {t, (c >> 5) >> 2, 1 << 24})."""
+    key = [0x2468ACE1, 0x13579BDF]
+    seed = key[0] | key[1] << 32
+    for t in (0, 1, 2, 3, 4, 7, (1 << 33) + 5):
+        q = t >> 2
+        blk = oracle.philox4x32_10(key, [q & 0xFFFFFFFF, q >> 32, 1 << 31, 1 << 24])
+        for m in (1, 6, 32):
+            for c in range(m):
+                assert oracle.random_init(seed, t, c, m) == (blk[t & 3] >> c) & 1
+        for m in (33, 200):
+            for c in (0, 31, 32, m - 1):
+                b = oracle.philox4x32_10(key, [t & 0xFFFFFFFF, t >> 32, (c >> 5) >> 2, 1 << 24])
+                assert oracle.random_init(seed, t, c, m) == (b[(c >> 5) & 3] >> (c & 31)) & 1
+    bits = [oracle.random_init(11, t, c, 6) for t in range(4000) for c in range(6)]
+    assert abs(sum(bits) / len(bits) - 0.5) < 0.01
+
+
 def test_launch_errors(reference_cases):
     for e in reference_cases["launch_errors"]:
         code = oracle.validate(e["N"], e["F"], e["init"], e["faulty"])
