@@ -102,7 +102,7 @@ __device__ __forceinline__ uint32_t small_pack(const mf_v16f &acc, int base) { r
 // cw of round group cg (0: none).  Returns the histogram bin; bit 31 flags an
 // agreement violation.
 template <int MM>
-__device__ uint32_t small_lane_trial(uint32_t k0, uint32_t k1, uint64_t tr, uint32_t x1, uint32_t F, uint32_t k_max,
+__device__ __forceinline__ uint32_t small_lane_trial(uint32_t k0, uint32_t k1, uint64_t tr, uint32_t x1, uint32_t F, uint32_t k_max,
                                      uint32_t r0, uint4 cw, uint32_t cg) {
   constexpr uint32_t live = MM == 32 ? ~0u : ((1u << MM) - 1u);
   const uint32_t tlo = (uint32_t)tr, thi = (uint32_t)(tr >> 32);
@@ -151,7 +151,7 @@ __device__ uint32_t small_lane_trial(uint32_t k0, uint32_t k1, uint64_t tr, uint
 // continues it from there (coin block of rounds 1-4 in hand, R <= 3); an
 // entry with bit 31 set (receivers not unanimous) starts over from round 1.
 template <int MM>
-__device__ void small_lane_path(const uint32_t *keys, uint32_t e, uint32_t fixed1, bool random_init, uint32_t F,
+__device__ __forceinline__ void small_lane_path(const uint32_t *keys, uint32_t e, uint32_t fixed1, bool random_init, uint32_t F,
                                 uint32_t k_max, uint32_t R, uint32_t *lhist, uint32_t hist_len) {
   constexpr uint32_t LIVE = MM == 32 ? ~0u : ((1u << MM) - 1u);
   const uint64_t tr = lds_u64(keys + 2) + (e & 0x7FFFFFFFu);
