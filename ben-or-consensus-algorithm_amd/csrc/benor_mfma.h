@@ -95,7 +95,8 @@ __device__ __forceinline__ uint32_t pack_signs8(const mf_v16f &acc, int base) {
 // the MFMA's A scale and the threshold sits half a vote from it), so each
 // nibble is exactly +6.0 (0x7, proposal 1) or -6.0 (0xF, proposal 0).
 __device__ __forceinline__ uint32_t pack_fp4_8(const mf_v16f &acc, int base) {
-  uint32_t r = 0u;
+  uint32_t r;
+  asm volatile("" : "=v"(r));   // no initial value: the four conversions write every byte (no v_mov 0)
   r = __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(r, acc[base + 0], acc[base + 1], 1.0f, 0);
   r = __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(r, acc[base + 2], acc[base + 3], 1.0f, 1);
   r = __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(r, acc[base + 4], acc[base + 5], 1.0f, 2);
@@ -144,6 +145,10 @@ __global__ void __launch_bounds__(256) benor_mfma_kernel(KParams p) {
   constexpr int NB = (W + 1) / 2;              // Philox init blocks per trial (128 senders each)
   constexpr int NJ = (NB + 1) / 2;             // blocks per lane: half h draws blocks h, h + 2, ...
   constexpr bool SURE = KIND == 0;
+  // (r05 measured the SURE W <= 4 proposal packing and P-phase fold through
+  // v_cvt_scalef32_pk_fp4_f32 instead of v_perm sign bytes and the f32 sign
+  // fold: 10 % fewer VALU, 8-12 % slower at configs[2] -- the conversion is
+  // the slower instruction; profiles/r05-h_mfma_fp4_fold_ab.jsonl.)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t lane = threadIdx.x & 63u, h = lane >> 5;
   const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
