@@ -10,6 +10,11 @@ median and minimum ms per launch and the variant's median / first variant's.
 
     python tools/ab_inproc.py --variants "coop=BENOR_BIG_FORM:coop;wave=BENOR_BIG_FORM:wave" \
         --shapes "4096,1365,400000;4096,0,100000" [--rounds 7] [--reps 3]
+
+A shape may carry a fourth field f < F (the first f nodes crashed, the rest of
+F the random-delivery slack: BO_MODE_RANDOM_DELIVERY).  Every line also reports
+the live node-rounds per second its launches represent (bench.py node_rounds),
+so variants that change the outcome (a diagnostic cap) compare per unit of work.
 """
 import argparse
 import json
@@ -36,17 +41,24 @@ def parse_variants(spec):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--variants", required=True, help="'name=VAR:val,VAR:val;name2=...' ('name=' = no variables)")
-    ap.add_argument("--shapes", required=True, help="'N,F,trials;...' (lockstep, the first F nodes crashed)")
+    ap.add_argument("--shapes", required=True,
+                    help="'N,F,trials[,f];...' (the first f nodes crashed, f = F by default)")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--reps", type=int, default=3)
     a = ap.parse_args()
     variants = parse_variants(a.variants)
-    shapes = [tuple(int(x) for x in s.split(",")) for s in a.shapes.split(";")]
+    shapes = []
+    for sp in a.shapes.split(";"):
+        v = [int(x) for x in sp.split(",")]
+        shapes.append((v[0], v[1], v[2], v[3] if len(v) > 3 else v[1]))
     knobs = sorted({k for _, env in variants for k in env})
 
+    import numpy as np
     import torch
 
     import benor
+    sys.path.insert(0, ROOT)
+    from bench import node_rounds
 
     torch.cuda.set_device(0)
     st = torch.cuda.current_stream()
@@ -56,9 +68,10 @@ def main():
             os.environ.pop(k, None)
         os.environ.update(env)
 
-    times = {}
-    for N, F, T in shapes:
-        plan = benor.TrialsPlan(N, F, [i < F for i in range(N)], seed=0x5EED + N, k_max=32)
+    times, work = {}, {}
+    for N, F, T, f in shapes:
+        mode = benor.BO_MODE_RANDOM_DELIVERY if f < F else benor.BO_MODE_LOCKSTEP
+        plan = benor.TrialsPlan(N, F, [i < f for i in range(N)], seed=0x5EED + N, k_max=32, mode=mode)
         h = torch.zeros(plan.hist_len, dtype=torch.int64, device="cuda")
         for _, env in variants:                       # warm-up per variant (allocations, code load)
             set_env(env)
@@ -69,6 +82,7 @@ def main():
             order = variants[rnd % len(variants):] + variants[:rnd % len(variants)]
             for name, env in order:
                 set_env(env)
+                h.zero_()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(st)
                 for _ in range(a.reps):
@@ -76,14 +90,18 @@ def main():
                     nxt += T
                 e1.record(st)
                 torch.cuda.synchronize()
-                times.setdefault((N, F, T, name), []).append(e0.elapsed_time(e1) / a.reps)
+                ms = e0.elapsed_time(e1) / a.reps
+                times.setdefault((N, F, T, f, name), []).append(ms)
+                nr, _ = node_rounds(h.cpu().numpy().astype(np.uint64), N - f, 32)
+                work.setdefault((N, F, T, f, name), []).append(nr / a.reps / (ms * 1e-3))
     set_env({})
-    for N, F, T in shapes:
-        base = statistics.median(times[(N, F, T, variants[0][0])])
+    for N, F, T, f in shapes:
+        base = statistics.median(times[(N, F, T, f, variants[0][0])])
         for name, _ in variants:
-            t = times[(N, F, T, name)]
-            print(json.dumps({"N": N, "F": F, "trials": T, "variant": name, "median_ms": statistics.median(t),
+            t = times[(N, F, T, f, name)]
+            print(json.dumps({"N": N, "F": F, "f": f, "trials": T, "variant": name, "median_ms": statistics.median(t),
                               "min_ms": min(t), "rounds": len(t), "median_vs_first": statistics.median(t) / base,
+                              "node_rounds_per_s": statistics.median(work[(N, F, T, f, name)]),
                               "kernel_version": benor.kernel_version()}), flush=True)
 
 
