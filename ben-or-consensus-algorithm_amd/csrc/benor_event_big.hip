@@ -13,7 +13,10 @@
 //   * the message pool (uniform pick, swap-remove) lives in the workgroup's
 //     HBM scratch slice: 4N^2 + 64 u32 messages, to | ph << 12 | x << 13 |
 //     (k & 3) << 15 (k is recovered from the completion round `cur`, as in
-//     benor_event_kernel: a message to a running node is for [cur, cur + 2]);
+//     benor_event_kernel: a message to a running node is for [cur, cur + 2]).
+//     A pool of at most kEventBigLdsPool bytes (N <= 78: the reference's own
+//     network sizes, live runs) lives in LDS instead (LP), so a batch's pool
+//     loads are LDS reads rather than L2 round trips;
 //   * per-node state lives in LDS: inbox counters {c0, c1, len} per phase
 //     (13 bits each, bit 63 = killed), x, k, the compact index for coins, and
 //     node bitsets (killed, decided, completion of rounds cur .. cur + 3).
@@ -94,6 +97,7 @@ struct BigState {
 
 }  // namespace
 
+template <bool LP>
 __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t lane = threadIdx.x;
@@ -119,7 +123,9 @@ __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
   const uint64_t allw = lane < NWd ? (N >= 64u * (lane + 1u) ? ~0ull : (1ull << (N - 64u * lane)) - 1ull) : 0ull;
   const uint64_t wmask = NWd >= 64u ? ~0ull : ((1ull << NWd) - 1ull);   // lanes holding a bitset word
   const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
-  uint32_t *pool = p.scratch + (uint64_t)blockIdx.x * p.ev_stride;
+  uint32_t *pool;
+  if constexpr (LP) pool = reinterpret_cast<uint32_t *>(S.rstops + p.ev_rstops);   // after the LDS state
+  else pool = p.scratch + (uint64_t)blockIdx.x * p.ev_stride;
   const uint32_t cap = p.ev_cap;
 
   // a | b == all, over the bitset words (one per lane)
@@ -289,8 +295,13 @@ __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
         if (halted) break;
       }
       if (len == 0u) { halted = 3; break; }
-      // ---- a batch of speculative events e .. e + B - 1
+      // ---- a batch of speculative events e .. e + B - 1.  A small pool (a small
+      // network) has a trigger every few deliveries and picks that collide, so
+      // its batches are shorter: B <= max(8, len / 8) keeps the collision scan
+      // and the replay up to a trigger short (any B gives the same result).
+      const uint32_t bcap = len >> 3 > 8u ? len >> 3 : 8u;
       uint64_t B = len < 64u ? len : 64u;
+      if (B > bcap) B = bcap;
       if (next_key != ~0ull) {
         const uint64_t until = (next_key >> 12) - e;
         if (until < B) B = until;
@@ -327,7 +338,9 @@ __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
       pf_e = ~0ull;
       {
         const uint32_t len2 = len - (uint32_t)B;
+        const uint32_t bcap2 = len2 >> 3 > 8u ? len2 >> 3 : 8u;   // the same batch rule as above
         uint64_t B2 = len2 < 64u ? len2 : 64u;
+        if (B2 > bcap2) B2 = bcap2;
         bool ok = len2 > 0u;
         if (next_key != ~0ull) {
           const uint64_t until2 = (next_key >> 12) - (e + B);
@@ -533,21 +546,29 @@ __global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
   flush_hist(lhist, p);
 }
 
+bool event_big_lds_pool(const KParams &p) { return (uint64_t)p.ev_cap * 4u <= kEventBigLdsPool; }
+
 uint32_t event_big_lds_bytes(const KParams &p) {
   const uint32_t N = p.N;
   return p.hist_bytes + 16u * N + 8u * 64u * 6u + 2u * ((N + 3u) & ~3u) * 2u + ((N + 15u) & ~15u) + 2u * 2048u * 4u +
-         8u * 64u + 8u * p.ev_rstops;   // random /stop schedule: Floyd set, keys
+         8u * 64u + 8u * p.ev_rstops +   // random /stop schedule: Floyd set, keys
+         (event_big_lds_pool(p) ? 4u * p.ev_cap : 0u);   // the message pool, when it fits
 }
 
-hipError_t launch_event_big(const KParams &p, int grid, hipStream_t s) {
+template <bool LP>
+static hipError_t launch_event_big_lp(const KParams &p, int grid, hipStream_t s) {
   const uint32_t lds = event_big_lds_bytes(p);
   if (lds > 64u * 1024u) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&benor_event_big_kernel),
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&benor_event_big_kernel<LP>),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(benor_event_big_kernel, dim3(grid), dim3(64), lds, s, p);
+  hipLaunchKernelGGL(benor_event_big_kernel<LP>, dim3(grid), dim3(64), lds, s, p);
   return hipGetLastError();
+}
+
+hipError_t launch_event_big(const KParams &p, int grid, hipStream_t s) {
+  return event_big_lds_pool(p) ? launch_event_big_lp<true>(p, grid, s) : launch_event_big_lp<false>(p, grid, s);
 }
 
 }  // namespace benor

@@ -115,6 +115,12 @@ struct KParams {
   // diagnostics (BENOR_TIMELINE=<file>, packed matrix-core kernel): per wave,
   // kTimelineWords u64 -- wall-clock stamps of its phases and its batch counts
   unsigned long long *timeline;
+  // packed matrix-core kernel (variant 8): workgroups [0, small_pwgs) run the
+  // batches of trials [0, small_rbeg); each workgroup after them runs 256
+  // trials of [small_rbeg, trial_count) on the lane path, one per lane.
+  // small_pwgs = 0: every workgroup runs batches.  Set per launch by
+  // launch_lockstep (benor_kernels.hip).
+  uint32_t small_pwgs, small_rbeg;
 };
 
 constexpr uint32_t kTimelineWords = 12;
@@ -149,6 +155,10 @@ uint32_t random_bern_rows(uint32_t m, uint32_t b);
 hipError_t launch_random_bern(const KParams &p, int grid_blocks, hipStream_t stream);
 
 // Event level for kMaxEventN < N <= BO_MAX_N (benor_event_big.hip): one wave per trial.
+// The wave-per-trial event kernel keeps its message pool in LDS when it is at
+// most this many bytes (4N^2 + 64 u32: N <= 78).
+constexpr uint64_t kEventBigLdsPool = 96u * 1024u;
+bool event_big_lds_pool(const KParams &p);
 uint32_t event_big_lds_bytes(const KParams &p);
 hipError_t launch_event_big(const KParams &p, int grid_blocks, hipStream_t stream);
 
