@@ -115,12 +115,6 @@ struct KParams {
   // diagnostics (BENOR_TIMELINE=<file>, packed matrix-core kernel): per wave,
   // kTimelineWords u64 -- wall-clock stamps of its phases and its batch counts
   unsigned long long *timeline;
-  // packed matrix-core kernel (variant 8): workgroups [0, small_pwgs) run the
-  // batches of trials [0, small_rbeg); each workgroup after them runs 256
-  // trials of [small_rbeg, trial_count) on the lane path, one per lane.
-  // small_pwgs = 0: every workgroup runs batches.  Set per launch by
-  // launch_lockstep (benor_kernels.hip).
-  uint32_t small_pwgs, small_rbeg;
 };
 
 constexpr uint32_t kTimelineWords = 12;

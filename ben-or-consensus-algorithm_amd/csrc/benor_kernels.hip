@@ -760,26 +760,8 @@ hipError_t launch_lockstep(const KParams &p, int grid, hipStream_t s) {
   }
   if (p.variant == 5) return launch_event_big(p, grid, s);
   if (p.variant == 6) return dispatch_lane(p, grid, s, std::make_integer_sequence<int, (int)kMaxLaneM>{});
-  if (p.variant == 8 && !small_on_lane(p)) {
-    // Fresh batches go out in strides of grid * kWavesPerBlock waves.  A last,
-    // short stride would leave the waves that get one of its batches a whole
-    // batch (and its round lists) behind the rest -- at 10^6 trials and m = 6,
-    // 53 of 1024 waves, ~2.3 us.  When it holds at most 64 trials per wave, its
-    // trials run instead on extra workgroups appended to the grid, one trial per
-    // lane on the lane path, beside the batch waves (which wait on their own
-    // dependency chains at one wave per SIMD).
-    KParams q = p;
-    q.small_pwgs = q.small_rbeg = 0u;
-    int g = grid;
-    const uint64_t batch = 64u * small_slots(p.m), waves = (uint64_t)grid * kWavesPerBlock;
-    const uint64_t gfull = p.trial_count / batch / waves * waves, rbeg = gfull * batch, rem = p.trial_count - rbeg;
-    if (gfull != 0u && rem != 0u && rem <= 64u * waves) {
-      q.small_pwgs = (uint32_t)grid;
-      q.small_rbeg = (uint32_t)rbeg;
-      g = grid + (int)((rem + 64u * kWavesPerBlock - 1u) / (64u * kWavesPerBlock));
-    }
-    return dispatch_mfma_small(q, g, s, std::make_integer_sequence<int, (int)kMaxSmallMfmaM - 1>{});   // m = 2..32
-  }
+  if (p.variant == 8 && !small_on_lane(p))
+    return dispatch_mfma_small(p, grid, s, std::make_integer_sequence<int, (int)kMaxSmallMfmaM - 1>{});   // m = 2..32
   if (p.variant == 8) {                      // state launch or short launch of a packed shape: the lane kernel
     KParams q = p;
     q.variant = p.base_variant;

@@ -138,21 +138,21 @@ __device__ __forceinline__ mf_v4i expand_votes(uint32_t w) {
                 (int)((w >> 2) & 0x22222222u)};
 }
 
-template <int W, bool HALF, int KIND, bool EQB>
+template <int W, bool HALF, int KIND>
 __global__ void __launch_bounds__(256) benor_mfma_kernel(KParams p) {
   constexpr int MT = 2 * W - (HALF ? 1 : 0);   // 32-receiver tiles (HALF: the last chunk holds <= 32 senders)
   constexpr int KP = (MT + 1) / 2;             // P-phase K chunks: two tiles' results each
   constexpr int NB = (W + 1) / 2;              // Philox init blocks per trial (128 senders each)
   constexpr int NJ = (NB + 1) / 2;             // blocks per lane: half h draws blocks h, h + 2, ...
   constexpr bool SURE = KIND == 0;
-  // EQB (KIND 0 only): the R- and P-phase thresholds coincide, (M1 >> 1) = F --
-  // N = 3F + 1 with no "?" input, the headline and configs[2] -- so both phases
-  // start from one bias accumulator: 16 VGPRs fewer, one more wave per SIMD.
-  static_assert(!EQB || SURE, "EQB is a KIND 0 form");
   // (r05 measured the SURE W <= 4 proposal packing and P-phase fold through
   // v_cvt_scalef32_pk_fp4_f32 instead of v_perm sign bytes and the f32 sign
   // fold: 10 % fewer VALU, 8-12 % slower at configs[2] -- the conversion is
-  // the slower instruction; profiles/r05-h_mfma_fp4_fold_ab.jsonl.)
+  // the slower instruction; profiles/r05-h_mfma_fp4_fold_ab.jsonl.  And one
+  // bias accumulator for both phases where they coincide (N = 3F + 1: 16 VGPRs
+  // fewer, 5 waves per SIMD at W = 3): configs[2] and the headline unchanged
+  // within 1 %, with or without a grid sized to the resident waves (that one
+  // 2-5 % slower); profiles/r05-k_eqb_resident_grid_ab.jsonl, r05-l_mfma_eqb_ab.jsonl.)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t lane = threadIdx.x & 63u, h = lane >> 5;
   const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -355,7 +355,7 @@ __global__ void __launch_bounds__(256) benor_mfma_kernel(KParams p) {
         for (int i = 0; i <= MT; ++i) {
           if (i < MT) {
             asm volatile("" : "+v"(ones));
-            mf_v16f acc = mfma_count(ones, pb[0], EQB ? cr : cp);
+            mf_v16f acc = mfma_count(ones, pb[0], cp);
 #pragma unroll
             for (int c = 1; c < KP; ++c) acc = mfma_count(ones, pb[c], acc);
             pacc[i & 1] = acc;
@@ -382,7 +382,7 @@ __global__ void __launch_bounds__(256) benor_mfma_kernel(KParams p) {
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
         asm volatile("" : "+v"(ones));
-        mf_v16f acc = mfma_count(ones, pb[0], EQB ? cr : cp);
+        mf_v16f acc = mfma_count(ones, pb[0], cp);
 #pragma unroll
         for (int c = 1; c < KP; ++c) acc = mfma_count(ones, pb[c], acc);
         // Padded receiver rows of the last tile need no mask here: A is all
@@ -485,47 +485,19 @@ __global__ void __launch_bounds__(256) benor_mfma_kernel(KParams p) {
   flush_hist(lhist, p);
 }
 
-// KIND 0 launches keep no per-wave state beyond their grid-stride loop, so
-// the grid is the resident capacity: workgroups per CU from the kernel's own
-// register occupancy (lockstep_grid assumes 32 waves per CU), so that no
-// second, partial wave round trails the first.
-// (Registers bound these kernels, not their ~1 KB of LDS, so the first
-// launch's answer holds for every k_max; one process drives one device.)
-template <typename K>
-static inline int resident_grid(K kernel, const KParams &p, int grid) {
-  static const int cap = [&] {
-    int nb = 0, dev = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, 64 * kWavesPerBlock, p.hist_bytes) != hipSuccess) nb = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    return nb * cus;
-  }();
-  return cap > 0 && grid > cap ? cap : grid;
-}
-
-template <int W, int KIND, bool EQB = false>
+template <int W, int KIND>
 static inline void launch_mfma_kind(const KParams &p, int grid, hipStream_t s) {
-  if (p.m <= 64u * (uint32_t)(W - 1) + 32u) {
-    auto k = benor_mfma_kernel<W, true, KIND, EQB>;
-    if (KIND == 0) grid = resident_grid(k, p, grid);
-    hipLaunchKernelGGL(k, dim3(grid), dim3(64 * kWavesPerBlock), p.hist_bytes, s, p);
-  } else {
-    auto k = benor_mfma_kernel<W, false, KIND, EQB>;
-    if (KIND == 0) grid = resident_grid(k, p, grid);
-    hipLaunchKernelGGL(k, dim3(grid), dim3(64 * kWavesPerBlock), p.hist_bytes, s, p);
-  }
+  if (p.m <= 64u * (uint32_t)(W - 1) + 32u)
+    hipLaunchKernelGGL((benor_mfma_kernel<W, true, KIND>), dim3(grid), dim3(64 * kWavesPerBlock), p.hist_bytes, s, p);
+  else
+    hipLaunchKernelGGL((benor_mfma_kernel<W, false, KIND>), dim3(grid), dim3(64 * kWavesPerBlock), p.hist_bytes, s, p);
 }
 
 template <int W>
 hipError_t launch_mfma(const KParams &p, int grid, hipStream_t s) {
-  if (p.G == 0u) {
-    if (((p.m - p.init_q) >> 1) == p.F) launch_mfma_kind<W, 0, true>(p, grid, s);   // one bias for both phases
-    else launch_mfma_kind<W, 0>(p, grid, s);
-  } else if (p.G == 1u) {
-    launch_mfma_kind<W, 1>(p, grid, s);
-  } else {
-    launch_mfma_kind<W, 2>(p, grid, s);
-  }
+  if (p.G == 0u) launch_mfma_kind<W, 0>(p, grid, s);
+  else if (p.G == 1u) launch_mfma_kind<W, 1>(p, grid, s);
+  else launch_mfma_kind<W, 2>(p, grid, s);
   return hipGetLastError();
 }
 

@@ -53,8 +53,6 @@
 // from there with the lane kernel's per-lane round logic (benor_lane.h), 64
 // queued trials at a time; one whose receivers are not unanimous (impossible
 // in lockstep) is re-run from round 1 the same way.
-// A short last stride of fresh batches (at most 64 trials per batch wave) runs
-// on extra lane-path workgroups appended to the grid instead (KParams::small_pwgs).
 #pragma once
 
 #include "benor_lane.h"
@@ -207,16 +205,6 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
   const uint32_t fixed1 = random_init ? 0u : (p.init_plane[0].z & LIVE);
   const uint32_t F = p.F, k_max = p.k_max;
   const uint32_t R = k_max < kSmallMaxRound ? k_max : kSmallMaxRound;   // last matrix-core round
-  const uint32_t pwgs = p.small_pwgs ? p.small_pwgs : gridDim.x;        // batch workgroups
-  if (blockIdx.x >= pwgs) {
-    // a lane-path workgroup: the short last stride's trials, one per lane,
-    // from round 1 (launch_lockstep)
-    const uint32_t off = p.small_rbeg + ((blockIdx.x - pwgs) * kWavesPerBlock + wv) * 64u + lane;
-    if (off < trial_count) small_lane_path<MM>(keys, off | 0x80000000u, fixed1, random_init, F, k_max, R, lhist, hist_len);
-    __syncthreads();
-    flush_hist(lhist, p);
-    return;
-  }
 
   // Block-diagonal A of the two tiles (see the header): lane (row rho, K half hk).
   mf_v4i A0, A1;
@@ -250,11 +238,9 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
 #pragma unroll
   for (int j = 0; j < 16; ++j) zero[j] = 0.0f;
 
-  const uint32_t waves_total = pwgs * kWavesPerBlock;
+  const uint32_t waves_total = gridDim.x * kWavesPerBlock;
   const uint32_t wave_id = blockIdx.x * kWavesPerBlock + wv;
-  // fresh batches: every batch of the launch, or those before the lane-path
-  // workgroups' trials (small_rbeg, a multiple of BATCH)
-  const uint32_t ngroups = p.small_pwgs ? p.small_rbeg / BATCH : (trial_count + BATCH - 1u) / BATCH;
+  const uint32_t ngroups = (trial_count + BATCH - 1u) / BATCH;
   uint32_t g = wave_id, len2 = 0u, len3 = 0u, lql = 0u;          // wave-uniform
   uint32_t h0[3] = {0u, 0u, 0u}, h1[3] = {0u, 0u, 0u};             // halts with 0 / 1 in rounds 1..3 (wave totals)
   // diagnostics: [0] start, [1] fresh batches exhausted, [2] lists drained,

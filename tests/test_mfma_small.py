@@ -137,17 +137,17 @@ def test_mfma_small_random_fault_placement():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("N,F,T,k_max", [
-    (10, 4, 1_000_000, 16),               # configs[1]: 3 full strides of 1024 waves + 16 960 trials
-    (10, 4, 3 * 1024 * 320 + 64 * 1024, 16),   # the largest short stride: 64 per wave
-    (10, 4, 3 * 1024 * 320 + 64 * 1024 + 1, 16),   # one more: a fourth fresh stride instead
+    (10, 4, 1_000_000, 16),               # configs[1]: 3 full strides of 1024 waves + 53 batches
+    (10, 4, 3 * 1024 * 320 + 64 * 1024, 16),
+    (10, 4, 3 * 1024 * 320 + 64 * 1024 + 1, 16),
     (32, 0, 2 * 1024 * 64 + 1_000, 4),   # S = 1
     (20, 4, 1024 * 128 + 4_097, 2),      # S = 2, k_max below the matrix-core rounds
     (9, 4, 1024 * 384 + 77, 16),         # m = 5, F = 4 (S = 6)
 ])
-def test_mfma_small_short_stride_lane_path_matches_oracle(N, F, T, k_max):
-    """A last fresh stride of at most 64 trials per wave runs on the lane path,
-    spread over every wave, as round-1 entries (benor_mfma_small.h): launches
-    of >= 1024 batches on a 256-CU MI355X, their histogram against the oracle."""
+def test_mfma_small_full_launch_matches_oracle(N, F, T, k_max):
+    """Launches of >= 1024 batches (the full grid on a 256-CU MI355X, several
+    fresh strides per wave and a short last one), their histogram against the
+    oracle itself rather than the lane kernel."""
     seed = 0x5151 + 97 * N + T
     p = plan(N, F, seed=seed, k_max=k_max)
     assert p.kernel == benor.BO_KERNEL_MFMA_SMALL
