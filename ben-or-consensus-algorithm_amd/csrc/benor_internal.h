@@ -122,7 +122,8 @@ constexpr uint32_t kTimelineWords = 12;
 
 constexpr uint32_t kLiveReq = 2;                 // live mailbox: request bitset words (BO_MAX_N / 32)
 constexpr uint32_t kLiveEv = kLiveReq + 128;     // live mailbox: per-node stop delivery counts
-constexpr uint64_t kLivePollTicks = 1000;        // wall-clock ticks (100 MHz) between mailbox polls
+constexpr uint64_t kLivePollTicks = 1000;        // wall-clock ticks (100 MHz) between wave 0's own mailbox polls
+constexpr uint32_t kEvMailboxWords = 4u + 128u;  // the event kernel's LDS mirror of it: seq, done, request bits, pad
 
 constexpr uint32_t kMfmaContRounds = 3;       // matrix-core passes up to round 3, then the popcount kernel
 // The deferral buffer's 64-word length block: pass r's list length at 16 (r - 1).

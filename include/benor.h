@@ -123,7 +123,7 @@ int bo_consensus_start_sched(bo_network *net, uint64_t seed, uint32_t k_max,
  * while it runs land in it (node.ts:191-194, :45).  Launches the event-level
  * kernel (seeded delivery order, trial 0 of `seed`, any N <= BO_MAX_N) on its
  * own HIP stream and returns.  While it runs, bo_node_stop / bo_consensus_stop
- * also post to a host-mapped mailbox the kernel polls (every ~10 us): a
+ * also post to a host-mapped mailbox the kernel polls (every 2-10 us): a
  * request is applied before the next delivery, and that delivery count is
  * recorded (bo_live_stop_events).  bo_get_state / bo_status answer from the
  * pre-run states (killed flags include the posted stops) until
