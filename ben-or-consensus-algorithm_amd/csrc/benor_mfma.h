@@ -152,7 +152,10 @@ __global__ void __launch_bounds__(256) benor_mfma_kernel(KParams p) {
   // bias accumulator for both phases where they coincide (N = 3F + 1: 16 VGPRs
   // fewer, 5 waves per SIMD at W = 3): configs[2] and the headline unchanged
   // within 1 %, with or without a grid sized to the resident waves (that one
-  // 2-5 % slower); profiles/r05-k_eqb_resident_grid_ab.jsonl, r05-l_mfma_eqb_ab.jsonl.)
+  // 2-5 % slower); profiles/r05-k_eqb_resident_grid_ab.jsonl, r05-l_mfma_eqb_ab.jsonl.
+  // Nor did distinct product-phase priorities per wave slot (s_setprio 1..3 by
+  // HW_ID, so that one wave's products run ahead of the others'): within
+  // noise everywhere; profiles/r05-o_mfma_slot_priority_ab.jsonl.)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t lane = threadIdx.x & 63u, h = lane >> 5;
   const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
