@@ -379,16 +379,20 @@ __global__ void __launch_bounds__(256) benor_mfma_small_kernel(KParams p) {
     uint32_t o1[S], o0[S], oq[S];                         // nonzero: some receiver's count is not 0
 #pragma unroll
     for (uint32_t s = 0; s < S; ++s) o1[s] = o0[s] = oq[s] = 0u;
-#pragma unroll
-    for (int T = 0; T < 2; ++T) {
-      const mf_v4i A = T == 0 ? A0 : A1;
-      // one product live at a time (the scheduler would otherwise issue all six first)
-      small_or_rows<MM>(mfma_count<3>(A, bn1, zero), T, o1);
-      __builtin_amdgcn_sched_barrier(0);
-      small_or_rows<MM>(mfma_count<3>(A, bn0, zero), T, o0);
-      __builtin_amdgcn_sched_barrier(0);
-      small_or_rows<MM>(mfma_count<3>(A, bnq, zero), T, oq);
-      __builtin_amdgcn_sched_barrier(0);
+    {
+      // all six products first, then their folds: at one wave per SIMD the
+      // registers are free and each product's latency hides behind the others
+      // (a dependent read of a 32x32x64 result waits ~48 cycles at one wave,
+      // tools/mfma32_probe.hip)
+      const mf_v16f r10 = mfma_count<3>(A0, bn1, zero), r00 = mfma_count<3>(A0, bn0, zero);
+      const mf_v16f rq0 = mfma_count<3>(A0, bnq, zero), r11 = mfma_count<3>(A1, bn1, zero);
+      const mf_v16f r01 = mfma_count<3>(A1, bn0, zero), rq1 = mfma_count<3>(A1, bnq, zero);
+      small_or_rows<MM>(r10, 0, o1);
+      small_or_rows<MM>(r00, 0, o0);
+      small_or_rows<MM>(rq0, 0, oq);
+      small_or_rows<MM>(r11, 1, o1);
+      small_or_rows<MM>(r01, 1, o0);
+      small_or_rows<MM>(rq1, 1, oq);
     }
 
     __builtin_amdgcn_s_setprio(0);
