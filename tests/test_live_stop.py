@@ -204,6 +204,28 @@ def test_default_start_then_stop_consensus_replays(N, F, seed):
     assert states == expected_live(N, F, faulty, init, seed, 16, ev, set(range(N)))
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,F", [(78, 26), (79, 26)])
+def test_live_pool_in_lds_and_in_hbm_replay(N, F):
+    """The two forms of a live run: at N = 78 the message pool (4N^2 + 64
+    words) fits kEventBigLdsPool and a polling wave mirrors the mailbox in LDS;
+    at N = 79 the pool is in HBM and wave 0 reads the mailbox itself.  A stop
+    for a third of the running nodes sent right after the default start; the
+    states equal oracle (iii)'s replay of the recorded landing points."""
+    seed = 0x4C50 + N
+    faulty, init = shape(N, F, half(N - F) if (N - F) % 2 else [1, 0] * ((N - F) // 2))
+    benor.launchNetwork(N, F, init, faulty)
+    benor.startConsensus(N, seed=seed, k_max=16)
+    stopped = set(range(F, N, 3))
+    for i in sorted(stopped):
+        benor._current.stop_node(i)                 # GET /stop on node i (node.ts:191-194)
+    states = benor.getNodesState(N)
+    ev = benor._current.live_stop_events()
+    assert all(ev[i] is None for i in range(F))
+    assert all(states[i]["killed"] for i in stopped)
+    assert states == expected_live(N, F, faulty, init, seed, 16, ev, stopped)
+
+
 SCRIPT = os.path.join(ROOT, "tests", "js", "live_stop.test.js")
 ADDON = os.path.join(ROOT, "ben-or-consensus-algorithm_amd", "js", "benor.node")
 
