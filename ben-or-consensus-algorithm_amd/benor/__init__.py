@@ -60,6 +60,7 @@ KNOBS = {
     "BENOR_NO_MFMA": "validation", "BENOR_NO_MFMA_BIG": "validation", "BENOR_BIG_FORM": "validation",
     "BENOR_COOP_BW": "validation", "BENOR_SMALL_MIN_TRIALS": "validation", "BENOR_BLOCKS_PER_CU": "tuning",
     "BENOR_EVENT_LANES_PER_CU": "tuning", "BENOR_TEST_DEFER_SEG_CAP": "test", "BENOR_TIMELINE": "diagnostic",
+    "BENOR_EVENT_FORM": "validation", "BENOR_LIVE_WAVES": "tuning",
 }
 
 BASE_NODE_PORT = 3000          # src/config.ts:1 (kept for the HTTP-shaped helpers)
@@ -73,7 +74,7 @@ EXPORTED_SYMBOLS = (
     "bo_plan_live_nodes", "bo_plan_destroy", "bo_run_trials", "bo_run_trial_states",
     "bo_popc_peak", "bo_last_error", "bo_abi_version", "bo_kernel_version", "bo_plan_kernel", "bo_kernel_for",
     "bo_mfma_peak", "bo_consensus_start_sched", "bo_plan_check",
-    "bo_consensus_start_live", "bo_consensus_wait", "bo_live_stop_events",
+    "bo_consensus_start_live", "bo_consensus_wait", "bo_live_stop_events", "bo_get_states", "bo_consensus_poll",
 )
 
 
@@ -127,6 +128,8 @@ def lib() -> ctypes.CDLL:
     L.bo_consensus_stop.argtypes = [ctypes.c_void_p]
     L.bo_node_stop.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
     L.bo_get_state.argtypes = [ctypes.c_void_p, ctypes.c_uint32, P(NodeStateC)]
+    L.bo_get_states.argtypes = [ctypes.c_void_p, P(NodeStateC), ctypes.c_uint32, P(ctypes.c_uint64)]
+    L.bo_consensus_poll.argtypes = [ctypes.c_void_p, P(ctypes.c_int)]
     L.bo_status.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
     L.bo_network_size.argtypes = [ctypes.c_void_p]
     L.bo_network_size.restype = ctypes.c_uint32
@@ -275,10 +278,29 @@ class Network:
     def stop_node(self, i: int) -> None:
         _check(lib().bo_node_stop(self._h, i))
 
+    def poll(self) -> bool:
+        """True while a live run is in flight; once it has ended its final states
+        are merged (bo_consensus_poll, no blocking)."""
+        r = ctypes.c_int(0)
+        _check(lib().bo_consensus_poll(self._h, ctypes.byref(r)))
+        return bool(r.value)
+
     def get_state(self, i: int) -> dict:
+        """GET /getState (node.ts:197-199): at once, from a snapshot during a live run."""
         s = NodeStateC()
         _check(lib().bo_get_state(self._h, i, ctypes.byref(s)))
         return _state_dict(s)
+
+    def get_states_at(self) -> tuple[list, int | None]:
+        """Every node's state at once (bo_get_states) and, during a live run, the
+        delivery count the snapshot reflects (None otherwise)."""
+        st = (NodeStateC * max(1, self.N))()
+        ev = ctypes.c_uint64(0)
+        _check(lib().bo_get_states(self._h, st, self.N, ctypes.byref(ev)))
+        return [_state_dict(st[i]) for i in range(self.N)], (None if ev.value == 2 ** 64 - 1 else int(ev.value))
+
+    def get_states(self) -> list[dict]:
+        return self.get_states_at()[0]
 
     def status(self, i: int) -> tuple[int, str]:
         """GET /status (node.ts:33-39): (500, "faulty") or (200, "live")."""
@@ -311,8 +333,9 @@ def startConsensus(N: int, seed: int | None = None, k_max: int = DEFAULT_K_MAX, 
     """src/nodes/consensus.ts:3-8: GET /start on every node.  As the
     reference's, it returns once the round loop (node.ts:43-163) is launched
     on the GPU, before consensus finishes (Network.start_live): stopConsensus /
-    a node's stop land in the running kernel, and getNodesState / getNodeState
-    wait for the run.  sync=True returns after the run (every live node
+    a node's stop land in the running kernel, getNodesState / getNodeState
+    answer at once with the running network's states (a snapshot), and
+    waitConsensus(N) waits for the end.  sync=True (or live=False) returns after the run (every live node
     decided, or k_max rounds; Network.start).  stop_after: a mid-run GET /stop
     schedule given up front (Network.start; returns after the run).  A second
     start on a network returns as the reference's does (every GET /start
@@ -324,6 +347,8 @@ def startConsensus(N: int, seed: int | None = None, k_max: int = DEFAULT_K_MAX, 
         raise ValueError("stop_after and live are exclusive: a live run takes /stop as it comes")
     if live and sync:
         raise ValueError("live and sync are exclusive")
+    if live is False:
+        sync = True                      # an explicit non-live start is the run-to-completion form
     try:
         if not stop_after and not sync:
             _net(N).start_live(seed, k_max)
@@ -342,18 +367,25 @@ def stopConsensus(N: int) -> None:
 
 
 def getNodeState(nodeId: int) -> dict:
-    """__test__/tests/utils.ts:4-12 (GET /getState)."""
+    """__test__/tests/utils.ts:4-12 (GET /getState, node.ts:197-199): answers at
+    once -- during a live run, with the running network's state."""
     if _current is None:
         raise RuntimeError("no launched network")
-    _current.wait()                      # a live run's final states
     return _current.get_state(nodeId)
 
 
 def getNodesState(N: int) -> list[dict]:
-    """__test__/tests/utils.ts:14-20 (after a live run has ended)."""
-    net = _net(N)
-    net.wait()
-    return [net.get_state(i) for i in range(N)]
+    """__test__/tests/utils.ts:14-20: every node's state at once (one snapshot of
+    a running network, bo_get_states).  Callers poll it until reachedFinality, as
+    the reference's tests do (benorconsensus.test.ts:153-160)."""
+    return _net(N).get_states()
+
+
+def waitConsensus(N: int) -> None:
+    """The end of the network's live run (no-op otherwise): its final states."""
+    if N == 0:
+        return
+    _net(N).wait()
 
 
 def getStatus(nodeId: int) -> tuple[int, str]:

@@ -1,0 +1,617 @@
+// benor_event_live.hip -- the workgroup-batched event kernel (r06): live runs
+// (bo_consensus_start_live, the default startConsensus) at every N <= 4096.
+//
+// The reference's GET /start answers before consensus finishes
+// (consensus.ts:3-8, node.ts:167-188): its round loop is the POST /message
+// handler (node.ts:43-163) firing message by message, and a GET /stop
+// (node.ts:191-194) or GET /getState (node.ts:197-199) may arrive at any
+// moment.  This kernel runs the message-granular model of oracle (iii),
+// oracle/benor_oracle.c event_trial() -- one delivery per event in the seeded
+// order (uniform pick from the pending pool, swap-remove), scheduled and live
+// stops applied before their delivery count -- for ONE trial per workgroup.
+// r05 ran a live trial on one wave (benor_event_big.hip: 64 events per batch,
+// every step on one SIMD); here a trial gets a workgroup of up to 15 event
+// waves plus one control wave:
+//
+//   * the event waves take a batch of B <= 64 W consecutive events: lane i
+//     draws the pick of event e + i assuming no trigger (splitmix64 is a
+//     counter), loads the two pool words its swap-remove touches, and inserts
+//     its pick into an LDS hash table that keeps, per position, the first
+//     event of the batch that picks it;
+//   * a batch is exact up to its first *conflict* -- an event that picks a
+//     position an earlier event of the batch picked, or whose tail word an
+//     earlier event overwrote -- so the batch is cut there (the conflict-free
+//     prefix reads the pool's own words: no chains to resolve);
+//   * its deliveries are applied at once with 64-bit LDS adds of
+//     {len, c0 | c1} to the receivers' inbox slots.  With exactly F faulty
+//     every slot receives exactly N - F messages per round (each trigger fires
+//     once), so a slot that reaches its quorum inside the batch
+//     triggers at the LAST batch event into it; the batch is cut after the
+//     earliest such event and the later events' adds are undone;
+//   * the conflict-free prefix then writes its moved words back, the control
+//     wave runs the trigger (node.ts:53-80 R-phase, :89-157 P-phase: decide,
+//     adopt, coin, all-decided halting) and the event waves append its
+//     broadcast of N messages;
+//   * the control wave issues no pool access: it owns the round state in LDS,
+//     applies scheduled /stop (delivery counts) and live /stop requests, and
+//     polls the host-mapped mailbox with an uncached load that it consumes
+//     ~5 us later (so the PCIe round trip is never waited for), and serves
+//     GET /getState snapshots: on request, the event waves write every node's
+//     {killed, x, decided, k} at a batch boundary to host memory with the
+//     delivery count it reflects, so a snapshot is oracle (iii) truncated at
+//     that count.
+//
+// Pool: `to | ph << 12 | x << 13 | (k & 3) << 15` (k decoded against the
+// completion round `cur`, as benor_event_big.hip), in HBM scratch or -- when
+// 4N^2 + 64 words fit kEventBigLdsPool (N <= 78) -- in LDS.
+#include "benor_device.h"
+
+namespace benor {
+
+namespace {
+
+constexpr uint64_t kGm = 0x9E3779B97F4A7C15ull;   // splitmix64 increment
+constexpr uint64_t kF13 = (1ull << 13) - 1ull;
+constexpr uint64_t kDead = 1ull << 63;             // inbox slot of a killed node
+
+__device__ __forceinline__ uint64_t smix(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// LDS hash slots per batch: at least twice the batch (load <= 1/2)
+constexpr uint32_t hash_slots(int W) { return 64u * (uint32_t)W <= 64u ? 128u : (64u * (uint32_t)W <= 256u ? 512u : (64u * (uint32_t)W <= 512u ? 1024u : 2048u)); }
+
+// The control block: round state the control wave owns, and the batch's
+// reduction words.
+struct Ctl {
+  uint64_t e;          // deliveries so far
+  uint64_t rng;        // splitmix64 state at e
+  uint32_t len;        // pending messages
+  uint32_t B;          // this batch's events
+  uint32_t conf;       // first conflicting event of the batch (B if none)
+  uint32_t ncross;     // inbox slots that reached their quorum in the batch
+  uint32_t trig;       // the batch's first trigger event (~0: none)
+  uint32_t tmsg;       // its message
+  uint32_t halted;     // 0 running, 1 all decided, 2 k_max, 3 stall
+  uint32_t snap;       // serve a snapshot at this batch boundary (the request number), 0 none
+  uint32_t body;       // the trigger's broadcast body, ~0 none
+  uint32_t cur, R;     // completion round; halting round
+  uint32_t overflow;
+};
+
+__device__ __forceinline__ uint32_t hslot(uint32_t key, uint32_t mask) { return (key * 0x9E3779B1u >> 11) & mask; }
+
+}  // namespace
+
+// Wave 0: control.  Waves 1..W: events.  One trial per workgroup (grid-stride
+// over the launch's trials).
+template <int W, bool LP>
+__global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p) {
+  constexpr uint32_t T = 64u * (uint32_t)W;        // event lanes
+  constexpr uint32_t HS = hash_slots(W);
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const bool ctl = tid < 64u;                      // the control wave
+  const uint32_t ei = tid - 64u;                   // event lane index (event waves)
+  const uint32_t N = p.N, F = p.F, quorum = p.N - p.F, m = p.m;
+  const uint32_t NWd = (N + 63u) >> 6;
+  Ctl &C = *reinterpret_cast<Ctl *>(smem);
+  unsigned char *q = smem + ((sizeof(Ctl) + 15u) & ~15u);
+  uint64_t *ibox = reinterpret_cast<uint64_t *>(q);               // [2N] {c0, c1, len}, bit 63 killed
+  uint64_t *killed = ibox + 2u * N;                              // [64]
+  uint64_t *decided = killed + 64;                               // [64]
+  uint64_t *comp = decided + 64;                                 // [4][64] round k complete at k & 3
+  uint64_t *ht = comp + 256;                                     // [HS] (pos + 1) << 32 | first event
+  uint64_t *rset = ht + HS;                                      // [64] random /stop schedule: Floyd set
+  uint64_t *rstops = rset + 64;                                  // [ev_rstops] (event << 12 | node), ~0 applied
+  uint32_t *smax = reinterpret_cast<uint32_t *>(rstops + p.ev_rstops);   // [2N] last batch event + 1 into a crossed slot
+  int16_t *ks = reinterpret_cast<int16_t *>(smax + 2u * N);      // [N]
+  uint16_t *cidx = reinterpret_cast<uint16_t *>(ks + ((N + 7u) & ~7u));  // [N] compact index (coins)
+  int8_t *xs = reinterpret_cast<int8_t *>(cidx + ((N + 7u) & ~7u));       // [N]
+  uint32_t *pool;
+  if constexpr (LP) pool = reinterpret_cast<uint32_t *>(xs + ((N + 15u) & ~15u));
+  else pool = p.scratch + (uint64_t)blockIdx.x * p.ev_stride;
+  const uint32_t cap = p.ev_cap;
+  const uint64_t allw = lane < NWd ? (N >= 64u * (lane + 1u) ? ~0ull : (1ull << (N - 64u * lane)) - 1ull) : 0ull;
+  const uint64_t wmask = NWd >= 64u ? ~0ull : ((1ull << NWd) - 1ull);
+  const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
+  uint32_t *box = p.live_box;                                    // host-mapped mailbox (live runs)
+
+  // a | b == all, over the bitset words (control wave: one word per lane)
+  auto full = [&](const uint64_t *a, const uint64_t *b) {
+    const bool ok = lane >= NWd || ((a[lane] | b[lane]) == allw);
+    return (__ballot(ok) & wmask) == wmask;
+  };
+  // pool words: HBM slices are read around L1 (the batch's own stores went to L2)
+  auto load = [&](uint32_t i) -> uint32_t {
+    if constexpr (LP) return pool[i];
+    else return __hip_atomic_load(&pool[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  auto vm_drain = [&]() {                          // this wave's pool stores are in L2
+    if constexpr (!LP) __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+  };
+
+  for (uint32_t i = tid; i < HS; i += blockDim.x) ht[i] = 0ull;
+  for (uint32_t i = tid; i < 2u * N; i += blockDim.x) smax[i] = 0u;
+
+  // the control wave's mailbox poll: lane l < NWd reads request bits 64l ..
+  // 64l + 63, lane 0 also the snapshot request; issued at `polled`, consumed
+  // >= kPollTicks later
+  constexpr long long kPollTicks = 500;            // 5 us of the 100 MHz wall clock
+  uint64_t pv_req = 0ull;
+  uint32_t pv_snap = 0u, snap_served = 0u;
+  long long polled = 0;
+  bool poll_out = false;
+  auto poll_issue = [&]() {
+    if (lane < NWd)
+      pv_req = __hip_atomic_load(reinterpret_cast<uint64_t *>(box + kLiveReq) + lane, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lane == 0u) pv_snap = __hip_atomic_load(box + kSnapReq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    polled = wall_clock64();
+    poll_out = true;
+  };
+  if (ctl && box) poll_issue();
+
+  for (uint64_t t = blockIdx.x; t < p.trial_count; t += gridDim.x) {
+    const uint64_t trial = p.trial_begin + t;
+    const uint32_t tlo = (uint32_t)trial, thi = (uint32_t)(trial >> 32);
+    // ---- node.ts:21-26: faulty nodes killed, live nodes x = initial value
+    if (ctl) {
+      killed[lane] = lane < NWd ? allw : 0ull;     // every node, then the live ones cleared
+      decided[lane] = 0ull;
+      for (int r = 0; r < 4; ++r) comp[r * 64 + lane] = 0ull;
+    }
+    for (uint32_t i = tid; i < N; i += blockDim.x) {
+      xs[i] = -1;
+      ks[i] = -1;
+      ibox[2u * i] = kDead;
+      ibox[2u * i + 1u] = kDead;
+    }
+    __syncthreads();
+    for (uint32_t c = tid; c < m; c += blockDim.x) {
+      const uint32_t i = p.live_ids[c];
+      int8_t v;
+      if (p.init_mode == BO_INIT_RANDOM) {        // oracle_random_init
+        if (m <= 32u) {
+          v = (int8_t)((init_word_small(k0, k1, trial) >> c) & 1u);
+        } else {
+          const uint4 ir = philox4x32_10<false>(k0, k1, make_uint4(tlo, thi, c >> 7, kStreamInit << 24));
+          v = (int8_t)((coin_word_v(ir, ((c >> 5) & 3u) + 1u) >> (c & 31u)) & 1u);
+        }
+      } else {
+        v = p.init_x[i];
+      }
+      xs[i] = v;
+      ks[i] = 1;                                   // /start: k = 1 (node.ts:172)
+      cidx[i] = (uint16_t)c;
+      ibox[2u * i] = 0ull;
+      ibox[2u * i + 1u] = 0ull;
+      __hip_atomic_fetch_and(reinterpret_cast<unsigned long long *>(&killed[i >> 6]), ~(1ull << (i & 63u)),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __syncthreads();
+    // ---- /start (node.ts:167-188): every live node broadcasts its x, in node order
+    if (!ctl) {
+      for (uint32_t c = 0; c < m; ++c) {
+        const uint32_t body = ((uint32_t)(xs[p.live_ids[c]] & 3) << 13) | (1u << 15);
+        for (uint32_t to = ei; to < N; to += T) pool[c * N + to] = to | body;
+      }
+      vm_drain();
+    }
+    // ---- the /stop schedule: explicit (ev_stops, ascending event << 12 | node)
+    // or random (crash_count): Floyd over compact live indices from Philox
+    // stream 4, then one uniform delivery count in [0, crash_window) per pick
+    const uint32_t kr = p.ev_rstops;
+    if (ctl && kr) {
+      rset[lane] = 0ull;
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0u) {
+        DStream ds;
+        ds.k0 = k0; ds.k1 = k1; ds.c0 = tlo; ds.c1 = thi; ds.c2 = 0u; ds.c3 = kStreamCrash << 24; ds.widx = 0;
+        ds.sh = 12u;
+        for (uint32_t j = m - kr, n = 0; j < m; ++j, ++n) {
+          const uint32_t tt = ds.uniform(j + 1u);
+          const uint32_t idx = ((rset[tt >> 6] >> (tt & 63u)) & 1ull) ? j : tt;
+          rset[idx >> 6] |= 1ull << (idx & 63u);
+          rstops[n] = idx;
+        }
+        for (uint32_t n = 0; n < kr; ++n) {
+          const uint32_t when = ds.uniform(p.crash_window);
+          rstops[n] = ((uint64_t)when << 12) | p.live_ids[(uint32_t)rstops[n]];
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    }
+    auto rstops_min = [&]() {                      // control wave: the random schedule's next key
+      uint64_t v = ~0ull;
+      for (uint32_t i = lane; i < kr; i += 64u) v = v < rstops[i] ? v : rstops[i];
+      for (int off = 32; off >= 1; off >>= 1) {
+        const uint64_t o = __shfl_xor(v, off);
+        v = v < o ? v : o;
+      }
+      return v;
+    };
+    uint32_t next = 0;
+    uint64_t next_key = 0;
+    if (ctl) {
+      next_key = kr ? rstops_min() : (p.ev_nstops ? p.ev_stops[0] : ~0ull);
+      if (lane == 0u) {
+        const uint4 o = philox4x32_10<false>(k0, k1, make_uint4(tlo, thi, 0u, kStreamOrder << 24));
+        C.rng = (((uint64_t)o.x << 32) | o.y) ^ 0xD1B54A32D192ED03ull;
+        C.e = 0ull;
+        C.len = m * N;
+        C.cur = 1u;
+        C.R = 0u;
+        C.halted = 0u;
+        C.overflow = 0u;
+      }
+    }
+    // control wave: round completion and halting (node.ts:116-145 as DESIGN §2)
+    auto advance = [&](uint32_t &cur, uint32_t &halted, uint32_t &R) {
+      while (full(comp + (cur & 3u) * 64u, killed)) {
+        if (full(decided, killed)) { halted = 1u; R = cur; return; }
+        if (cur >= p.k_max) { halted = 2u; R = cur; return; }
+        comp[(cur & 3u) * 64u + lane] = 0ull;
+        ++cur;
+      }
+    };
+    __syncthreads();
+
+    // The batch loop, as two loops that meet at the same barriers (A .. H, with
+    // E .. G only when a slot crossed its quorum): the control wave's and the
+    // event waves'.  Kept apart so that the control wave's in-flight mailbox
+    // poll is never waited for by an s_waitcnt the event code needs.
+    if (ctl) {
+      for (;;) {
+        // ================= control: stops, mailbox, snapshot, the batch size
+        uint32_t cur = C.cur, halted = C.halted, R = C.R, len = C.len;
+        const uint64_t e = C.e;
+        bool crashed = false;
+        // scheduled GET /stop (node.ts:191-194) before delivery e
+        while ((next_key >> 12) == e) {
+          const uint32_t i = (uint32_t)(next_key & 4095u);
+          if (lane == 0u) {
+            killed[i >> 6] |= 1ull << (i & 63u);
+            ibox[2u * i] |= kDead;
+            ibox[2u * i + 1u] |= kDead;
+          }
+          crashed = true;
+          if (kr) {
+            for (uint32_t j = lane; j < kr; j += 64u)
+              if (rstops[j] == next_key) rstops[j] = ~0ull;
+            next_key = rstops_min();
+          } else {
+            ++next;
+            next_key = next < p.ev_nstops ? p.ev_stops[next] : ~0ull;
+          }
+        }
+        uint32_t snap = 0u;
+        if (box && poll_out && wall_clock64() - polled >= kPollTicks) {
+          // live GET /stop requests and /getState snapshot requests: the poll
+          // issued >= 5 us ago (its PCIe round trip is long done)
+          const uint64_t req = pv_req;
+          const uint32_t sreq = __shfl(pv_snap, 0);
+          uint64_t fresh = 0ull;
+          if (lane < NWd) {
+            fresh = req & allw & ~killed[lane];
+            killed[lane] |= fresh;
+          }
+          for (uint64_t f = fresh; f; f &= f - 1ull) {
+            const uint32_t i = 64u * lane + (uint32_t)__builtin_ctzll(f);
+            ibox[2u * i] |= kDead;
+            ibox[2u * i + 1u] |= kDead;
+            __hip_atomic_store(box + kLiveEv + i, e < 0xFFFFFFFFull ? (uint32_t)e : 0xFFFFFFFEu, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+          crashed = crashed || __any(fresh != 0ull);
+          if (sreq != snap_served) {
+            snap_served = sreq;
+            snap = sreq;
+          }
+          poll_issue();
+        }
+        if (crashed) {
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+          const bool alive = lane < NWd && killed[lane] != allw;
+          if (!__any(alive)) halted = 3u;
+          else advance(cur, halted, R);
+        }
+        if (!halted && len == 0u) halted = 3u;
+        uint32_t B = len < T ? len : T;
+        if (next_key != ~0ull) {
+          const uint64_t until = (next_key >> 12) - e;
+          if (until < B) B = (uint32_t)until;
+        }
+        if (lane == 0u) {
+          C.cur = cur;
+          C.halted = halted;
+          C.R = R;
+          C.B = B;
+          C.conf = B;
+          C.ncross = 0u;
+          C.trig = 0xFFFFFFFFu;
+          C.body = 0xFFFFFFFFu;
+          C.snap = snap;
+        }
+        if (snap && lane == 0u) {                  // the delivery count this snapshot reflects
+          __hip_atomic_store(box + kSnapE, (uint32_t)e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(box + kSnapE + 1u, (uint32_t)(e >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        __syncthreads();                           // ---- A
+        if (halted) break;
+        __syncthreads();                           // ---- B: the snapshot's states are written
+        if (snap && lane == 0u)
+          __hip_atomic_store(box + kSnapSeq, snap, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __syncthreads();                           // ---- C
+        const uint32_t used0 = C.conf;
+        __syncthreads();                           // ---- D
+        uint32_t used = used0;
+        if (C.ncross) {
+          __syncthreads();                         // ---- E
+          __syncthreads();                         // ---- F
+          used = C.trig + 1u;
+          __syncthreads();                         // ---- G
+        }
+        const uint32_t tr = C.trig;
+        if (tr != 0xFFFFFFFFu) {
+          // ---- the trigger (node.ts:52-80 R-phase, :88-157 P-phase)
+          const uint32_t tmsg = C.tmsg;
+          const uint32_t to = tmsg & 4095u, ph = (tmsg >> 12) & 1u;
+          const uint32_t k = cur + (((tmsg >> 15) - cur) & 3u);
+          const uint64_t tbox = ibox[2u * to + ph];
+          __builtin_amdgcn_wave_barrier();
+          if (lane == 0u) ibox[2u * to + ph] = 0ull;   // every message of the phase arrived: the slot is free
+          const uint32_t c0 = (uint32_t)(tbox & kF13), c1 = (uint32_t)((tbox >> 13) & kF13);
+          uint32_t body = 0xFFFFFFFFu, ncur = cur, nhalted = 0u;
+          if (ph == 0u) {
+            const uint32_t v = c0 > c1 ? 0u : (c1 > c0 ? 1u : 2u);
+            body = (1u << 12) | (v << 13) | ((k & 3u) << 15);
+          } else {
+            int8_t nx;
+            bool dec = true;
+            if (c0 > F) nx = 0;
+            else if (c1 > F) nx = 1;
+            else {
+              dec = false;
+              if (c0 + c1 > 0u && c0 > c1) nx = 0;
+              else if (c0 + c1 > 0u && c0 < c1) nx = 1;
+              else {
+                const uint32_t c = cidx[to];       // the coin of compact node c in round k (node.ts:111)
+                const uint4 rr = coin_block<false>(k0, k1, tlo, thi, c, k);
+                nx = (int8_t)((coin_word(rr, k) >> (c & 31u)) & 1u);
+              }
+            }
+            if (lane == 0u) {
+              xs[to] = nx;
+              ks[to] = (int16_t)(k + 1u);
+              if (dec) decided[to >> 6] |= 1ull << (to & 63u);
+              comp[(k & 3u) * 64u + (to >> 6)] |= 1ull << (to & 63u);
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+            advance(ncur, nhalted, R);
+            if (!nhalted) body = ((uint32_t)(nx & 3) << 13) | (((k + 1u) & 3u) << 15);
+          }
+          if (body != 0xFFFFFFFFu && (uint64_t)(len - used) + N > cap) {
+            body = 0xFFFFFFFFu;                    // the pool would overflow: stop (flagged)
+            nhalted = 3u;
+            if (lane == 0u) C.overflow = 1u;
+          }
+          if (lane == 0u) {
+            C.body = body;
+            C.cur = ncur;
+            C.R = R;
+            C.halted = nhalted;
+          }
+          len = len - used + (body != 0xFFFFFFFFu ? N : 0u);
+        } else {
+          len -= used;
+        }
+        __syncthreads();                           // ---- H
+        if (lane == 0u) {
+          C.len = len;
+          C.e = e + used;
+          C.rng += (uint64_t)used * kGm;
+        }
+      }
+    } else {
+      for (;;) {
+        __syncthreads();                           // ---- A
+        const uint32_t halted = C.halted, B = C.B, len = C.len, cur = C.cur, snap = C.snap;
+        const uint64_t rng = C.rng;
+        if (halted) break;
+        if (snap) {
+          // GET /getState (node.ts:197-199) mid-run: every node's state as of
+          // delivery e, to host memory (bo_get_states reads it after the sequence word)
+          for (uint32_t i = ei; i < N; i += T) {
+            const bool f = ks[i] < 0 && xs[i] < 0;   // faulty from launch (never ran)
+            const uint32_t kl =
+                (uint32_t)(uint8_t)((killed[i >> 6] >> (i & 63u)) & 1ull) | ((uint32_t)(uint8_t)xs[i] << 8) |
+                ((uint32_t)(uint8_t)(f ? (int8_t)-1 : (int8_t)((decided[i >> 6] >> (i & 63u)) & 1ull)) << 16);
+            __hip_atomic_store(box + kSnapSt + 2u * i, kl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(box + kSnapSt + 2u * i + 1u, (uint32_t)(int32_t)ks[i], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+          __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0): the states reached the host
+        }
+        // ================= the batch's picks: event e + i takes position q_i and
+        // moves the word at t_i = len - 1 - i there (swap-remove)
+        uint32_t qi = 0u, ti = 0u, pv = 0u, tv = 0u, hs = 0u;
+        const bool act = ei < B;
+        if (act) {
+          const uint64_t z = smix(rng + (uint64_t)(ei + 1u) * kGm);
+          qi = (uint32_t)(((uint64_t)(uint32_t)(z >> 32) * (uint64_t)(len - ei)) >> 32);
+          ti = len - 1u - ei;
+          pv = load(qi);
+          tv = load(ti);
+          // first event of the batch that picks qi
+          const uint64_t val = ((uint64_t)(qi + 1u) << 32) | ei;
+          hs = hslot(qi, HS - 1u);
+          for (;;) {
+            const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long *>(&ht[hs]), 0ull, val);
+            if (old == 0ull) break;
+            if ((uint32_t)(old >> 32) == qi + 1u) {
+              atomicMin(reinterpret_cast<unsigned long long *>(&ht[hs]), val);
+              break;
+            }
+            hs = (hs + 1u) & (HS - 1u);
+          }
+        }
+        __syncthreads();                           // ---- B
+        if (act) {
+          // conflict: an earlier event of the batch picked qi, or picked ti (its
+          // word moved there is then not the pool's own); q_j == t_i implies j <= i
+          auto first = [&](uint32_t key) -> uint32_t {
+            uint32_t h = hslot(key, HS - 1u);
+            for (;;) {
+              const uint64_t v = ht[h];
+              if (v == 0ull) return 0xFFFFFFFFu;
+              if ((uint32_t)(v >> 32) == key + 1u) return (uint32_t)v;
+              h = (h + 1u) & (HS - 1u);
+            }
+          };
+          const uint32_t fq = first(qi), ft = first(ti);
+          if (fq < ei || ft < ei) atomicMin(&C.conf, ei);
+        }
+        __syncthreads();                           // ---- C
+        if (act) ht[hs] = 0ull;                    // every lookup is done: the table is empty again
+        const uint32_t used0 = C.conf;
+        // ================= POST /message (node.ts:45-158): the prefix's deliveries at once
+        uint64_t inc = 0ull;
+        uint32_t slot = 0u;
+        if (act && ei < used0) {
+          const uint32_t to = pv & 4095u, ph = (pv >> 12) & 1u, xv = (pv >> 13) & 3u;
+          const uint32_t k = cur + (((pv >> 15) - cur) & 3u);
+          slot = 2u * to + ph;
+          if (k < p.k_max + 3u)                    // beyond the oracle's round window: dropped
+            inc = (1ull << 26) + (xv == 0u ? 1ull : (xv == 1u ? 1ull << 13 : 0ull));
+          if (inc) {
+            const uint64_t old = __hip_atomic_fetch_add(reinterpret_cast<unsigned long long *>(&ibox[slot]), inc,
+                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            // killed receivers drop the message (node.ts:45): their slot counts
+            // on, never tested; a live slot crosses its quorum (node.ts:52, :88)
+            if (!(old & kDead) && ((old >> 26) & kF13) + 1u == quorum) atomicAdd(&C.ncross, 1u);
+          }
+        }
+        __syncthreads();                           // ---- D
+        uint32_t used = used0;
+        if (C.ncross) {
+          // a crossed slot triggers at the last batch event into it; the batch
+          // ends after the earliest such event
+          bool mine = false;
+          if (inc) {
+            const uint64_t b = ibox[slot];
+            mine = !(b & kDead) && ((b >> 26) & kF13) == quorum;
+            if (mine) atomicMax(&smax[slot], ei + 1u);
+          }
+          __syncthreads();                         // ---- E
+          if (mine) atomicMin(&C.trig, smax[slot] - 1u);
+          __syncthreads();                         // ---- F
+          const uint32_t tr = C.trig;
+          if (mine) smax[slot] = 0u;
+          if (inc && ei > tr)
+            __hip_atomic_fetch_add(reinterpret_cast<unsigned long long *>(&ibox[slot]), 0ull - inc,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (act && ei == tr) C.tmsg = pv;
+          used = tr + 1u;
+          __syncthreads();                         // ---- G
+        }
+        // ================= the prefix's pool writes: q_i keeps the word moved
+        // there unless q_i itself was popped (q_i == t_i)
+        if (act && ei < used && qi < len - used) pool[qi] = tv;
+        vm_drain();
+        __syncthreads();                           // ---- H
+        const uint32_t body = C.body;
+        if (body != 0xFFFFFFFFu) {                 // the trigger's broadcast (node.ts:72-80, :149-157)
+          for (uint32_t d = ei; d < N; d += T) pool[len - used + d] = d | body;
+          vm_drain();
+        }
+      }
+    }
+    // ---- outcome over the nodes still running
+    const uint32_t hlt = C.halted, R = C.R;
+    __syncthreads();
+    if (ctl) {
+      bool any0 = false, any1 = false, anyq = false, nl = false;
+      for (uint32_t i = lane; i < N; i += 64u) {
+        if ((killed[i >> 6] >> (i & 63u)) & 1ull) continue;
+        nl = true;
+        const int8_t v = xs[i];
+        if (v == 0) any0 = true; else if (v == 1) any1 = true; else anyq = true;
+      }
+      const bool g0 = __any(any0), g1 = __any(any1), gq = __any(anyq), gl = __any(nl);
+      const uint32_t v = (!gl || gq || (g0 && g1)) ? 2u : (g1 ? 1u : 0u);
+      if (lane == 0u) {
+        atomicAdd(&p.hist[hlt == 1u ? (R * 3u + v) : v], 1ull);
+        if (hlt == 1u && v == 2u) atomicAdd(&p.hist[p.hist_len - 1u], 1ull);
+        if (C.overflow && p.rounds_out) atomicOr(p.rounds_out, 0x80000000u);
+        if (C.overflow && p.overflow) atomicOr(p.overflow, 2u);
+        if (p.node_out && p.rounds_out) atomicOr(p.rounds_out, hlt == 1u ? R : 0u);
+      }
+    }
+    if (p.node_out) {
+      for (uint32_t i = tid; i < N; i += blockDim.x) {
+        bo_node_state ns;
+        const bool f = ks[i] < 0 && xs[i] < 0;
+        ns.killed = (int8_t)((killed[i >> 6] >> (i & 63u)) & 1ull);
+        ns.x = xs[i];
+        ns.decided = f ? (int8_t)-1 : (int8_t)((decided[i >> 6] >> (i & 63u)) & 1ull);
+        ns.pad = 0;
+        ns.k = ks[i];
+        p.node_out[i] = ns;
+      }
+    }
+    __syncthreads();
+  }
+  // the control wave's last poll must land before the wave ends
+  if (ctl && box && poll_out) __builtin_amdgcn_s_waitcnt(0x0F70);
+}
+
+uint32_t event_wg_waves(const KParams &p) {
+  const uint32_t forced = knob_u32("BENOR_LIVE_WAVES", 0u);
+  if (forced == 1u || forced == 3u || forced == 7u || forced == 15u) return forced;
+  if (p.N <= 32u) return 1u;
+  if (p.N <= 128u) return 3u;
+  if (p.N <= 512u) return 7u;
+  return 15u;
+}
+
+bool event_wg_lds_pool(const KParams &p) { return (uint64_t)p.ev_cap * 4u <= kEventBigLdsPool; }
+
+uint32_t event_wg_lds_bytes(const KParams &p, uint32_t W) {
+  const uint32_t N = p.N;
+  const uint32_t HS = W == 1u ? hash_slots(1) : W == 3u ? hash_slots(3) : W == 7u ? hash_slots(7) : hash_slots(15);
+  uint32_t b = ((uint32_t)sizeof(Ctl) + 15u) & ~15u;
+  b += 16u * N + 8u * 64u * 6u + 8u * HS + 8u * 64u + 8u * p.ev_rstops;   // ibox, killed/decided/comp, hash, Floyd set, keys
+  b += 8u * N;                                                            // smax
+  b += 2u * ((N + 7u) & ~7u) * 2u + ((N + 15u) & ~15u);                   // ks, cidx, xs
+  if (event_wg_lds_pool(p)) b += 4u * p.ev_cap;
+  return b;
+}
+
+template <int W, bool LP>
+static hipError_t launch_wg(const KParams &p, int grid, hipStream_t s) {
+  const uint32_t lds = event_wg_lds_bytes(p, (uint32_t)W);
+  if (lds > 64u * 1024u) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&benor_event_wg_kernel<W, LP>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL((benor_event_wg_kernel<W, LP>), dim3(grid), dim3(64 * (W + 1)), lds, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_event_wg(const KParams &p, int grid, hipStream_t s) {
+  const uint32_t W = event_wg_waves(p);
+  const bool lp = event_wg_lds_pool(p);
+  if (W == 1u) return lp ? launch_wg<1, true>(p, grid, s) : launch_wg<1, false>(p, grid, s);
+  if (W == 3u) return lp ? launch_wg<3, true>(p, grid, s) : launch_wg<3, false>(p, grid, s);
+  if (W == 7u) return lp ? launch_wg<7, true>(p, grid, s) : launch_wg<7, false>(p, grid, s);
+  return lp ? launch_wg<15, true>(p, grid, s) : launch_wg<15, false>(p, grid, s);
+}
+
+}  // namespace benor

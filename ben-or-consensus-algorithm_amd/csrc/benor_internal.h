@@ -105,6 +105,9 @@ struct KParams {
   // [kLiveEv + i] the delivery count at which node i's stop landed (device)
   uint32_t live;
   uint32_t *live_box;
+  // event level: run the workgroup-batched kernel (benor_event_live.hip) --
+  // live runs, and batch plans under BENOR_EVENT_FORM=wg
+  uint32_t ev_wg;
   // W kernel trial-list mode: run the trials trial_begin + trial_list[i],
   // i < min(*trial_list_len, trial_count), instead of a contiguous range
   const uint32_t *trial_list, *trial_list_len;
@@ -120,8 +123,14 @@ struct KParams {
 constexpr uint32_t kTimelineWords = 12;
 
 
-constexpr uint32_t kLiveReq = 2;                 // live mailbox: request bitset words (BO_MAX_N / 32)
-constexpr uint32_t kLiveEv = kLiveReq + 128;     // live mailbox: per-node stop delivery counts
+// The live run's host-mapped mailbox (u32 words):
+constexpr uint32_t kLiveReq = 2;                 // request bitset words (BO_MAX_N / 32), GET /stop posted
+constexpr uint32_t kLiveEv = kLiveReq + 128;     // per-node stop delivery counts (device writes)
+constexpr uint32_t kSnapReq = kLiveEv + BO_MAX_N;   // GET /getState snapshot requests (host increments)
+constexpr uint32_t kSnapSeq = kSnapReq + 1u;     // the last request served (device writes, after the snapshot)
+constexpr uint32_t kSnapE = kSnapSeq + 1u;       // u64: the delivery count the snapshot reflects
+constexpr uint32_t kSnapSt = kSnapE + 4u;        // [BO_MAX_N] {killed | x << 8 | decided << 16, k}: the snapshot
+constexpr uint32_t kLiveBoxWords = kSnapSt + 2u * BO_MAX_N;
 constexpr uint64_t kLivePollTicks = 1000;        // wall-clock ticks (100 MHz) between wave 0's own mailbox polls
 constexpr uint32_t kEvMailboxWords = 4u + 128u;  // the event kernel's LDS mirror of it: seq, done, request bits, pad
 
@@ -156,6 +165,14 @@ constexpr uint64_t kEventBigLdsPool = 96u * 1024u;
 bool event_big_lds_pool(const KParams &p);
 uint32_t event_big_lds_bytes(const KParams &p);
 hipError_t launch_event_big(const KParams &p, int grid_blocks, hipStream_t stream);
+
+// Workgroup-batched event kernel (benor_event_live.hip, r06): one trial per
+// workgroup of a control wave and 1, 3, 7 or 15 event waves; live runs (mailbox
+// /stop, /getState snapshots) and single-trial network runs.
+uint32_t event_wg_waves(const KParams &p);
+bool event_wg_lds_pool(const KParams &p);
+uint32_t event_wg_lds_bytes(const KParams &p, uint32_t waves);
+hipError_t launch_event_wg(const KParams &p, int grid_blocks, hipStream_t stream);
 
 // Per-shape launchers, explicitly instantiated in benor_w_*.hip (W = 1..32)
 // and benor_blocked.hip (G = 11..22).

@@ -590,14 +590,18 @@ void plan_geometry(KParams &p) {
   const uint32_t W = p.W;
   p.hist_len = (p.k_max + 1u) * 3u + 1u;
   p.hist_bytes = (((p.hist_len * 4u) + 15u) & ~15u) + kParamBytes;   // histogram + parameter block
-  if (p.mode == BO_MODE_EVENT && (p.N > kMaxEventN || p.live)) {   // one wave per trial (benor_event_big.hip)
+  // one wave per trial (benor_event_big.hip), or one workgroup per trial
+  // (benor_event_live.hip: live runs; batch plans under BENOR_EVENT_FORM=wg)
+  const bool wg = p.mode == BO_MODE_EVENT && (p.live || knob_is("BENOR_EVENT_FORM", "wg"));
+  if (p.mode == BO_MODE_EVENT && (p.N > kMaxEventN || wg)) {
     p.G = 1;
     p.nblocks = 1;
     p.variant = 5;
     p.wave_bytes = 0;
+    p.ev_wg = wg ? 1u : 0u;
     p.ev_cap = 4u * p.N * p.N + 64u;
     p.ev_stride = p.ev_cap;                          // u32 messages
-    p.lds_bytes = event_big_lds_bytes(p);
+    p.lds_bytes = wg ? event_wg_lds_bytes(p, event_wg_waves(p)) : event_big_lds_bytes(p);
     return;
   }
   if (p.mode == BO_MODE_EVENT) {
@@ -758,7 +762,7 @@ hipError_t launch_lockstep(const KParams &p, int grid, hipStream_t s) {
     }
     return hipGetLastError();
   }
-  if (p.variant == 5) return launch_event_big(p, grid, s);
+  if (p.variant == 5) return p.ev_wg ? launch_event_wg(p, grid, s) : launch_event_big(p, grid, s);
   if (p.variant == 6) return dispatch_lane(p, grid, s, std::make_integer_sequence<int, (int)kMaxLaneM>{});
   if (p.variant == 8 && !small_on_lane(p))
     return dispatch_mfma_small(p, grid, s, std::make_integer_sequence<int, (int)kMaxSmallMfmaM - 1>{});   // m = 2..32

@@ -17,7 +17,11 @@
  *   networkWait(handle) -> Promise<void>            end of a live run (bo_consensus_wait)
  *   liveStopEvents(handle) -> Array<number|null>    where a live run applied each /stop
  *   networkStop(handle) / nodeStop(handle, i)       consensus.ts:10-15, node.ts:191-194
- *   getState(handle, i) -> {killed, x, decided, k}  node.ts:197-199
+ *   getState(handle, i) -> {killed, x, decided, k}  node.ts:197-199 (at once: a snapshot
+ *       of a live run in flight)
+ *   getStates(handle) -> {states, events}          every node at once (bo_get_states):
+ *       events = the deliveries a live run's snapshot reflects, null otherwise
+ *   consensusPoll(handle) -> boolean               a live run is in flight (bo_consensus_poll)
  *   status(handle, i) -> 500 | 200                  node.ts:33-39
  *   runTrials(cfg) -> Promise<BigUint64Array>       batch histogram (bo_run_trials)
  */
@@ -347,18 +351,7 @@ static napi_value node_stop(napi_env env, napi_callback_info info) {
     return NULL;
 }
 
-static napi_value get_state(napi_env env, napi_callback_info info) {
-    size_t argc = 2;
-    napi_value argv[2];
-    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-    bo_network *net = get_net(env, argv[0]);
-    if (!net) return NULL;
-    int ok = 1;
-    uint32_t i = get_u32(env, argv[1], &ok);
-    if (!ok) { napi_throw_type_error(env, NULL, "node index must be a uint32"); return NULL; }
-    bo_node_state s;
-    int rc = bo_get_state(net, i, &s);
-    if (rc) { throw_bo(env, rc); return NULL; }
+static napi_value state_object(napi_env env, bo_node_state s) {
     napi_value o, v;
     NAPI_CALL(env, napi_create_object(env, &o));
     napi_get_boolean(env, s.killed != 0, &v);
@@ -374,6 +367,58 @@ static napi_value get_state(napi_env env, napi_callback_info info) {
     else napi_create_int32(env, s.k, &v);
     napi_set_named_property(env, o, "k", v);
     return o;
+}
+
+static napi_value get_state(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    bo_network *net = get_net(env, argv[0]);
+    if (!net) return NULL;
+    int ok = 1;
+    uint32_t i = get_u32(env, argv[1], &ok);
+    if (!ok) { napi_throw_type_error(env, NULL, "node index must be a uint32"); return NULL; }
+    bo_node_state s;
+    int rc = bo_get_state(net, i, &s);
+    if (rc) { throw_bo(env, rc); return NULL; }
+    return state_object(env, s);
+}
+
+static napi_value get_states(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1];
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    bo_network *net = get_net(env, argv[0]);
+    if (!net) return NULL;
+    const uint32_t N = bo_network_size(net);
+    bo_node_state *st = (bo_node_state *)malloc(sizeof(bo_node_state) * (N ? N : 1));
+    uint64_t ev = 0;
+    int rc = bo_get_states(net, st, N, &ev);
+    if (rc) { free(st); throw_bo(env, rc); return NULL; }
+    napi_value o, arr, v;
+    napi_create_object(env, &o);
+    napi_create_array_with_length(env, N, &arr);
+    for (uint32_t i = 0; i < N; ++i) napi_set_element(env, arr, i, state_object(env, st[i]));
+    free(st);
+    napi_set_named_property(env, o, "states", arr);
+    if (ev == UINT64_MAX) napi_get_null(env, &v);
+    else napi_create_double(env, (double)ev, &v);
+    napi_set_named_property(env, o, "events", v);
+    return o;
+}
+
+static napi_value consensus_poll(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1];
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    bo_network *net = get_net(env, argv[0]);
+    if (!net) return NULL;
+    int running = 0;
+    int rc = bo_consensus_poll(net, &running);
+    if (rc) { throw_bo(env, rc); return NULL; }
+    napi_value v;
+    napi_get_boolean(env, running != 0, &v);
+    return v;
 }
 
 static napi_value status(napi_env env, napi_callback_info info) {
@@ -557,6 +602,8 @@ static napi_value init_module(napi_env env, napi_value exports) {
         {"networkStop", NULL, network_stop, NULL, NULL, NULL, napi_default, NULL},
         {"nodeStop", NULL, node_stop, NULL, NULL, NULL, napi_default, NULL},
         {"getState", NULL, get_state, NULL, NULL, NULL, napi_default, NULL},
+        {"getStates", NULL, get_states, NULL, NULL, NULL, napi_default, NULL},
+        {"consensusPoll", NULL, consensus_poll, NULL, NULL, NULL, napi_default, NULL},
         {"status", NULL, status, NULL, NULL, NULL, napi_default, NULL},
         {"runTrials", NULL, run_trials, NULL, NULL, NULL, napi_default, NULL},
     };

@@ -15,7 +15,10 @@
 #include <algorithm>
 #include <utility>
 #include <cstdlib>
+#include <memory>
 #include <mutex>
+#include <thread>
+#include <chrono>
 #include <vector>
 
 #include "benor.h"
@@ -81,6 +84,8 @@ constexpr KnobSpec kKnobs[] = {
     {"BENOR_SMALL_MIN_TRIALS", "validation"},   // packed matrix-core kernel from this launch size
     {"BENOR_BLOCKS_PER_CU", "tuning"},          // workgroups per CU (grid)
     {"BENOR_EVENT_LANES_PER_CU", "tuning"},     // event level, N <= 256: lanes per CU
+    {"BENOR_EVENT_FORM", "validation"},         // "wg": batch event plans on the workgroup-batched kernel
+    {"BENOR_LIVE_WAVES", "tuning"},             // 1 / 3 / 7 / 15: event waves of the workgroup-batched kernel
     {"BENOR_TEST_DEFER_SEG_CAP", "test"},       // deferral segment capacity below the sizing rule
     {"BENOR_TIMELINE", "diagnostic"},           // packed matrix-core kernel: per-wave phase stamps to a file
 };
@@ -114,10 +119,12 @@ struct bo_network {
   std::vector<uint8_t> faulty;
   bool started = false;     // GET /start was served (node.ts:167-188); inboxes persist after it
   bool in_flight = false;   // a start's kernel is running
-  bo_live *live = nullptr;  // a live run (bo_consensus_start_live) not yet waited for
-  std::vector<uint32_t> stop_events;   // its /stop delivery counts, after bo_consensus_wait
+  std::shared_ptr<bo_live> live;   // a live run (bo_consensus_start_live) not yet finalized
+  int live_rc = 0;          // the result of the last live run finalized
+  std::vector<uint32_t> stop_events;   // its /stop delivery counts, after the run
   mutable std::mutex mu;
-  std::mutex wait_mu;       // serialises bo_consensus_wait
+  std::mutex wait_mu;       // serialises the end of a live run (live_finalize)
+  std::mutex snap_mu;       // one GET /getState snapshot request in flight at a time
 };
 
 struct bo_plan {
@@ -137,44 +144,56 @@ struct bo_plan {
 };
 
 namespace {
-// The resources of one live run, kept for the next one (r05: the default
-// startConsensus is a live run, and a network of the reference's size spent
-// 0.8 ms of its 0.83 ms creating a stream, pinning a mailbox and allocating
-// and freeing ten device buffers).  A slot is one device's stream, a
-// host-mapped mailbox for BO_MAX_N nodes and one device buffer that grows to
-// the largest run it served; slots are handed out under a lock and returned
-// by bo_consensus_wait.  Never freed (process lifetime, like StateScratch).
+// The resources of one single-trial event-level run, kept for the next one
+// (r05: the default startConsensus is a live run, and a network of the
+// reference's size spent 0.8 ms of its 0.83 ms creating a stream, pinning a
+// mailbox and allocating and freeing ten device buffers).  A slot is one
+// device's stream, a host-mapped mailbox for BO_MAX_N nodes (GET /stop
+// requests, their landing points, GET /getState snapshots) and one device
+// buffer that grows to the largest run it served.  Slots are handed out under
+// a lock and returned when their run ends; a buffer above kSlotKeepBytes is
+// freed on return (a process that once ran a large network does not keep its
+// message pool), and a slot whose run failed is destroyed, not reused.
 struct LiveSlot {
   int device = -1;
   hipStream_t s = nullptr;
-  uint32_t *box = nullptr;             // host-mapped mailbox (benor::kLiveReq / kLiveEv layout)
+  uint32_t *box = nullptr;             // host-mapped mailbox (benor::kLiveReq .. kLiveBoxWords layout)
   uint32_t *dbox = nullptr;            // its device address
-  unsigned char *d = nullptr;          // flag | states | hist | rounds | live ids | init plane | init x | pool
+  unsigned char *d = nullptr;          // flag | states | hist | rounds | live ids | init x | stops | pool
   size_t bytes = 0;
   std::vector<unsigned char> h;        // host staging of the buffer's head
 };
+constexpr size_t kSlotKeepBytes = 64u << 20;
 std::mutex g_slots_mu;
 std::vector<LiveSlot *> g_free_slots;
+
+// Where the run's results sit in the slot's buffer.
+struct WgRun {
+  size_t o_st = 0, o_r = 0;            // states [N], round word (the head read back ends after it)
+};
 }  // namespace
 
-// A live run (bo_consensus_start_live): the event-level kernel runs on its
-// slot's stream while the caller serves /stop, /getState and /status; GET
-// /stop requests reach the running kernel through the slot's mailbox.
+// A live run (bo_consensus_start_live): the workgroup-batched event kernel
+// (benor_event_live.hip) runs on its slot's stream while the caller serves
+// /stop, /getState and /status; GET /stop requests and /getState snapshot
+// requests reach the running kernel through the slot's mailbox.  Shared by the
+// network and by every caller that reads its mailbox (snapshots), so the slot
+// goes back to the pool only when the last of them is done.
 struct bo_live {
   LiveSlot *slot = nullptr;
-  bo_plan pl;                          // device tables: views into the slot's buffer
-  uint32_t *box = nullptr;             // slot->box
-  size_t o_st = 0, o_r = 0;            // offsets of the states and the round word
-  std::vector<uint32_t> active;
+  WgRun run;
+  std::vector<uint32_t> active;        // the nodes that run
+  bool failed = false;                 // the run's stream reported an error: the slot is not reused
+  ~bo_live();
 };
 
 namespace {
 // Post GET /stop requests to a live run (caller holds net->mu): the nodes'
-// request bits first, then the sequence word the kernel polls.
+// request bits, which the kernel's control wave polls.
 void live_post(bo_live *lr, const uint32_t *ids, uint32_t n) {
+  uint32_t *box = lr->slot->box;
   for (uint32_t j = 0; j < n; ++j)
-    __atomic_fetch_or(&lr->box[benor::kLiveReq + (ids[j] >> 5)], 1u << (ids[j] & 31u), __ATOMIC_RELAXED);
-  __atomic_fetch_add(&lr->box[0], 1u, __ATOMIC_RELEASE);
+    __atomic_fetch_or(&box[benor::kLiveReq + (ids[j] >> 5)], 1u << (ids[j] & 31u), __ATOMIC_RELEASE);
 }
 }  // namespace
 
@@ -235,12 +254,27 @@ int bo_status(const bo_network *net, uint32_t i) {   // node.ts:33-39
   return net->st[i].killed ? 500 : 200;
 }
 
+namespace {
+int get_states_impl(bo_network *net, bo_node_state *out, uint64_t *events_out);
+}  // namespace
+
+// GET /getState answers at once with the node's current state (node.ts:197-199):
+// during a live run, from a snapshot the kernel takes at its next batch
+// boundary (bo_get_states).
 int bo_get_state(const bo_network *net, uint32_t i, bo_node_state *out) {   // node.ts:197-199
   if (!net || !out) return fail(BO_ERR_INVALID_ARGUMENT, "NULL argument");
   if (i >= net->N) return fail(BO_ERR_OUT_OF_RANGE, "node index out of range");
-  std::lock_guard<std::mutex> g(net->mu);
-  *out = net->st[i];
-  return BO_OK;
+  {
+    std::lock_guard<std::mutex> g(net->mu);
+    if (!net->live) {
+      *out = net->st[i];
+      return net->live_rc;
+    }
+  }
+  std::vector<bo_node_state> all(net->N);
+  const int rc = get_states_impl(const_cast<bo_network *>(net), all.data(), nullptr);
+  *out = all[i];
+  return rc;
 }
 
 int bo_node_stop(bo_network *net, uint32_t i) {   // node.ts:191-194
@@ -248,7 +282,7 @@ int bo_node_stop(bo_network *net, uint32_t i) {   // node.ts:191-194
   if (i >= net->N) return fail(BO_ERR_OUT_OF_RANGE, "node index out of range");
   std::lock_guard<std::mutex> g(net->mu);
   net->st[i].killed = 1;
-  if (net->live) live_post(net->live, &i, 1u);
+  if (net->live) live_post(net->live.get(), &i, 1u);
   return BO_OK;
 }
 
@@ -259,7 +293,7 @@ int bo_consensus_stop(bo_network *net) {   // consensus.ts:10-15
   if (net->live) {
     std::vector<uint32_t> all(net->N);
     for (uint32_t i = 0; i < net->N; ++i) all[i] = i;
-    live_post(net->live, all.data(), net->N);
+    live_post(net->live.get(), all.data(), net->N);
   }
   return BO_OK;
 }
@@ -364,6 +398,10 @@ void merge_states(bo_network *net, const std::vector<uint32_t> &active, const st
 }
 }  // namespace
 
+namespace {
+int run_sched_wg(const bo_trials_cfg *cfg, std::vector<bo_node_state> &states);
+}  // namespace
+
 // startConsensus with GET /stop requests landing during the run (node.ts:191-194
 // served while the round loop is in flight).  Without a schedule: the lockstep
 // round loop (every running node hears every running node).  With
@@ -379,7 +417,9 @@ int bo_consensus_start_sched(bo_network *net, uint64_t seed, uint32_t k_max, con
   const bo_trials_cfg cfg = start_cfg(net, seed, k_max, sp, sp.scheduled ? BO_MODE_EVENT : BO_MODE_LOCKSTEP);
   std::vector<bo_node_state> states(net->N);
   uint32_t rounds = 0;
-  rc = bo_run_trial_states(&cfg, 0, states.data(), &rounds);
+  // a schedule: one trial of the workgroup-batched event kernel; none: the
+  // lockstep round loop
+  rc = sp.scheduled ? run_sched_wg(&cfg, states) : bo_run_trial_states(&cfg, 0, states.data(), &rounds);
   std::lock_guard<std::mutex> g(net->mu);
   net->in_flight = false;
   if (rc) {
@@ -970,6 +1010,13 @@ int bo_run_trial_states(const bo_trials_cfg *cfg, uint64_t trial, bo_node_state 
 
 // ------------------------------------------------------------ live runs
 namespace {
+void slot_destroy(LiveSlot *sl) {
+  if (sl->d) (void)hipFree(sl->d);
+  if (sl->box) (void)hipHostFree(sl->box);
+  if (sl->s) (void)hipStreamDestroy(sl->s);
+  delete sl;
+}
+
 LiveSlot *slot_acquire(int dev) {
   {
     std::lock_guard<std::mutex> g(g_slots_mu);
@@ -982,58 +1029,56 @@ LiveSlot *slot_acquire(int dev) {
   }
   auto *sl = new LiveSlot();
   sl->device = dev;
-  const size_t box_bytes = sizeof(uint32_t) * (benor::kLiveEv + BO_MAX_N);
+  const size_t box_bytes = sizeof(uint32_t) * benor::kLiveBoxWords;
   if (hipStreamCreateWithFlags(&sl->s, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void **>(&sl->box), box_bytes, hipHostMallocMapped | hipHostMallocCoherent) !=
           hipSuccess ||
       hipHostGetDevicePointer(reinterpret_cast<void **>(&sl->dbox), sl->box, 0) != hipSuccess) {
-    if (sl->box) (void)hipHostFree(sl->box);
-    if (sl->s) (void)hipStreamDestroy(sl->s);
-    delete sl;
+    slot_destroy(sl);
     return nullptr;
   }
   return sl;
 }
 
+// Back to the pool after its run ended (the stream is idle): a large buffer is
+// freed rather than kept (k concurrent N = 4096 runs kept k
+// message pools of 268 MB for the life of the process).
 void slot_release(LiveSlot *sl) {
   if (!sl) return;
+  if (sl->bytes > kSlotKeepBytes) {
+    (void)hipFree(sl->d);
+    sl->d = nullptr;
+    sl->bytes = 0;
+  }
   std::lock_guard<std::mutex> g(g_slots_mu);
   g_free_slots.push_back(sl);
 }
 
-void live_free(bo_live *lr) {
-  if (!lr) return;
-  if (lr->slot) {
-    (void)hipStreamSynchronize(lr->slot->s);   // the kernel no longer reads the mailbox or the buffer
-    slot_release(lr->slot);
-  }
-  delete lr;
-}
-
 size_t align_up(size_t v, size_t a) { return (v + a - 1u) & ~(a - 1u); }
 
-// Plan (host), slot, one upload and the launch on the slot's stream.
-int live_launch(bo_live *lr, const bo_trials_cfg *cfg) {
-  std::vector<uint32_t> live;
+// One trial of a network on the workgroup-batched event kernel
+// (benor_event_live.hip), on the slot's stream: the plan (host), the slot's
+// buffer -- flag | states [N] | hist [H] | rounds | live ids [m] | init x [N]
+// | stop schedule | message pool (HBM form only) -- one upload and the launch.
+// `live`: the kernel polls the slot's mailbox for GET /stop and /getState.
+int wg_launch(LiveSlot *sl, const bo_trials_cfg *cfg, bool live, WgRun &run) {
+  std::vector<uint32_t> ids;
   std::vector<uint4> plane;
   benor::KParams kp;
-  int rc = plan_host(cfg, live, plane, kp, true);
+  int rc = plan_host(cfg, ids, plane, kp, true);
   if (rc) return rc;
-  int dev = 0;
-  rc = check_device(&dev);
-  if (rc) return rc;
-  LiveSlot *sl = slot_acquire(dev);
-  if (!sl) return fail(BO_ERR_HIP, "live run: stream / mailbox allocation failed");
-  lr->slot = sl;
-  lr->box = sl->box;
   const uint32_t N = cfg->N, H = bo_hist_len(cfg->k_max), m = kp.m;
-  // layout: flag | states [N] | hist [H] u64 | rounds | live [m] | init [W] uint4 | init x [N] | pool
+  std::vector<uint64_t> stops;
+  if (cfg->crash_at)
+    for (uint32_t i = 0; i < N; ++i)
+      if (cfg->crash_at[i] != 0xFFFFFFFFu) stops.push_back(((uint64_t)cfg->crash_at[i] << 12) | i);
+  std::sort(stops.begin(), stops.end());
   const size_t o_st = 16u, o_h = align_up(o_st + sizeof(bo_node_state) * N, 16u);
   const size_t o_r = o_h + sizeof(uint64_t) * H, o_live = align_up(o_r + 4u, 16u);
-  const size_t o_init = align_up(o_live + sizeof(uint32_t) * m, 16u);
-  const size_t o_ix = o_init + sizeof(uint4) * plane.size();
-  const size_t o_pool = align_up(o_ix + N, 256u);
-  const size_t bytes = o_pool + (size_t)kp.ev_stride * 4u;
+  const size_t o_ix = align_up(o_live + sizeof(uint32_t) * m, 16u);
+  const size_t o_stops = align_up(o_ix + N, 16u);
+  const size_t o_pool = align_up(o_stops + sizeof(uint64_t) * stops.size(), 256u);
+  const size_t bytes = o_pool + (benor::event_wg_lds_pool(kp) ? 0u : (size_t)kp.ev_cap * 4u);
   if (sl->bytes < bytes) {
     if (sl->d) (void)hipFree(sl->d);
     sl->d = nullptr;
@@ -1045,105 +1090,235 @@ int live_launch(bo_live *lr, const bo_trials_cfg *cfg) {
   std::vector<bo_node_state> st;
   initial_states(cfg, st);
   std::memcpy(sl->h.data() + o_st, st.data(), sizeof(bo_node_state) * N);
-  if (m) std::memcpy(sl->h.data() + o_live, live.data(), sizeof(uint32_t) * m);
-  if (!plane.empty()) std::memcpy(sl->h.data() + o_init, plane.data(), sizeof(uint4) * plane.size());
-  if (cfg->init_mode == BO_INIT_FIXED) std::memcpy(sl->h.data() + o_ix, cfg->init, N);
-  // the mailbox: no request, no stop landed (the previous run's kernel has ended)
-  std::memset(sl->box, 0, sizeof(uint32_t) * benor::kLiveEv);
-  for (uint32_t i = 0; i < N; ++i) sl->box[benor::kLiveEv + i] = 0xFFFFFFFFu;
+  if (m) std::memcpy(sl->h.data() + o_live, ids.data(), sizeof(uint32_t) * m);
+  std::memcpy(sl->h.data() + o_ix, cfg->init, N);
+  if (!stops.empty()) std::memcpy(sl->h.data() + o_stops, stops.data(), sizeof(uint64_t) * stops.size());
+  if (live) {
+    // the mailbox: no request, no stop landed, no snapshot asked (the slot's
+    // previous kernel has ended)
+    std::memset(sl->box, 0, sizeof(uint32_t) * benor::kLiveEv);
+    for (uint32_t i = 0; i < N; ++i) sl->box[benor::kLiveEv + i] = 0xFFFFFFFFu;
+    std::memset(sl->box + benor::kSnapReq, 0, sizeof(uint32_t) * (benor::kSnapSt - benor::kSnapReq));
+  }
   HIP_TRY(hipMemcpyAsync(sl->d, sl->h.data(), o_pool, hipMemcpyHostToDevice, sl->s));
-  bo_plan &pl = lr->pl;
-  pl.cfg = *cfg;
-  pl.cfg.faulty = nullptr;
-  pl.cfg.init = nullptr;
-  pl.cfg.crash_at = nullptr;
-  pl.device = dev;
-  pl.live_ids = live;
-  pl.kp = kp;
-  pl.d_flag = reinterpret_cast<uint32_t *>(sl->d);
-  pl.kp.live_ids = reinterpret_cast<uint32_t *>(sl->d + o_live);
-  pl.kp.init_plane = reinterpret_cast<uint4 *>(sl->d + o_init);
-  pl.kp.init_x = reinterpret_cast<int8_t *>(sl->d + o_ix);
-  pl.kp.scratch = reinterpret_cast<uint32_t *>(sl->d + o_pool);
-  pl.kp.ev_lanes = 1u;                           // one trial
-  pl.kp.live_box = sl->dbox;
-  lr->o_st = o_st;
-  lr->o_r = o_r;
-  return plan_launch_impl(&pl, 0, 1, reinterpret_cast<uint64_t *>(sl->d + o_h),
-                          reinterpret_cast<bo_node_state *>(sl->d + o_st), reinterpret_cast<uint32_t *>(sl->d + o_r),
-                          sl->s);
+  kp.hist = reinterpret_cast<unsigned long long *>(sl->d + o_h);
+  kp.overflow = reinterpret_cast<uint32_t *>(sl->d);
+  kp.node_out = reinterpret_cast<bo_node_state *>(sl->d + o_st);
+  kp.rounds_out = reinterpret_cast<uint32_t *>(sl->d + o_r);
+  kp.live_ids = reinterpret_cast<uint32_t *>(sl->d + o_live);
+  kp.init_x = reinterpret_cast<int8_t *>(sl->d + o_ix);
+  kp.ev_stops = reinterpret_cast<uint64_t *>(sl->d + o_stops);
+  kp.ev_nstops = (uint32_t)stops.size();
+  kp.scratch = reinterpret_cast<uint32_t *>(sl->d + o_pool);
+  kp.ev_lanes = 1u;                              // one trial
+  kp.live_box = live ? sl->dbox : nullptr;
+  kp.trial_begin = 0;
+  kp.trial_count = 1;
+  run.o_st = o_st;
+  run.o_r = o_r;
+  HIP_TRY(benor::launch_event_wg(kp, 1, sl->s));
+  return BO_OK;
+}
+
+// The run's head (flag | states | hist | rounds), read back on the slot's stream.
+int wg_read(LiveSlot *sl, const WgRun &run, uint32_t N, std::vector<bo_node_state> &states) {
+  std::vector<unsigned char> head(run.o_r + 4u);
+  hipError_t e = hipMemcpyAsync(head.data(), sl->d, head.size(), hipMemcpyDeviceToHost, sl->s);
+  if (e == hipSuccess) e = hipStreamSynchronize(sl->s);
+  if (e != hipSuccess) return hip_fail(e, "event-level run");
+  uint32_t flag = 0, rounds = 0;
+  std::memcpy(&flag, head.data(), 4u);
+  std::memcpy(&rounds, head.data() + run.o_r, 4u);
+  states.resize(N);
+  std::memcpy(states.data(), head.data() + run.o_st, sizeof(bo_node_state) * N);
+  int rc = plan_flag_error(flag);
+  if (!rc && (rounds & 0x80000000u))
+    rc = fail(BO_ERR_INTERNAL, "event-level message pool filled up: the run stopped early");
+  return rc;
+}
+
+// bo_consensus_start_sched with a /stop schedule: one trial on the
+// workgroup-batched event kernel, synchronously.
+int run_sched_wg(const bo_trials_cfg *cfg, std::vector<bo_node_state> &states) {
+  int dev = 0;
+  int rc = check_device(&dev);
+  if (rc) return rc;
+  LiveSlot *sl = slot_acquire(dev);
+  if (!sl) return fail(BO_ERR_HIP, "event-level run: stream allocation failed");
+  WgRun run;
+  rc = wg_launch(sl, cfg, false, run);
+  if (!rc) rc = wg_read(sl, run, cfg->N, states);
+  if (hipStreamSynchronize(sl->s) == hipSuccess && rc != BO_ERR_HIP) slot_release(sl);
+  else slot_destroy(sl);
+  return rc;
+}
+
+// The end of a live run whose stream reported `e` (hipStreamSynchronize or a
+// finished hipStreamQuery): read back, merge the final states, forget the run.
+// Idempotent -- the first caller finalizes, later ones get its result.
+int live_finalize(bo_network *net, const std::shared_ptr<bo_live> &lr, hipError_t e) {
+  std::lock_guard<std::mutex> w(net->wait_mu);
+  {
+    std::lock_guard<std::mutex> g(net->mu);
+    if (net->live != lr) return net->live_rc;
+  }
+  const uint32_t N = net->N;
+  std::vector<bo_node_state> states;
+  int rc = e != hipSuccess ? hip_fail(e, "bo_consensus_wait") : wg_read(lr->slot, lr->run, N, states);
+  if (rc == BO_ERR_HIP) lr->failed = true;       // the slot's stream is not trusted again
+  std::lock_guard<std::mutex> g(net->mu);
+  net->live.reset();                             // from here a /stop is ordered after the run
+  net->in_flight = false;
+  net->live_rc = rc;
+  if (!rc) {
+    net->stop_events.assign(lr->slot->box + benor::kLiveEv, lr->slot->box + benor::kLiveEv + N);
+    merge_states(net, lr->active, states);
+  }
+  return rc;
 }
 }  // namespace
+
+bo_live::~bo_live() {
+  if (!slot) return;
+  if (failed || hipStreamSynchronize(slot->s) != hipSuccess) {
+    // a faulted or aborted run: its stream, mailbox and buffer are not reused
+    slot_destroy(slot);
+  } else {
+    slot_release(slot);
+  }
+}
 
 // startConsensus whose GET /stop requests land while it runs (node.ts:191-194
 // served during the round loop): the event-level kernel is launched and the
 // call returns, as the reference's GET /start answers before consensus
 // finishes (node.ts:167-188).  bo_node_stop / bo_consensus_stop post to the
-// running kernel; bo_consensus_wait ends the run.
+// running kernel, bo_get_state(s) answer from its snapshots, and
+// bo_consensus_wait / bo_consensus_poll end the run.
 int bo_consensus_start_live(bo_network *net, uint64_t seed, uint32_t k_max) {
   StartPlan sp;
   int rc = start_prologue(net, k_max, nullptr, 0u, sp);
   if (rc || !sp.launch) return rc;
   const bo_trials_cfg cfg = start_cfg(net, seed, k_max, sp, BO_MODE_EVENT);
-  auto *lr = new bo_live();
+  int dev = 0;
+  rc = check_device(&dev);
+  auto lr = std::make_shared<bo_live>();
   lr->active = sp.active;
-  rc = live_launch(lr, &cfg);
+  if (!rc) {
+    lr->slot = slot_acquire(dev);
+    if (!lr->slot) rc = fail(BO_ERR_HIP, "live run: stream / mailbox allocation failed");
+  }
+  if (!rc) rc = wg_launch(lr->slot, &cfg, true, lr->run);
   std::lock_guard<std::mutex> g(net->mu);
   if (rc) {
-    live_free(lr);
+    if (rc == BO_ERR_HIP) lr->failed = true;
     net->in_flight = false;
     net->started = false;          // nothing ran: the start may be retried
     return rc;
   }
   net->live = lr;
+  net->live_rc = 0;
   net->stop_events.clear();
   // stops served between the prologue and now reach the kernel too
   std::vector<uint32_t> late;
   for (uint32_t i : sp.active)
     if (net->st[i].killed) late.push_back(i);
-  if (!late.empty()) live_post(lr, late.data(), (uint32_t)late.size());
+  if (!late.empty()) live_post(lr.get(), late.data(), (uint32_t)late.size());
   return BO_OK;
 }
 
 int bo_consensus_wait(bo_network *net) {
   if (!net) return fail(BO_ERR_INVALID_ARGUMENT, "net is NULL");
-  std::lock_guard<std::mutex> w(net->wait_mu);
-  bo_live *lr = nullptr;
+  std::shared_ptr<bo_live> lr;
   {
     std::lock_guard<std::mutex> g(net->mu);
     lr = net->live;
   }
   if (!lr) return BO_OK;
-  const uint32_t N = net->N;
-  LiveSlot *sl = lr->slot;
-  // one stream-ordered read-back of flag | states | hist | rounds
-  std::vector<unsigned char> head(lr->o_r + 4u);
-  hipError_t e = hipMemcpyAsync(head.data(), sl->d, head.size(), hipMemcpyDeviceToHost, sl->s);
-  if (e == hipSuccess) e = hipStreamSynchronize(sl->s);
-  std::vector<bo_node_state> states(N);
-  uint32_t rounds = 0, flag = 0;
-  int rc = BO_OK;
-  if (e != hipSuccess) {
-    rc = hip_fail(e, "bo_consensus_wait");
-  } else {
-    std::memcpy(&flag, head.data(), 4u);
-    std::memcpy(states.data(), head.data() + lr->o_st, sizeof(bo_node_state) * N);
-    std::memcpy(&rounds, head.data() + lr->o_r, 4u);
-    rc = plan_flag_error(flag);
-  }
-  if (!rc && (rounds & 0x80000000u))
-    rc = fail(BO_ERR_INTERNAL, "event-level message pool filled up: the run stopped early");
+  const hipError_t e = hipStreamSynchronize(lr->slot->s);   // no lock held: /stop, /getState stay served
+  return live_finalize(net, lr, e);
+}
+
+int bo_consensus_poll(bo_network *net, int *running_out) {
+  if (!net || !running_out) return fail(BO_ERR_INVALID_ARGUMENT, "NULL argument");
+  *running_out = 0;
+  std::shared_ptr<bo_live> lr;
   {
     std::lock_guard<std::mutex> g(net->mu);
-    net->live = nullptr;           // from here a /stop is ordered after the run
-    net->in_flight = false;
-    if (!rc) {
-      net->stop_events.assign(lr->box + benor::kLiveEv, lr->box + benor::kLiveEv + N);
-      merge_states(net, lr->active, states);
+    lr = net->live;
+  }
+  if (!lr) return BO_OK;
+  const hipError_t e = hipStreamQuery(lr->slot->s);
+  if (e == hipErrorNotReady) {
+    *running_out = 1;
+    return BO_OK;
+  }
+  return live_finalize(net, lr, e);
+}
+
+namespace {
+// Every node's state into out[N]: the network's own states, or -- while a live
+// run is in flight -- a snapshot the kernel takes at its next batch boundary
+// (the delivery count it reflects in *events_out), with the killed flags of
+// GET /stop requests it has not applied yet (node.ts:191-194 sets killed at
+// once).  A run that ends before it answers is finalized and its final states
+// returned.
+int get_states_impl(bo_network *net, bo_node_state *out, uint64_t *events_out) {
+  if (events_out) *events_out = UINT64_MAX;
+  std::shared_ptr<bo_live> lr;
+  {
+    std::lock_guard<std::mutex> g(net->mu);
+    lr = net->live;
+    if (!lr) {
+      std::copy(net->st.begin(), net->st.end(), out);
+      return net->live_rc;
     }
   }
-  live_free(lr);
+  LiveSlot *sl = lr->slot;
+  hipError_t q = hipStreamQuery(sl->s);
+  if (q == hipErrorNotReady) {
+    std::lock_guard<std::mutex> s(net->snap_mu);
+    uint32_t *box = sl->box;
+    const uint32_t want = __atomic_add_fetch(&box[benor::kSnapReq], 1u, __ATOMIC_RELEASE);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 0;; ++spin) {
+      if (__atomic_load_n(&box[benor::kSnapSeq], __ATOMIC_ACQUIRE) == want) {
+        const uint64_t e = (uint64_t)__atomic_load_n(&box[benor::kSnapE], __ATOMIC_RELAXED) |
+                           ((uint64_t)__atomic_load_n(&box[benor::kSnapE + 1u], __ATOMIC_RELAXED) << 32);
+        std::lock_guard<std::mutex> g(net->mu);
+        std::copy(net->st.begin(), net->st.end(), out);   // nodes that do not run keep theirs
+        for (uint32_t i : lr->active) {
+          const uint32_t w0 = box[benor::kSnapSt + 2u * i], w1 = box[benor::kSnapSt + 2u * i + 1u];
+          bo_node_state s;
+          s.killed = (int8_t)((w0 & 0xFFu) | (uint32_t)(net->st[i].killed != 0));
+          s.x = (int8_t)(w0 >> 8);
+          s.decided = (int8_t)(w0 >> 16);
+          s.pad = 0;
+          s.k = (int32_t)w1;
+          out[i] = s;
+        }
+        if (events_out) *events_out = e;
+        return BO_OK;
+      }
+      if ((spin & 63u) == 63u) {
+        q = hipStreamQuery(sl->s);
+        if (q != hipErrorNotReady) break;          // the run ended before it served the request
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
+          return fail(BO_ERR_INTERNAL, "a live run did not serve a /getState snapshot within 10 s");
+        std::this_thread::yield();
+      }
+    }
+  }
+  const int rc = live_finalize(net, lr, q);
+  std::lock_guard<std::mutex> g(net->mu);
+  std::copy(net->st.begin(), net->st.end(), out);
   return rc;
+}
+}  // namespace
+
+int bo_get_states(const bo_network *net, bo_node_state *out, uint32_t n, uint64_t *events_out) {
+  if (!net || !out) return fail(BO_ERR_INVALID_ARGUMENT, "NULL argument");
+  if (n != net->N) return fail(BO_ERR_INVALID_ARGUMENT, "out must have N entries");
+  return get_states_impl(const_cast<bo_network *>(net), out, events_out);
 }
 
 int bo_live_stop_events(const bo_network *net, uint32_t *events_out, uint32_t n) {

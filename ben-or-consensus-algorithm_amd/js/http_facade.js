@@ -48,8 +48,9 @@ async function launchNetwork(N, F, initialValues, faultyList, options = {}) {
   // The run starts when every running node has served /start, and /start
   // answers at once (node.ts:167-188 answers before consensus finishes); a
   // GET /stop served over HTTP while it runs lands in the kernel
-  // (bo_consensus_start_live), and /getState shows the final states once the
-  // run has ended -- the reference's callers poll it.
+  // (bo_consensus_start_live), and /getState answers at once with a snapshot
+  // of the running network, then its final states -- the reference's callers
+  // poll it.
   // options.sync: /start answers once the run has finished; a /stop arriving
   // over HTTP while it is in flight is ordered after it.
   // options.stopAfter: GET /stop requests that land during the run, as delivery
@@ -61,7 +62,8 @@ async function launchNetwork(N, F, initialValues, faultyList, options = {}) {
     sched = stopSchedule(N, options.stopAfter);
   }
   if (options.live && options.sync) throw new RangeError('live and sync are exclusive');
-  const live = sched === undefined && !options.sync;
+  // an explicit {live: false} is the run-to-completion form, as {sync: true}
+  const live = sched === undefined && !options.sync && options.live !== false;
   const handle = addon.networkCreate(N, F, initialValues, faultyList);   // launchNodes.ts:10-13 errors
   const net = {
     handle, N, started: new Array(N).fill(false), running: null, ran: false, seed: options.seed,
@@ -69,7 +71,7 @@ async function launchNetwork(N, F, initialValues, faultyList, options = {}) {
 
   const runningNodes = () => {
     const r = [];
-    for (let i = 0; i < N; i++) if (!addon.getState(handle, i).killed) r.push(i);
+    for (let i = 0; i < N; i++) if (addon.status(handle, i) !== 500) r.push(i);
     return r;
   };
 
@@ -99,9 +101,11 @@ async function launchNetwork(N, F, initialValues, faultyList, options = {}) {
     return net.running;
   }
 
+  // GET /getState (node.ts:197-199) answers at once: a live run in flight
+  // serves a snapshot of the running kernel (bo_get_state)
   function state(i) {
     const s = addon.getState(handle, i);
-    if (!net.ran && net.started[i] && !s.killed) s.k = 1;   // node.ts:172, before the run lands
+    if (!net.ran && !(live && net.running) && net.started[i] && !s.killed) s.k = 1;   // node.ts:172, before the run lands
     return s;
   }
 
@@ -123,19 +127,17 @@ async function launchNetwork(N, F, initialValues, faultyList, options = {}) {
         return send(res, 200, 'killed');
       }
       if (req.method === 'GET' && url === '/start') {
-        if (!addon.getState(handle, i).killed) net.started[i] = true;
+        if (addon.status(handle, i) !== 500) net.started[i] = true;
         const p = maybeRun();
         const reply = () => send(res, 200, { message: 'Algorithm started' }, true);
-        // respond once the round loop has landed, so a caller that polls
-        // /getState right after startConsensus sees final states (live: once
-        // the kernel is launched)
+        // respond once the round loop is launched (live), or has run (sync)
         if (p) p.then(reply, (e) => send(res, 500, { message: String(e && e.message) }, true));
         else reply();
         return undefined;
       }
       if (req.method === 'POST' && url === '/message') {
         req.resume();
-        if (addon.getState(handle, i).killed) return undefined;   // node.ts:45,161: no reply
+        if (addon.status(handle, i) === 500) return undefined;   // node.ts:45,161: no reply
         return send(res, 200, { message: 'Message received' }, true);
       }
       return send(res, 404, 'not found');

@@ -52,13 +52,17 @@ export interface StartOptions {
 }
 
 /** Resolves once the round loop is launched (before consensus finishes, like GET /start);
- * stopNode / stopConsensus then land in the running kernel, and getNodesState / getNodeState /
- * waitConsensus wait for the run.  {sync: true}: resolves after the run. */
+ * stopNode / stopConsensus then land in the running kernel, getNodesState / getNodeState answer
+ * at once with a snapshot of the running network (GET /getState, node.ts:197-199), and
+ * waitConsensus waits for the end of the run.  {sync: true}: resolves after the run. */
 export declare function startConsensus(N: number, options?: StartOptions): Promise<void>;
 export declare function stopConsensus(N: number): Promise<void>;
 export declare function stopNode(nodeId: number): Promise<void>;
 export declare function getNodeState(nodeId: number): Promise<NodeState>;
 export declare function getNodesState(N: number): Promise<NodeState[]>;
+/** getNodesState with the delivery count a live run's snapshot reflects (null when no run is in
+ * flight): the states are oracle (iii) truncated before that many POST /message deliveries. */
+export declare function getNodesStateAt(N: number): Promise<{ states: NodeState[]; events: number | null }>;
 export declare function getNodeStatus(nodeId: number): Promise<{ status: 200 | 500; body: "live" | "faulty" }>;
 export declare function reachedFinality(states: NodeState[]): boolean;
 export declare function delay(ms: number): Promise<void>;

@@ -66,8 +66,10 @@ function randomSeed() {
 // (bo_consensus_start_live), before consensus finishes (node.ts:167-188
 // answers right after the round-1 broadcasts).  A stopConsensus / stopNode sent
 // afterwards lands in the running kernel before its next delivery (node.ts:45,
-// :191-194); getNodesState / getNodeState / waitConsensus wait for the run to
-// end, so the reference's start-then-poll callers see final states.
+// :191-194); getNodesState / getNodeState answer at once, as GET /getState does
+// (node.ts:197-199), with a snapshot of the running network, so the reference's
+// start-then-poll callers see the run progress and then its final states;
+// waitConsensus(N) waits for the end.
 // liveStopEvents(N) gives the delivery count at which each /stop landed
 // (replayable as stopAfter on a fresh network with the same seed).
 // options.sync: resolve when the round loop has run to completion (every live
@@ -90,13 +92,14 @@ async function startConsensus(N, options = {}) {
     sched = stopSchedule(N, options.stopAfter);
   }
   if (options.live && options.sync) throw new RangeError('live and sync are exclusive');
-  const live = sched === undefined && !options.sync;
+  // an explicit {live: false} is the run-to-completion form, as {sync: true}
+  const live = sched === undefined && !options.sync && options.live !== false;
   const cur = net(N);
   try {
     if (live) {
       addon.networkStartLive(cur.handle, seed, kMax);
-      // kept until the network is replaced: every reader waits for it, and a
-      // failed run fails every later read rather than serving pre-run states
+      // the end of the run, for waitConsensus / liveStopEvents (a failed run
+      // also fails every later getNodeState / getNodesState, in libbenor)
       cur.running = addon.networkWait(cur.handle);
       cur.running.catch(() => {});
       return;
@@ -132,19 +135,21 @@ async function stopConsensus(N) {
 
 async function stopNode(nodeId) { addon.nodeStop(net().handle, nodeId); }
 
+// GET /getState (node.ts:197-199): at once, the node's current state (a
+// snapshot of a live run in flight; its final state once the run has ended).
 async function getNodeState(nodeId) {
-  const cur = net();
-  await settle(cur);
-  return addon.getState(cur.handle, nodeId);
+  return addon.getState(net().handle, nodeId);
 }
 
+// __test__/tests/utils.ts:14-20: every node's state, from one snapshot.
 async function getNodesState(N) {
-  const cur = net(N);
-  await settle(cur);
-  const h = cur.handle;
-  const out = [];
-  for (let i = 0; i < N; i++) out.push(addon.getState(h, i));
-  return out;
+  return addon.getStates(net(N).handle).states;
+}
+
+// The same with the delivery count a live run's snapshot reflects (null when
+// no run is in flight): oracle (iii) truncated there gives the states.
+async function getNodesStateAt(N) {
+  return addon.getStates(net(N).handle);
 }
 
 // GET /status: { status: 500, body: "faulty" } | { status: 200, body: "live" }
@@ -166,5 +171,5 @@ const delay = (ms) => new Promise((res) => setTimeout(res, ms));   // src/utils.
 module.exports = {
   BASE_NODE_PORT, DEFAULT_K_MAX, launchNetwork, startConsensus, stopConsensus, stopNode,
   getNodeState, getNodesState, getNodeStatus, reachedFinality, runTrials, delay,
-  waitConsensus, liveStopEvents,
+  waitConsensus, liveStopEvents, getNodesStateAt,
 };

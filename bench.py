@@ -341,15 +341,16 @@ def event_network(benor, N=1024, F=341, stop_node=500, stop_after=300_000, seed=
         st = benor.getNodesState(N)
         out[label] = {"seconds": dt, "stopped_nodes": sum(1 for s in st[F:] if s["killed"])}
     # the default start (bo_consensus_start_live): startConsensus returns at
-    # launch, the /stop is sent 5 ms later and lands in the running kernel; the
-    # run ends at getNodesState.  Reported: the wall time from the start to the
+    # launch, the /stop is sent 1 ms later and lands in the running kernel; the
+    # run ends at waitConsensus.  Reported: the wall time from the start to the
     # final states and where the stop landed (replayable as a schedule).
     benor.launchNetwork(N, F, init, faulty)
     t0 = time.perf_counter()
     benor.startConsensus(N, seed=seed)
     t_start = time.perf_counter() - t0
-    time.sleep(0.005)                                # the run is under way: the stop lands mid-round
+    time.sleep(0.001)                                # the run is under way: the stop lands mid-round
     benor._current.stop_node(stop_node)
+    benor.waitConsensus(N)
     st = benor.getNodesState(N)
     dt = time.perf_counter() - t0
     landed = benor._current.live_stop_events()[stop_node]
@@ -364,7 +365,7 @@ def network_latency(benor, reps=200):
     initial values [1,1,1,0,0], benorconsensus.test.ts:179-223) through the
     reference's own calls -- launchNetwork + startConsensus + getNodesState --
     on the GPU; median and p90 wall time over `reps` networks, for the default
-    start (resolves at launch, getNodesState waits for the run) and the sync one."""
+    start (resolves at launch; waitConsensus, then the final states) and the sync one."""
     out = {"networks": reps}
     for label, kw in (("default", {}), ("sync", {"sync": True})):
         times = []
@@ -372,6 +373,7 @@ def network_latency(benor, reps=200):
             t0 = time.perf_counter()
             benor.launchNetwork(5, 1, [1, 1, 1, 0, 0], [False, False, False, False, True])
             benor.startConsensus(5, seed=rep, **kw)
+            benor.waitConsensus(5)
             states = benor.getNodesState(5)
             dt = time.perf_counter() - t0
             if rep >= 5:

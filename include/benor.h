@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define BENOR_ABI_VERSION 7
+#define BENOR_ABI_VERSION 8
 
 /* Return codes.  The first two are the reference's two launch errors. */
 enum {
@@ -57,8 +57,9 @@ enum {
  * (node.ts:45-158) delivery by delivery, in a seeded random order, with the
  * reference's mid-run GET /stop (node.ts:191-194) applied at scheduled
  * delivery counts.  Exactly F crash-faulty nodes; N <= 4096 (one lane per
- * trial up to N = 256, one wave per trial above; a random /stop schedule,
- * crash_count, needs N <= 256). */
+ * trial up to N = 256, one wave per trial above).  Both /stop schedules --
+ * explicit (crash_at) and random (crash_count, crash_window) -- work at every
+ * N <= 4096. */
 enum { BO_MODE_LOCKSTEP = 0, BO_MODE_RANDOM_DELIVERY = 1, BO_MODE_EVENT = 2 };
 
 enum { BO_INIT_RANDOM = 0, BO_INIT_FIXED = 1 };
@@ -119,23 +120,34 @@ int bo_consensus_start_sched(bo_network *net, uint64_t seed, uint32_t k_max,
                              const uint32_t *stop_after, uint32_t n_stop_after);
 
 /* startConsensus(N) as the reference runs it (consensus.ts:3-8, node.ts:167-188):
- * GET /start answers before consensus finishes, and GET /stop requests served
- * while it runs land in it (node.ts:191-194, :45).  Launches the event-level
- * kernel (seeded delivery order, trial 0 of `seed`, any N <= BO_MAX_N) on its
- * own HIP stream and returns.  While it runs, bo_node_stop / bo_consensus_stop
- * also post to a host-mapped mailbox the kernel polls (every 2-10 us): a
- * request is applied before the next delivery, and that delivery count is
- * recorded (bo_live_stop_events).  bo_get_state / bo_status answer from the
- * pre-run states (killed flags include the posted stops) until
- * bo_consensus_wait merges the run's final states (a request the kernel did
- * not see before it finished is ordered after the run, as for
- * bo_consensus_start).  The one-start and auto-stop rules of
- * bo_consensus_start apply; bo_network_destroy waits for a live run. */
+ * GET /start answers before consensus finishes, and GET /stop / GET /getState
+ * requests served while it runs land in it (node.ts:191-199, :45).  Launches
+ * the event-level kernel (seeded delivery order, trial 0 of `seed`, any
+ * N <= BO_MAX_N; one workgroup of 1-15 event waves and a control wave) on its
+ * own HIP stream and returns.  While it runs:
+ *   - bo_node_stop / bo_consensus_stop also post to a host-mapped mailbox the
+ *     kernel polls (every ~5 us): a request is applied before the next
+ *     delivery, and that delivery count is recorded (bo_live_stop_events);
+ *   - bo_get_state / bo_get_states answer at once from a snapshot the kernel
+ *     writes at its next batch boundary (tens of microseconds): every node's
+ *     state as of a delivery count, with the killed flag of every /stop already
+ *     served (node.ts:191-194 sets it at once);
+ *   - bo_status answers from the killed flags.
+ * bo_consensus_wait (blocking) or bo_consensus_poll (not) end the run and merge
+ * its final states; a request the kernel did not see before it finished is
+ * ordered after the run, as for bo_consensus_start.  The one-start and
+ * auto-stop rules of bo_consensus_start apply; bo_network_destroy waits for a
+ * live run. */
 int bo_consensus_start_live(bo_network *net, uint64_t seed, uint32_t k_max);
 
 /* Wait for a live run (bo_consensus_start_live) and merge its final states;
  * BO_OK at once when none is in flight. */
 int bo_consensus_wait(bo_network *net);
+
+/* Without blocking: *running_out = 1 while a live run is in flight; once it
+ * has ended, its final states are merged (as bo_consensus_wait) and
+ * *running_out = 0. */
+int bo_consensus_poll(bo_network *net, int *running_out);
 
 /* After bo_consensus_wait: for each node, the delivery count at which a live
  * run applied its GET /stop, UINT32_MAX if it applied none (n == N).  Passed as
@@ -151,8 +163,17 @@ int bo_consensus_stop(bo_network *net);
  * run, posted to the running kernel). */
 int bo_node_stop(bo_network *net, uint32_t node);
 
-/* GET /getState (node.ts:197-199). */
+/* GET /getState (node.ts:197-199): the node's current state, answered at once
+ * (during a live run: from a snapshot, see bo_get_states). */
 int bo_get_state(const bo_network *net, uint32_t node, bo_node_state *out);
+
+/* GET /getState on every node at once (__test__/tests/utils.ts:14-20), out[n],
+ * n == N.  During a live run: one snapshot of the running kernel, taken at a
+ * batch boundary after *events_out POST /message deliveries -- exactly oracle
+ * (iii) truncated there, plus the killed flags of /stop requests served but
+ * not yet applied; otherwise the network's states and *events_out =
+ * UINT64_MAX.  events_out may be NULL. */
+int bo_get_states(const bo_network *net, bo_node_state *out, uint32_t n, uint64_t *events_out);
 
 /* GET /status (node.ts:33-39): returns 500 ("faulty") or 200 ("live"), or a
  * negative BO_ERR_* code. */

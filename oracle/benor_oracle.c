@@ -651,9 +651,12 @@ static inline int set_union_full(const orc_set *a, const orc_set *b, const orc_s
 }
 
 /* One trial.  Returns the outcome bin (index into the histogram) and fills
- * state_out[N] when given; *events_out = messages delivered. */
+ * state_out[N] when given; *events_out = messages delivered.  max_events <
+ * UINT64_MAX truncates the run before delivery max_events (after the stops
+ * scheduled there): the states of a GET /getState served at that point of a
+ * live run (bo_get_states), if the run has not halted by then. */
 static uint32_t event_trial(const orc_event_cfg *cfg, uint64_t trial, orc_node_state *st_out,
-                            uint64_t *events_out) {
+                            uint64_t *events_out, uint64_t max_events) {
     const uint32_t N = cfg->N, F = cfg->F, KR = cfg->k_max + 3;
     const int64_t quorum = (int64_t)N - (int64_t)F;
     orc_node_state *st = (orc_node_state *)malloc(sizeof(orc_node_state) * N);
@@ -742,6 +745,7 @@ static uint32_t event_trial(const orc_event_cfg *cfg, uint64_t trial, orc_node_s
             }
             if (halted) break;
         }
+        if (e >= max_events) break;                      /* a snapshot of the running network */
         if (len == 0) { halted = 3; break; }
         const uint32_t pick = (uint32_t)(((uint64_t)(uint32_t)(orc_splitmix(&rng) >> 32) * (uint64_t)len) >> 32);
         const uint32_t msg = pool[pick];
@@ -821,7 +825,7 @@ int oracle_event_trials(const orc_event_cfg *cfg, uint64_t *hist, orc_node_state
         tid = omp_get_thread_num();
 #endif
         uint64_t e = 0;
-        const uint32_t bin = event_trial(cfg, cfg->trial_begin + (uint64_t)t, node_out, &e);
+        const uint32_t bin = event_trial(cfg, cfg->trial_begin + (uint64_t)t, node_out, &e, UINT64_MAX);
         hl[(size_t)tid * HS + (bin & 0x7FFFFFFFu)]++;
         if (bin & 0x80000000u) hl[(size_t)tid * HS + HS - 1]++;
         el[tid] += e;
@@ -832,5 +836,21 @@ int oracle_event_trials(const orc_event_cfg *cfg, uint64_t *hist, orc_node_state
     }
     free(hl); free(el);
     if (events_out) *events_out = ev;
+    return 0;
+}
+
+/* The per-node states of trial `trial` before delivery max_events (a live
+ * run's GET /getState snapshot, include/benor.h bo_get_states); *halted_out =
+ * 1 when the run halted before reaching that count (the states are then the
+ * final ones).  *events_out = deliveries made. */
+int oracle_event_states_at(const orc_event_cfg *cfg, uint64_t trial, uint64_t max_events, orc_node_state *st_out,
+                           uint64_t *events_out) {
+    if (cfg->k_max < 1 || cfg->N < 1 || cfg->N > ORC_EV_MAX_N || !st_out) return -1;
+    uint32_t f = 0;
+    for (uint32_t i = 0; i < cfg->N; ++i) f += cfg->faulty[i] ? 1 : 0;
+    if (f != cfg->F) return -2;                          /* launchNodes.ts:12-13 */
+    uint64_t e = 0;
+    (void)event_trial(cfg, trial, st_out, &e, max_events);
+    if (events_out) *events_out = e;
     return 0;
 }

@@ -70,6 +70,9 @@ def lib():
         L.oracle_event_trials.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
                                           ctypes.POINTER(NodeState), ctypes.POINTER(ctypes.c_uint64)]
         L.oracle_event_trials.restype = ctypes.c_int
+        L.oracle_event_states_at.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                             ctypes.POINTER(NodeState), ctypes.POINTER(ctypes.c_uint64)]
+        L.oracle_event_states_at.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -189,6 +192,31 @@ def event_trials(N, F, faulty_list, *, seed=0, trial_begin=0, trial_count=1, k_m
     if rc != 0:
         raise ValueError(f"oracle_event_trials rc={rc}")
     return TrialsResult(hist, _states(st, N) if want_states else None), int(ev.value)
+
+
+def event_states_at(N, F, faulty_list, max_events, *, seed=0, trial=0, k_max=64, initial_values=None,
+                    crash_at=None):
+    """(iii) truncated before delivery `max_events` (after the stops scheduled
+    there): the per-node states a live run's GET /getState snapshot taken at
+    that delivery count must show (bo_get_states).  Returns (states, events
+    delivered) -- fewer events when the run halted first."""
+    f = (ctypes.c_uint8 * max(1, N))(*[1 if v else 0 for v in faulty_list])
+    if initial_values is None:
+        init, init_mode = (ctypes.c_int8 * max(1, N))(), 0
+    else:
+        init, init_mode = (ctypes.c_int8 * max(1, N))(*[VAL_CODE[v] for v in initial_values]), 1
+    ca = None
+    if crash_at is not None:
+        ca = (ctypes.c_uint32 * max(1, N))(*[NEVER if v is None else int(v) for v in crash_at])
+    cfg = EventCfg(N, F, k_max, init_mode, seed, 0, 1,
+                   ctypes.cast(f, ctypes.POINTER(ctypes.c_uint8)), ctypes.cast(init, ctypes.POINTER(ctypes.c_int8)),
+                   ctypes.cast(ca, ctypes.POINTER(ctypes.c_uint32)) if ca is not None else None, 0, 0, 1)
+    st = (NodeState * max(1, N))()
+    ev = ctypes.c_uint64(0)
+    rc = lib().oracle_event_states_at(ctypes.byref(cfg), trial, max_events, st, ctypes.byref(ev))
+    if rc != 0:
+        raise ValueError(f"oracle_event_states_at rc={rc}")
+    return _states(st, N), int(ev.value)
 
 
 def run_trials(N, F, faulty_list, *, seed=0, trial_begin=0, trial_count=1, k_max=64,

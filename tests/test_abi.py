@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol():
     L = benor.lib()
     for s in header_symbols():
         assert hasattr(L, s)
-    assert L.bo_abi_version() == 7
+    assert L.bo_abi_version() == 8
     assert L.bo_hist_len(64) == 65 * 3 + 1
 
 

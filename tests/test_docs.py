@@ -73,6 +73,27 @@ def test_profile_index_entries_exist():
     assert not missing, f"profiles/README.md indexes files that are not in profiles/: {missing}"
 
 
+# ------------------------------------------------- boundary text vs code
+def test_random_stop_schedule_limits_match_the_code():
+    """A random /stop schedule (crash_count, crash_window) is planned at every
+    N <= BO_MAX_N (bo_kernel_for: the event-level family), so neither the C ABI
+    header nor INTEGRATION.md may state a lower network-size limit for it."""
+    import benor
+
+    for N, F in ((10, 4), (256, 85), (1024, 341), (4096, 1365)):
+        k = benor.kernel_for(N, F, [i < F for i in range(N)], mode=benor.BO_MODE_EVENT, k_max=16,
+                             crash_count=3, crash_window=1000)
+        assert k == benor.BO_KERNEL_EVENT, (N, k)
+    hdr = open(os.path.join(ROOT, "include", "benor.h"), encoding="utf-8").read()
+    integ = open(os.path.join(ROOT, "INTEGRATION.md"), encoding="utf-8").read()
+    for text, name in ((hdr, "benor.h"), (integ, "INTEGRATION.md")):
+        for line in text.splitlines():
+            if "crash_count" in line:
+                assert not re.search(r"N\s*(<=|≤|<)\s*(\d+)", line) or re.search(r"N\s*(<=|≤)\s*4096", line), \
+                    f"{name}: {line.strip()}"
+    assert "needs N <= 256" not in hdr
+
+
 # ------------------------------------------------- environment knobs (VERDICT r04 #5)
 CSRC = os.path.join(ROOT, PKG, "csrc")
 

@@ -124,6 +124,7 @@ def test_reference_known_answers_network_api(reference_cases):
             statuses = [benor.getStatus(i) for i in range(N)]
             if case["start"]:
                 benor.startConsensus(N, seed=0x5EED)
+                benor.waitConsensus(N)
                 states = benor.getNodesState(N)
                 assert benor.reachedFinality(states) or any(s["decided"] is False for s in states)
                 check_reference_expectations(case, states)
@@ -160,6 +161,7 @@ def test_second_start_is_a_no_op():
     the C ABI (and strict=True) reports BO_ERR_ALREADY_STARTED."""
     benor.launchNetwork(6, 2, [0, 0, 1, 1, 0, 1], [True, False, False, False, False, True])
     benor.startConsensus(6, seed=1)
+    benor.waitConsensus(6)
     a = benor.getNodesState(6)
     benor.startConsensus(6, seed=2)
     assert benor.getNodesState(6) == a and all(s["decided"] for s in a[1:5])
@@ -195,11 +197,13 @@ def test_auto_stop_kills_every_node_when_all_decided():
     (and without nodes stopped before the run)."""
     benor.launchNetwork(5, 0, [1, 1, 0, 1, 1], [False] * 5)
     benor.startConsensus(5, seed=4)
+    benor.waitConsensus(5)
     st = benor.getNodesState(5)
     assert all(s["killed"] and s["decided"] and s["x"] == 1 and s["k"] == 2 for s in st)
     assert all(benor.getStatus(i) == (500, "faulty") for i in range(5))
     benor.launchNetwork(5, 1, [1, 1, 0, 1, 1], [False] * 4 + [True])
     benor.startConsensus(5, seed=4)
+    benor.waitConsensus(5)
     assert not any(s["killed"] for s in benor.getNodesState(5)[:4])
 
 

@@ -169,13 +169,16 @@ def test_live_stop_after_the_run_is_ordered_after_it():
 
 
 @pytest.mark.gpu
-def test_module_api_live_start_waits_in_get_nodes_state():
+def test_module_api_live_start_then_wait():
     """benor.startConsensus(N, live=True) returns before the run ends;
-    getNodesState(N) waits for it (the reference's callers poll /getState)."""
+    getNodesState(N) answers at once (a snapshot, checked in
+    test_live_snapshots_*), waitConsensus(N) gives the final states."""
     N, F, seed = 1024, 341, 65
     faulty, init = shape(N, F, half(N - F))
     benor.launchNetwork(N, F, init, faulty)
     benor.startConsensus(N, seed=seed, k_max=16, live=True)
+    assert len(benor.getNodesState(N)) == N
+    benor.waitConsensus(N)
     assert benor.getNodesState(N) == expected(N, F, faulty, init, seed, 16, None)
 
 
@@ -193,6 +196,7 @@ def test_default_start_then_stop_consensus_replays(N, F, seed):
     benor.launchNetwork(N, F, init, faulty)
     benor.startConsensus(N, seed=seed, k_max=16)
     benor.stopConsensus(N)
+    benor.waitConsensus(N)
     states = benor.getNodesState(N)
     ev = benor._current.live_stop_events()
     running = set(range(F, N))
@@ -208,8 +212,8 @@ def test_default_start_then_stop_consensus_replays(N, F, seed):
 @pytest.mark.parametrize("N,F", [(78, 26), (79, 26)])
 def test_live_pool_in_lds_and_in_hbm_replay(N, F):
     """The two forms of a live run: at N = 78 the message pool (4N^2 + 64
-    words) fits kEventBigLdsPool and a polling wave mirrors the mailbox in LDS;
-    at N = 79 the pool is in HBM and wave 0 reads the mailbox itself.  A stop
+    words) fits kEventBigLdsPool and lives in LDS; at N = 79 it is in HBM
+    (benor_event_live.hip; the control wave polls the mailbox either way).  A stop
     for a third of the running nodes sent right after the default start; the
     states equal oracle (iii)'s replay of the recorded landing points."""
     seed = 0x4C50 + N
@@ -219,6 +223,7 @@ def test_live_pool_in_lds_and_in_hbm_replay(N, F):
     stopped = set(range(F, N, 3))
     for i in sorted(stopped):
         benor._current.stop_node(i)                 # GET /stop on node i (node.ts:191-194)
+    benor.waitConsensus(N)
     states = benor.getNodesState(N)
     ev = benor._current.live_stop_events()
     assert all(ev[i] is None for i in range(F))

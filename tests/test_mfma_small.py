@@ -201,6 +201,6 @@ def test_packed_shape_network_api_states():
     """The network API's one-trial state launch of a packed shape runs the
     lane kernel: benorconsensus.test.ts "Simple Majority" states."""
     benor.launchNetwork(5, 1, [1, 1, 1, 0, 0], [False, False, False, False, True])
-    benor.startConsensus(5, seed=3)
+    benor.startConsensus(5, seed=3, sync=True)
     st = benor.getNodesState(5)
     assert all(s["decided"] and s["x"] == 1 and s["k"] == 2 for s in st[:4])

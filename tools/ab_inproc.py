@@ -1,7 +1,8 @@
 """Interleaved A/B of environment-selected variants in ONE process (GPU).
 
-The runtime reads its A/B knobs (BENOR_BIG_FORM, BENOR_COOP_BW, BENOR_COOP_NT,
-BENOR_SMALL_FORM, BENOR_BLOCKS_PER_CU, ...) at every launch, so variants can
+The runtime reads its A/B knobs (BENOR_BIG_FORM, BENOR_COOP_BW, BENOR_BLOCKS_PER_CU,
+... -- the registered ones, benor.KNOBS; any other variable is refused, since a
+removed knob would time two identical variants) at every launch, so variants can
 alternate launch by launch on one plan, one process, one box: ROUNDS rounds,
 each timing every variant once per shape in rotated order (cdna_hip_programming.md
 section 5.4 rule 24).  Each timing is REPS back-to-back launches between HIP
@@ -53,10 +54,14 @@ def main():
         shapes.append((v[0], v[1], v[2], v[3] if len(v) > 3 else v[1]))
     knobs = sorted({k for _, env in variants for k in env})
 
+    import benor
+    unknown = [k for k in knobs if k not in benor.KNOBS]
+    if unknown:
+        ap.error(f"not a registered libbenor knob (benor.KNOBS): {unknown}")
+
     import numpy as np
     import torch
 
-    import benor
     sys.path.insert(0, ROOT)
     from bench import node_rounds
 

@@ -2,8 +2,8 @@
 shape): launchNetwork(N, F, ...) + startConsensus(N) + getNodesState(N) for one
 network, as __test__/tests/benorconsensus.test.ts and src/start.ts drive it.
 Prints one JSON line per (N, start) with the median and p90 wall time in ms:
-the default start (resolves at launch, getNodesState waits for the run) and
-the sync one.
+the default start (resolves at launch; waitConsensus, then getNodesState's
+final states) and the sync one.
 
     python tools/net_latency.py [--reps 200] [--max-n 1024]
 """
@@ -36,6 +36,7 @@ def main():
                 t0 = time.perf_counter()
                 benor.launchNetwork(N, F, init, faulty)
                 benor.startConsensus(N, seed=rep, **kw)
+                benor.waitConsensus(N)
                 states = benor.getNodesState(N)
                 dt = time.perf_counter() - t0
                 if rep >= 5:
