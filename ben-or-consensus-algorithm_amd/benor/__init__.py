@@ -60,7 +60,7 @@ KNOBS = {
     "BENOR_NO_MFMA": "validation", "BENOR_NO_MFMA_BIG": "validation", "BENOR_BIG_FORM": "validation",
     "BENOR_COOP_BW": "validation", "BENOR_SMALL_MIN_TRIALS": "validation", "BENOR_BLOCKS_PER_CU": "tuning",
     "BENOR_EVENT_LANES_PER_CU": "tuning", "BENOR_TEST_DEFER_SEG_CAP": "test", "BENOR_TIMELINE": "diagnostic",
-    "BENOR_EVENT_FORM": "validation", "BENOR_LIVE_WAVES": "tuning",
+    "BENOR_EVENT_FORM": "validation", "BENOR_LIVE_WAVES": "tuning", "BENOR_EVENT_STATS": "diagnostic",
 }
 
 BASE_NODE_PORT = 3000          # src/config.ts:1 (kept for the HTTP-shaped helpers)

@@ -46,6 +46,8 @@
 // 4N^2 + 64 words fit kEventBigLdsPool (N <= 78) -- in LDS.
 #include "benor_device.h"
 
+#include <utility>
+
 namespace benor {
 
 namespace {
@@ -63,30 +65,53 @@ __device__ __forceinline__ uint64_t smix(uint64_t z) {
 // LDS hash slots per batch: at least twice the batch (load <= 1/2)
 constexpr uint32_t hash_slots(int W) { return 64u * (uint32_t)W <= 64u ? 128u : (64u * (uint32_t)W <= 256u ? 512u : (64u * (uint32_t)W <= 512u ? 1024u : 2048u)); }
 
-// The control block: round state the control wave owns, and the batch's
-// reduction words.
+// The control block: the round state the control wave publishes for the next
+// batch, and the batch's reduction words (double-buffered by batch parity:
+// the control wave prepares batch n + 1 while the event waves still read
+// batch n's).
 struct Ctl {
-  uint64_t e;          // deliveries so far
-  uint64_t rng;        // splitmix64 state at e
+  uint64_t rng;        // splitmix64 state at the batch's first delivery
   uint32_t len;        // pending messages
-  uint32_t B;          // this batch's events
-  uint32_t conf;       // first conflicting event of the batch (B if none)
-  uint32_t ncross;     // inbox slots that reached their quorum in the batch
-  uint32_t trig;       // the batch's first trigger event (~0: none)
-  uint32_t tmsg;       // its message
+  uint32_t B;          // the batch's events
+  uint32_t cur;        // completion round (decodes a message's k & 3)
   uint32_t halted;     // 0 running, 1 all decided, 2 k_max, 3 stall
-  uint32_t snap;       // serve a snapshot at this batch boundary (the request number), 0 none
-  uint32_t body;       // the trigger's broadcast body, ~0 none
-  uint32_t cur, R;     // completion round; halting round
+  uint32_t snap;       // serve a snapshot before this batch (the request number), 0 none
+  uint32_t body;       // the last batch's trigger broadcast, ~0 none
+  uint32_t bpos;       // where it goes (the pool's length after that batch)
+  uint32_t tmsg;       // the batch's first trigger message
   uint32_t overflow;
+  uint32_t R;          // the halting round (after the run)
+  uint32_t conf[2];    // first event of the batch that cannot be resolved (B if none)
+  uint32_t ncross[2];  // inbox slots that reached their quorum in the batch
+  uint32_t trig[2];    // the batch's first trigger event (~0: none)
 };
 
 __device__ __forceinline__ uint32_t hslot(uint32_t key, uint32_t mask) { return (key * 0x9E3779B1u >> 11) & mask; }
 
 }  // namespace
 
-// Wave 0: control.  Waves 1..W: events.  One trial per workgroup (grid-stride
-// over the launch's trials).
+// Wave 0: control.  Waves 1..W: events, one per lane.  One trial per
+// workgroup (grid-stride over the launch's trials).
+//
+// A batch of B events e .. e + B - 1 (lane i: event e + i) in four phases
+// between workgroup barriers:
+//   1. pick q_i (assuming no trigger), load pool[q_i] and the tail word
+//      pool[t_i], t_i = len - 1 - i; count the batch's pickers of q_i in an
+//      LDS hash slot {position, count, first picker}; a pick of a tail
+//      position names the later event whose tail it overwrites (bmax);
+//   2. resolve, one level deep: event i's message is pool[q_i] unless an
+//      earlier event a picked q_i (then the word a moved there), and the word
+//      it moves is pool[t_i] unless an earlier event b picked t_i (then the
+//      word b moved).  A second level (the moved word was itself forwarded),
+//      or a third picker of one position, cuts the batch before that event;
+//   3. deliver the uncut prefix at once (64-bit LDS adds of {len, c0 | c1});
+//      a slot that reaches its quorum triggers at its last batch event, and
+//      the batch ends after the earliest one (later adds undone);
+//   4. each position's last writer among the used events stores its moved
+//      word (unless the position was popped).
+// Meanwhile the control wave runs the trigger, applies the next batch's
+// scheduled and live stops, serves snapshot requests and publishes the next
+// batch; the event waves then append the trigger's broadcast.
 template <int W, bool LP>
 __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p) {
   constexpr uint32_t T = 64u * (uint32_t)W;        // event lanes
@@ -103,11 +128,14 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
   uint64_t *killed = ibox + 2u * N;                              // [64]
   uint64_t *decided = killed + 64;                               // [64]
   uint64_t *comp = decided + 64;                                 // [4][64] round k complete at k & 3
-  uint64_t *ht = comp + 256;                                     // [HS] (pos + 1) << 32 | first event
+  uint64_t *ht = comp + 256;                                     // [HS] (pos + 1) << 32 | pickers << 16 | first
   uint64_t *rset = ht + HS;                                      // [64] random /stop schedule: Floyd set
   uint64_t *rstops = rset + 64;                                  // [ev_rstops] (event << 12 | node), ~0 applied
   uint32_t *smax = reinterpret_cast<uint32_t *>(rstops + p.ev_rstops);   // [2N] last batch event + 1 into a crossed slot
-  int16_t *ks = reinterpret_cast<int16_t *>(smax + 2u * N);      // [N]
+  uint32_t *bmax = smax + 2u * N;                                // [T] last earlier event + 1 that picked t_i
+  uint32_t *nxt = bmax + T;                                      // [T] the second picker + 1 of q_i (first picker's entry)
+  uint32_t *tvs = nxt + T;                                       // [T] the tail words
+  int16_t *ks = reinterpret_cast<int16_t *>(tvs + T);            // [N]
   uint16_t *cidx = reinterpret_cast<uint16_t *>(ks + ((N + 7u) & ~7u));  // [N] compact index (coins)
   int8_t *xs = reinterpret_cast<int8_t *>(cidx + ((N + 7u) & ~7u));       // [N]
   uint32_t *pool;
@@ -124,31 +152,44 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
     const bool ok = lane >= NWd || ((a[lane] | b[lane]) == allw);
     return (__ballot(ok) & wmask) == wmask;
   };
-  // pool words: HBM slices are read around L1 (the batch's own stores went to L2)
+  // pool words: only this workgroup (one CU) reads and writes its slice, so
+  // workgroup-scope loads, served by the CU's L1 and its XCD's L2 (an
+  // agent-scope load bypasses the L2 -- not coherent across XCDs -- and went to
+  // MALL/HBM, tools/live_profile.py); every pool store is drained (vm_drain)
+  // before the barrier that orders it with another wave's load
   auto load = [&](uint32_t i) -> uint32_t {
     if constexpr (LP) return pool[i];
-    else return __hip_atomic_load(&pool[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return __hip_atomic_load(&pool[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   };
-  auto vm_drain = [&]() {                          // this wave's pool stores are in L2
+  auto vm_drain = [&]() {
     if constexpr (!LP) __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
   };
 
   for (uint32_t i = tid; i < HS; i += blockDim.x) ht[i] = 0ull;
   for (uint32_t i = tid; i < 2u * N; i += blockDim.x) smax[i] = 0u;
+  for (uint32_t i = tid; i < T; i += blockDim.x) {
+    bmax[i] = 0u;
+    nxt[i] = 0u;
+  }
 
   // the control wave's mailbox poll: lane l < NWd reads request bits 64l ..
-  // 64l + 63, lane 0 also the snapshot request; issued at `polled`, consumed
-  // >= kPollTicks later
+  // 64l + 63, lane 0 also the request sequence word and lane 1 the snapshot
+  // request; issued at `polled`, consumed >= kPollTicks later.  The host sets a
+  // burst's bits (stopConsensus: every node) and then bumps the sequence word,
+  // so the bits of the poll AFTER the one that saw the new sequence hold the
+  // whole burst, which then lands at one delivery count.
   constexpr long long kPollTicks = 500;            // 5 us of the 100 MHz wall clock
   uint64_t pv_req = 0ull;
-  uint32_t pv_snap = 0u, snap_served = 0u;
+  uint32_t pv_word = 0u, snap_served = 0u, seq_seen = 0u;
+  bool apply_next = false;
   long long polled = 0;
   bool poll_out = false;
   auto poll_issue = [&]() {
     if (lane < NWd)
       pv_req = __hip_atomic_load(reinterpret_cast<uint64_t *>(box + kLiveReq) + lane, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_SYSTEM);
-    if (lane == 0u) pv_snap = __hip_atomic_load(box + kSnapReq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lane == 0u) pv_word = __hip_atomic_load(box, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lane == 1u) pv_word = __hip_atomic_load(box + kSnapReq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     polled = wall_clock64();
     poll_out = true;
   };
@@ -234,21 +275,6 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
       }
       return v;
     };
-    uint32_t next = 0;
-    uint64_t next_key = 0;
-    if (ctl) {
-      next_key = kr ? rstops_min() : (p.ev_nstops ? p.ev_stops[0] : ~0ull);
-      if (lane == 0u) {
-        const uint4 o = philox4x32_10<false>(k0, k1, make_uint4(tlo, thi, 0u, kStreamOrder << 24));
-        C.rng = (((uint64_t)o.x << 32) | o.y) ^ 0xD1B54A32D192ED03ull;
-        C.e = 0ull;
-        C.len = m * N;
-        C.cur = 1u;
-        C.R = 0u;
-        C.halted = 0u;
-        C.overflow = 0u;
-      }
-    }
     // control wave: round completion and halting (node.ts:116-145 as DESIGN §2)
     auto advance = [&](uint32_t &cur, uint32_t &halted, uint32_t &R) {
       while (full(comp + (cur & 3u) * 64u, killed)) {
@@ -258,19 +284,37 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
         ++cur;
       }
     };
-    __syncthreads();
 
-    // The batch loop, as two loops that meet at the same barriers (A .. H, with
-    // E .. G only when a slot crossed its quorum): the control wave's and the
-    // event waves'.  Kept apart so that the control wave's in-flight mailbox
-    // poll is never waited for by an s_waitcnt the event code needs.
+    // The batch loop, as two loops that meet at the same barriers (H [H2] B C
+    // D [E F G] per batch): the control wave's and the event waves'.  Kept
+    // apart so that the control wave's in-flight mailbox poll is never waited
+    // for by an s_waitcnt the event code needs.
     if (ctl) {
-      for (;;) {
-        // ================= control: stops, mailbox, snapshot, the batch size
-        uint32_t cur = C.cur, halted = C.halted, R = C.R, len = C.len;
-        const uint64_t e = C.e;
+      // diagnostics (BENOR_EVENT_STATS): batch counters and the shader cycles
+      // between the control wave's barriers, accumulated per trial
+      unsigned long long *const stats = p.ev_stats;
+      uint64_t st[16] = {};
+      uint64_t t_prev = stats ? __builtin_amdgcn_s_memtime() : 0ull;
+      const uint64_t t_start = t_prev, w_start = stats ? (uint64_t)wall_clock64() : 0ull;
+      auto stamp = [&](int slot) {
+        if (stats) {
+          const uint64_t t = __builtin_amdgcn_s_memtime();
+          st[slot] += t - t_prev;
+          t_prev = t;
+        }
+      };
+      uint32_t next = 0;
+      uint64_t next_key = kr ? rstops_min() : (p.ev_nstops ? p.ev_stops[0] : ~0ull);
+      uint64_t e = 0, rng;
+      {
+        const uint4 o = philox4x32_10<false>(k0, k1, make_uint4(tlo, thi, 0u, kStreamOrder << 24));
+        rng = (((uint64_t)o.x << 32) | o.y) ^ 0xD1B54A32D192ED03ull;
+      }
+      uint32_t len = m * N, cur = 1u, R = 0u, halted = 0u, body = 0xFFFFFFFFu, par = 0u, overflow = 0u;
+      // ---- the next batch, at delivery e: scheduled and live GET /stop
+      // (node.ts:191-194) before delivery e, a snapshot request, halting, its size
+      auto prepare = [&]() {
         bool crashed = false;
-        // scheduled GET /stop (node.ts:191-194) before delivery e
         while ((next_key >> 12) == e) {
           const uint32_t i = (uint32_t)(next_key & 4095u);
           if (lane == 0u) {
@@ -292,8 +336,10 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
         if (box && poll_out && wall_clock64() - polled >= kPollTicks) {
           // live GET /stop requests and /getState snapshot requests: the poll
           // issued >= 5 us ago (its PCIe round trip is long done)
-          const uint64_t req = pv_req;
-          const uint32_t sreq = __shfl(pv_snap, 0);
+          const uint64_t req = apply_next ? pv_req : 0ull;   // a burst is complete one poll after its sequence
+          const uint32_t seq = __shfl(pv_word, 0), sreq = __shfl(pv_word, 1);
+          apply_next = seq != seq_seen;
+          seq_seen = seq;
           uint64_t fresh = 0ull;
           if (lane < NWd) {
             fresh = req & allw & ~killed[lane];
@@ -326,39 +372,70 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
           const uint64_t until = (next_key >> 12) - e;
           if (until < B) B = (uint32_t)until;
         }
-        if (lane == 0u) {
-          C.cur = cur;
-          C.halted = halted;
-          C.R = R;
-          C.B = B;
-          C.conf = B;
-          C.ncross = 0u;
-          C.trig = 0xFFFFFFFFu;
-          C.body = 0xFFFFFFFFu;
-          C.snap = snap;
-        }
-        if (snap && lane == 0u) {                  // the delivery count this snapshot reflects
+        if (snap && !halted && lane == 0u) {       // the delivery count this snapshot reflects
           __hip_atomic_store(box + kSnapE, (uint32_t)e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           __hip_atomic_store(box + kSnapE + 1u, (uint32_t)(e >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
-        __syncthreads();                           // ---- A
+        return std::make_pair(B, halted ? 0u : snap);
+      };
+      auto publish = [&](uint32_t B, uint32_t snap, uint32_t bpos) {
+        if (lane == 0u) {
+          C.rng = rng;
+          C.len = len;
+          C.B = B;
+          C.cur = cur;
+          C.halted = halted;
+          C.snap = snap;
+          C.body = body;
+          C.bpos = bpos;
+          C.conf[par] = B;
+          C.ncross[par] = 0u;
+          C.trig[par] = 0xFFFFFFFFu;
+        }
+      };
+      {
+        const auto bs = prepare();
+        publish(bs.first, bs.second, 0u);
+      }
+      uint32_t snap = 0u;
+      for (;;) {
+        stamp(5);
+        __syncthreads();                           // ---- H: the batch is published
+        if (body != 0xFFFFFFFFu) __syncthreads();  // ---- H2: the broadcast is in the pool
+        snap = C.snap;
+        const uint32_t B = C.B;
         if (halted) break;
-        __syncthreads();                           // ---- B: the snapshot's states are written
-        if (snap && lane == 0u)
+        stamp(11);
+        __syncthreads();                           // ---- B: picks and loads
+        stamp(6);
+        if (snap && lane == 0u)                    // the snapshot's states are written
           __hip_atomic_store(box + kSnapSeq, snap, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        __syncthreads();                           // ---- C
-        const uint32_t used0 = C.conf;
-        __syncthreads();                           // ---- D
+        __syncthreads();                           // ---- C: resolution
+        stamp(7);
+        const uint32_t used0 = C.conf[par];
+        __syncthreads();                           // ---- D: deliveries
+        stamp(8);
         uint32_t used = used0;
-        if (C.ncross) {
+        if (C.ncross[par]) {
           __syncthreads();                         // ---- E
           __syncthreads();                         // ---- F
-          used = C.trig + 1u;
+          used = C.trig[par] + 1u;
           __syncthreads();                         // ---- G
+          stamp(9);
+          st[14] += 1u;
         }
-        const uint32_t tr = C.trig;
+        if (stats) {
+          st[0] += 1u;
+          st[1] += used;
+          st[2] += B;
+          st[4] += used0 < B ? 1u : 0u;
+          st[15] += snap ? 1u : 0u;
+        }
+        const uint32_t tr = C.trig[par];
+        body = 0xFFFFFFFFu;
         if (tr != 0xFFFFFFFFu) {
           // ---- the trigger (node.ts:52-80 R-phase, :88-157 P-phase)
+          st[3] += 1u;
           const uint32_t tmsg = C.tmsg;
           const uint32_t to = tmsg & 4095u, ph = (tmsg >> 12) & 1u;
           const uint32_t k = cur + (((tmsg >> 15) - cur) & 3u);
@@ -366,7 +443,6 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
           __builtin_amdgcn_wave_barrier();
           if (lane == 0u) ibox[2u * to + ph] = 0ull;   // every message of the phase arrived: the slot is free
           const uint32_t c0 = (uint32_t)(tbox & kF13), c1 = (uint32_t)((tbox >> 13) & kF13);
-          uint32_t body = 0xFFFFFFFFu, ncur = cur, nhalted = 0u;
           if (ph == 0u) {
             const uint32_t v = c0 > c1 ? 0u : (c1 > c0 ? 1u : 2u);
             body = (1u << 12) | (v << 13) | ((k & 3u) << 15);
@@ -393,40 +469,56 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
             }
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-            advance(ncur, nhalted, R);
-            if (!nhalted) body = ((uint32_t)(nx & 3) << 13) | (((k + 1u) & 3u) << 15);
+            advance(cur, halted, R);
+            if (!halted) body = ((uint32_t)(nx & 3) << 13) | (((k + 1u) & 3u) << 15);
           }
           if (body != 0xFFFFFFFFu && (uint64_t)(len - used) + N > cap) {
             body = 0xFFFFFFFFu;                    // the pool would overflow: stop (flagged)
-            nhalted = 3u;
-            if (lane == 0u) C.overflow = 1u;
+            halted = 3u;
+            overflow = 1u;
           }
-          if (lane == 0u) {
-            C.body = body;
-            C.cur = ncur;
-            C.R = R;
-            C.halted = nhalted;
-          }
-          len = len - used + (body != 0xFFFFFFFFu ? N : 0u);
-        } else {
-          len -= used;
         }
-        __syncthreads();                           // ---- H
-        if (lane == 0u) {
-          C.len = len;
-          C.e = e + used;
-          C.rng += (uint64_t)used * kGm;
+        const uint32_t bpos = len - used;
+        len = bpos + (body != 0xFFFFFFFFu ? N : 0u);
+        e += used;
+        rng += (uint64_t)used * kGm;
+        par ^= 1u;
+        uint32_t nB = 0u, nsnap = 0u;
+        if (!halted) {                             // (a halting trigger ends the run at once, as oracle (iii))
+          const auto bs = prepare();
+          nB = bs.first;
+          nsnap = bs.second;
         }
+        publish(nB, nsnap, bpos);
+        stamp(10);
+      }
+      if (lane == 0u) {
+        C.R = R;
+        C.overflow = overflow;
+      }
+      if (stats && lane == 0u) {
+        st[12] = __builtin_amdgcn_s_memtime() - t_start;
+        st[13] = (uint64_t)wall_clock64() - w_start;
+        for (int i = 0; i < 16; ++i) atomicAdd(&stats[i], (unsigned long long)st[i]);
       }
     } else {
+      uint32_t par = 0u;
       for (;;) {
-        __syncthreads();                           // ---- A
+        __syncthreads();                           // ---- H
+        const uint32_t body = C.body;
+        if (body != 0xFFFFFFFFu) {                 // the last trigger's broadcast (node.ts:72-80, :149-157)
+          const uint32_t bpos = C.bpos;
+          for (uint32_t d = ei; d < N; d += T) pool[bpos + d] = d | body;
+          vm_drain();
+          __syncthreads();                         // ---- H2
+        }
         const uint32_t halted = C.halted, B = C.B, len = C.len, cur = C.cur, snap = C.snap;
         const uint64_t rng = C.rng;
         if (halted) break;
         if (snap) {
           // GET /getState (node.ts:197-199) mid-run: every node's state as of
-          // delivery e, to host memory (bo_get_states reads it after the sequence word)
+          // this batch's first delivery, to host memory (bo_get_states reads it
+          // after the sequence word)
           for (uint32_t i = ei; i < N; i += T) {
             const bool f = ks[i] < 0 && xs[i] < 0;   // faulty from launch (never ran)
             const uint32_t kl =
@@ -438,8 +530,8 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
           }
           __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0): the states reached the host
         }
-        // ================= the batch's picks: event e + i takes position q_i and
-        // moves the word at t_i = len - 1 - i there (swap-remove)
+        // ================= 1. picks: event e + i takes position q_i and moves
+        // the word at t_i = len - 1 - i there (swap-remove)
         uint32_t qi = 0u, ti = 0u, pv = 0u, tv = 0u, hs = 0u;
         const bool act = ei < B;
         if (act) {
@@ -448,44 +540,61 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
           ti = len - 1u - ei;
           pv = load(qi);
           tv = load(ti);
-          // first event of the batch that picks qi
-          const uint64_t val = ((uint64_t)(qi + 1u) << 32) | ei;
+          // the batch's pickers of qi: count and first (event index)
+          const uint64_t key = (uint64_t)(qi + 1u) << 32;
           hs = hslot(qi, HS - 1u);
           for (;;) {
-            const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long *>(&ht[hs]), 0ull, val);
+            uint64_t old = atomicCAS(reinterpret_cast<unsigned long long *>(&ht[hs]), 0ull, key | (1u << 16) | ei);
             if (old == 0ull) break;
-            if ((uint32_t)(old >> 32) == qi + 1u) {
-              atomicMin(reinterpret_cast<unsigned long long *>(&ht[hs]), val);
+            if ((old >> 32) == (key >> 32)) {      // a repeated pick (rare): count it, keep the first
+              for (;;) {
+                const uint64_t lo = old & 0xFFFFull;
+                const uint64_t nv = (old & ~0xFFFFull) + (1ull << 16) | (lo < ei ? lo : (uint64_t)ei);
+                const uint64_t r = atomicCAS(reinterpret_cast<unsigned long long *>(&ht[hs]), old, nv);
+                if (r == old) break;
+                old = r;
+              }
               break;
             }
             hs = (hs + 1u) & (HS - 1u);
           }
+          // a pick of a tail position overwrites the word a later event moves
+          if (qi >= len - B && qi != ti) atomicMax(&bmax[len - 1u - qi], ei + 1u);
+          tvs[ei] = tv;
         }
         __syncthreads();                           // ---- B
+        // ================= 2. resolution, one level deep
+        uint32_t msg = pv, moved = tv;
         if (act) {
-          // conflict: an earlier event of the batch picked qi, or picked ti (its
-          // word moved there is then not the pool's own); q_j == t_i implies j <= i
-          auto first = [&](uint32_t key) -> uint32_t {
-            uint32_t h = hslot(key, HS - 1u);
-            for (;;) {
-              const uint64_t v = ht[h];
-              if (v == 0ull) return 0xFFFFFFFFu;
-              if ((uint32_t)(v >> 32) == key + 1u) return (uint32_t)v;
-              h = (h + 1u) & (HS - 1u);
+          bool cut = false;
+          const uint32_t b = bmax[ei];
+          if (b) {                                 // t_i was overwritten by event b - 1: its moved word
+            const uint32_t bb = bmax[b - 1u];
+            if (bb) cut = true;
+            else moved = tvs[b - 1u];
+          }
+          const uint64_t h = ht[hs];
+          const uint32_t cnt = (uint32_t)(h >> 16) & 0xFFFFu, first = (uint32_t)h & 0xFFFFu;
+          if (first != ei) {
+            if (cnt >= 3u) cut = true;             // its earlier picker is not known: cut before it
+            else {                                 // q_i was written by event `first`: its moved word
+              nxt[first] = ei + 1u;
+              const uint32_t ba = bmax[first];
+              if (!ba) msg = tvs[first];
+              else if (bmax[ba - 1u]) cut = true;
+              else msg = tvs[ba - 1u];
             }
-          };
-          const uint32_t fq = first(qi), ft = first(ti);
-          if (fq < ei || ft < ei) atomicMin(&C.conf, ei);
+          }
+          if (cut) atomicMin(&C.conf[par], ei);
         }
         __syncthreads();                           // ---- C
-        if (act) ht[hs] = 0ull;                    // every lookup is done: the table is empty again
-        const uint32_t used0 = C.conf;
-        // ================= POST /message (node.ts:45-158): the prefix's deliveries at once
+        const uint32_t used0 = C.conf[par];
+        // ================= 3. POST /message (node.ts:45-158): the prefix's deliveries at once
         uint64_t inc = 0ull;
         uint32_t slot = 0u;
         if (act && ei < used0) {
-          const uint32_t to = pv & 4095u, ph = (pv >> 12) & 1u, xv = (pv >> 13) & 3u;
-          const uint32_t k = cur + (((pv >> 15) - cur) & 3u);
+          const uint32_t to = msg & 4095u, ph = (msg >> 12) & 1u, xv = (msg >> 13) & 3u;
+          const uint32_t k = cur + (((msg >> 15) - cur) & 3u);
           slot = 2u * to + ph;
           if (k < p.k_max + 3u)                    // beyond the oracle's round window: dropped
             inc = (1ull << 26) + (xv == 0u ? 1ull : (xv == 1u ? 1ull << 13 : 0ull));
@@ -494,12 +603,12 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             // killed receivers drop the message (node.ts:45): their slot counts
             // on, never tested; a live slot crosses its quorum (node.ts:52, :88)
-            if (!(old & kDead) && ((old >> 26) & kF13) + 1u == quorum) atomicAdd(&C.ncross, 1u);
+            if (!(old & kDead) && ((old >> 26) & kF13) + 1u == quorum) atomicAdd(&C.ncross[par], 1u);
           }
         }
         __syncthreads();                           // ---- D
         uint32_t used = used0;
-        if (C.ncross) {
+        if (C.ncross[par]) {
           // a crossed slot triggers at the last batch event into it; the batch
           // ends after the earliest such event
           bool mine = false;
@@ -509,32 +618,33 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
             if (mine) atomicMax(&smax[slot], ei + 1u);
           }
           __syncthreads();                         // ---- E
-          if (mine) atomicMin(&C.trig, smax[slot] - 1u);
+          if (mine) atomicMin(&C.trig[par], smax[slot] - 1u);
           __syncthreads();                         // ---- F
-          const uint32_t tr = C.trig;
+          const uint32_t tr = C.trig[par];
           if (mine) smax[slot] = 0u;
           if (inc && ei > tr)
             __hip_atomic_fetch_add(reinterpret_cast<unsigned long long *>(&ibox[slot]), 0ull - inc,
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          if (act && ei == tr) C.tmsg = pv;
+          if (act && ei == tr) C.tmsg = msg;
           used = tr + 1u;
           __syncthreads();                         // ---- G
         }
-        // ================= the prefix's pool writes: q_i keeps the word moved
-        // there unless q_i itself was popped (q_i == t_i)
-        if (act && ei < used && qi < len - used) pool[qi] = tv;
-        vm_drain();
-        __syncthreads();                           // ---- H
-        const uint32_t body = C.body;
-        if (body != 0xFFFFFFFFu) {                 // the trigger's broadcast (node.ts:72-80, :149-157)
-          for (uint32_t d = ei; d < N; d += T) pool[len - used + d] = d | body;
-          vm_drain();
+        // ================= 4. pool writes: a position's last writer among the
+        // used events stores its moved word, unless the position was popped
+        if (act) {
+          const uint32_t nx = nxt[ei];
+          if (ei < used && (nx == 0u || nx - 1u >= used) && qi < len - used) pool[qi] = moved;
+          ht[hs] = 0ull;                           // the tables are empty again for the next batch
+          bmax[ei] = 0u;
+          nxt[ei] = 0u;
         }
+        vm_drain();
+        par ^= 1u;
       }
     }
     // ---- outcome over the nodes still running
-    const uint32_t hlt = C.halted, R = C.R;
     __syncthreads();
+    const uint32_t hlt = C.halted, R = C.R;
     if (ctl) {
       bool any0 = false, any1 = false, anyq = false, nl = false;
       for (uint32_t i = lane; i < N; i += 64u) {
@@ -587,7 +697,7 @@ uint32_t event_wg_lds_bytes(const KParams &p, uint32_t W) {
   const uint32_t HS = W == 1u ? hash_slots(1) : W == 3u ? hash_slots(3) : W == 7u ? hash_slots(7) : hash_slots(15);
   uint32_t b = ((uint32_t)sizeof(Ctl) + 15u) & ~15u;
   b += 16u * N + 8u * 64u * 6u + 8u * HS + 8u * 64u + 8u * p.ev_rstops;   // ibox, killed/decided/comp, hash, Floyd set, keys
-  b += 8u * N;                                                            // smax
+  b += 8u * N + 3u * 4u * 64u * W;                                        // smax; bmax, nxt, tvs
   b += 2u * ((N + 7u) & ~7u) * 2u + ((N + 15u) & ~15u);                   // ks, cidx, xs
   if (event_wg_lds_pool(p)) b += 4u * p.ev_cap;
   return b;

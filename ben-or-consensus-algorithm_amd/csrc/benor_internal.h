@@ -108,6 +108,9 @@ struct KParams {
   // event level: run the workgroup-batched kernel (benor_event_live.hip) --
   // live runs, and batch plans under BENOR_EVENT_FORM=wg
   uint32_t ev_wg;
+  // diagnostics (BENOR_EVENT_STATS): that kernel's per-batch counters and
+  // cycle split, 16 u64 (device) or nullptr
+  unsigned long long *ev_stats;
   // W kernel trial-list mode: run the trials trial_begin + trial_list[i],
   // i < min(*trial_list_len, trial_count), instead of a contiguous range
   const uint32_t *trial_list, *trial_list_len;

@@ -86,6 +86,7 @@ constexpr KnobSpec kKnobs[] = {
     {"BENOR_EVENT_LANES_PER_CU", "tuning"},     // event level, N <= 256: lanes per CU
     {"BENOR_EVENT_FORM", "validation"},         // "wg": batch event plans on the workgroup-batched kernel
     {"BENOR_LIVE_WAVES", "tuning"},             // 1 / 3 / 7 / 15: event waves of the workgroup-batched kernel
+    {"BENOR_EVENT_STATS", "diagnostic"},        // workgroup-batched kernel: batch counters and cycle split to a file
     {"BENOR_TEST_DEFER_SEG_CAP", "test"},       // deferral segment capacity below the sizing rule
     {"BENOR_TIMELINE", "diagnostic"},           // packed matrix-core kernel: per-wave phase stamps to a file
 };
@@ -170,6 +171,8 @@ std::vector<LiveSlot *> g_free_slots;
 // Where the run's results sit in the slot's buffer.
 struct WgRun {
   size_t o_st = 0, o_r = 0;            // states [N], round word (the head read back ends after it)
+  size_t o_stats = 0;                  // BENOR_EVENT_STATS counters (16 u64, after the round word)
+  uint32_t N = 0, F = 0;
 };
 }  // namespace
 
@@ -189,11 +192,16 @@ struct bo_live {
 
 namespace {
 // Post GET /stop requests to a live run (caller holds net->mu): the nodes'
-// request bits, which the kernel's control wave polls.
+// request bits (one OR per 32-node word), then the sequence word.  The
+// kernel's control wave applies the bits it reads in the poll after the one
+// that saw the new sequence, so one call's requests land together.
 void live_post(bo_live *lr, const uint32_t *ids, uint32_t n) {
   uint32_t *box = lr->slot->box;
-  for (uint32_t j = 0; j < n; ++j)
-    __atomic_fetch_or(&box[benor::kLiveReq + (ids[j] >> 5)], 1u << (ids[j] & 31u), __ATOMIC_RELEASE);
+  uint32_t words[BO_MAX_N / 32] = {};
+  for (uint32_t j = 0; j < n; ++j) words[ids[j] >> 5] |= 1u << (ids[j] & 31u);
+  for (uint32_t w = 0; w < BO_MAX_N / 32; ++w)
+    if (words[w]) __atomic_fetch_or(&box[benor::kLiveReq + w], words[w], __ATOMIC_RELAXED);
+  __atomic_fetch_add(&box[0], 1u, __ATOMIC_RELEASE);
 }
 }  // namespace
 
@@ -1074,7 +1082,8 @@ int wg_launch(LiveSlot *sl, const bo_trials_cfg *cfg, bool live, WgRun &run) {
       if (cfg->crash_at[i] != 0xFFFFFFFFu) stops.push_back(((uint64_t)cfg->crash_at[i] << 12) | i);
   std::sort(stops.begin(), stops.end());
   const size_t o_st = 16u, o_h = align_up(o_st + sizeof(bo_node_state) * N, 16u);
-  const size_t o_r = o_h + sizeof(uint64_t) * H, o_live = align_up(o_r + 4u, 16u);
+  const size_t o_r = o_h + sizeof(uint64_t) * H, o_stats = align_up(o_r + 4u, 16u);
+  const size_t o_live = o_stats + 16u * sizeof(uint64_t);
   const size_t o_ix = align_up(o_live + sizeof(uint32_t) * m, 16u);
   const size_t o_stops = align_up(o_ix + N, 16u);
   const size_t o_pool = align_up(o_stops + sizeof(uint64_t) * stops.size(), 256u);
@@ -1112,16 +1121,35 @@ int wg_launch(LiveSlot *sl, const bo_trials_cfg *cfg, bool live, WgRun &run) {
   kp.scratch = reinterpret_cast<uint32_t *>(sl->d + o_pool);
   kp.ev_lanes = 1u;                              // one trial
   kp.live_box = live ? sl->dbox : nullptr;
+  kp.ev_stats = benor::knob("BENOR_EVENT_STATS") ? reinterpret_cast<unsigned long long *>(sl->d + o_stats) : nullptr;
   kp.trial_begin = 0;
   kp.trial_count = 1;
   run.o_st = o_st;
   run.o_r = o_r;
+  run.o_stats = o_stats;
+  run.N = N;
+  run.F = cfg->F;
   HIP_TRY(benor::launch_event_wg(kp, 1, sl->s));
   return BO_OK;
 }
 
 // The run's head (flag | states | hist | rounds), read back on the slot's stream.
 int wg_read(LiveSlot *sl, const WgRun &run, uint32_t N, std::vector<bo_node_state> &states) {
+  if (const char *path = benor::knob("BENOR_EVENT_STATS")) {   // diagnostics: one JSON line per run
+    unsigned long long s[16] = {};
+    if (hipMemcpyAsync(s, sl->d + run.o_stats, sizeof s, hipMemcpyDeviceToHost, sl->s) == hipSuccess &&
+        hipStreamSynchronize(sl->s) == hipSuccess)
+      if (FILE *f = std::fopen(path, "a")) {
+        static const char *names[16] = {"batches", "events", "batch_slots", "trigger_batches", "conflict_cut",
+                                        "cyc_top", "cyc_picks", "cyc_lookup", "cyc_deliver", "cyc_cross",
+                                        "cyc_writes_trigger", "cyc_bcast", "cycles", "wall_ticks", "cross_batches",
+                                        "snapshots"};
+        std::fprintf(f, "{\"N\": %u, \"F\": %u", run.N, run.F);
+        for (int i = 0; i < 16; ++i) std::fprintf(f, ", \"%s\": %llu", names[i], s[i]);
+        std::fprintf(f, "}\n");
+        std::fclose(f);
+      }
+  }
   std::vector<unsigned char> head(run.o_r + 4u);
   hipError_t e = hipMemcpyAsync(head.data(), sl->d, head.size(), hipMemcpyDeviceToHost, sl->s);
   if (e == hipSuccess) e = hipStreamSynchronize(sl->s);

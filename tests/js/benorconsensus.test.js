@@ -109,19 +109,28 @@ it('live start excludes a stop schedule and sync', 'setup', async () => {
 });
 
 // __test__/tests/utils.ts:14-20 reads the states as Promise.all over GET
-// /getState: every concurrent read after the default start waits for the run
-it('Concurrent getNodeState reads after a default start all see the final states', 'gpu', async () => {
+// /getState: every read answers at once (node.ts:197-199) -- mid-run, a
+// snapshot of the running network; after waitConsensus, the final states
+it('Concurrent getNodeState reads during a default start answer at once, then the final states', 'gpu', async () => {
   const N = 1024, F = 341;
   const fa = Array.from({ length: N }, (_, i) => i < F);
   const init = Array.from({ length: N }, (_, i) => (i < F ? 0 : (i % 3 === 0 ? 0 : 1)));
   const servers = await b.launchNetwork(N, F, init, fa);
   await b.startConsensus(N, { seed: 0xC0FFEEn });
+  const mid = await Promise.all(Array.from({ length: N }, (_, i) => b.getNodeState(i)));
+  mid.forEach((s, i) => {
+    if (fa[i]) { assert.strictEqual(s.decided, null); return; }
+    assert.ok(s.k === 1 || s.k === 2); assert.strictEqual(s.killed, false);
+  });
+  await b.waitConsensus(N);
   const states = await Promise.all(Array.from({ length: N }, (_, i) => b.getNodeState(i)));
   states.forEach((s, i) => {
     if (fa[i]) { assert.strictEqual(s.decided, null); return; }
     assert.strictEqual(s.decided, true); assert.strictEqual(s.x, 1); assert.strictEqual(s.k, 2);
   });
   assert.deepStrictEqual(await b.getNodesState(N), states);
+  const at = await b.getNodesStateAt(N);
+  assert.strictEqual(at.events, null);
   await b.stopConsensus(N); await closeAllServers(servers);
 });
 

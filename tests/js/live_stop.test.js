@@ -3,7 +3,7 @@
 // (tests/test_live_stop.py writes the cases and checks the results against
 // the oracle for the recorded delivery counts):
 //   launchNetwork -> startConsensus(N, {seed, kMax: 16, live: true}) -> stopNode(i)
-//   -> getNodesState(N) (waits for the run) -> liveStopEvents(N)
+//   -> waitConsensus(N) -> getNodesState(N) -> liveStopEvents(N)
 // Usage: node live_stop.test.js cases.json out.json
 const fs = require('fs');
 const path = require('path');
@@ -21,6 +21,7 @@ async function main() {
       const st = await b.getNodeStatus(i);
       assert.strictEqual(st.status, 500);              // node.ts:33-39, answered mid-run
     }
+    await b.waitConsensus(c.N);
     const states = await b.getNodesState(c.N);
     const events = await b.liveStopEvents(c.N);
     results.push({ states, events });

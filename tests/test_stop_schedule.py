@@ -142,6 +142,7 @@ def test_no_schedule_is_the_lockstep_start():
     a = benor.getNodesState(c["N"])
     benor.launchNetwork(c["N"], c["F"], c["init"], c["faulty"])
     benor.startConsensus(c["N"], seed=c["seed"], k_max=c["k_max"])
+    benor.waitConsensus(c["N"])
     assert benor.getNodesState(c["N"]) == a
 
 

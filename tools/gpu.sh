@@ -29,6 +29,8 @@
 #   c5phases        tools/c5_phases.py: the C5 sweep's wall time split (plans / queue / drain / read-back), twice
 #   c5trace         the same under rocprofv3 --kernel-trace --stats
 #   matrix          tools/perf_matrix.py over its built-in shape list
+#   liveprof        tools/live_profile.py (LIVEPROF_ARGS): a live run's batch counters and cycle split
+#   netlat          tools/net_latency.py (NETLAT_ARGS): the reference's launch + start + final states
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R" || exit 1
 TAG=${TAG:-scratch}
@@ -62,7 +64,7 @@ for step in "$@"; do
       timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
       chk $? smoke; tail -1 "$OUT/smoke.log";;
     tests)
-      timeout -k 10 900 python -u -m pytest ${PYTEST_ARGS:-tests} ${PYTEST_K:+-k "$PYTEST_K"} -m gpu -x -v --durations=30 --timeout 200 --timeout-method thread \
+      timeout -k 10 ${TESTS_TIMEOUT:-900} python -u -m pytest ${PYTEST_ARGS:-tests} ${PYTEST_K:+-k "$PYTEST_K"} -m gpu ${PYTEST_X--x} -v --durations=30 --timeout 200 --timeout-method thread \
         > "$OUT/tests.log" 2>&1
       rc=$?; tail -3 "$OUT/tests.log"; chk $rc tests;;
     probe)
@@ -146,6 +148,12 @@ for step in "$@"; do
     matrix)
       timeout -k 10 400 python -u tools/perf_matrix.py > "$OUT/perf_matrix.jsonl" 2>&1
       chk $? matrix;;
+    liveprof)
+      timeout -k 10 300 python -u tools/live_profile.py ${LIVEPROF_ARGS:-} > "$OUT/live_profile.jsonl" 2> "$OUT/live_profile.err"
+      chk $? liveprof; cat "$OUT/live_profile.jsonl";;
+    netlat)
+      timeout -k 10 400 python -u tools/net_latency.py ${NETLAT_ARGS:---reps 60} > "$OUT/net_latency.jsonl" 2> "$OUT/net_latency.err"
+      chk $? netlat; cat "$OUT/net_latency.jsonl";;
     *)
       echo "unknown step $step"; exit 2;;
   esac

@@ -24,14 +24,14 @@ def main():
     a = ap.parse_args()
     import benor
 
-    for N, F in [(5, 1), (10, 4), (10, 5), (100, 33), (1024, 341)]:
+    for N, F in [(5, 1), (10, 4), (10, 5), (100, 33), (1024, 341), (1024, 512)]:
         if N > a.max_n:
             continue
         faulty = [i < F for i in range(N)]
         init = [(i * 7 + 3) % 2 for i in range(N)]
         for start, kw in (("default", {}), ("sync", {"sync": True})):
             times = []
-            reps = a.reps if N < 1024 or start == "sync" else max(5, a.reps // 20)
+            reps = a.reps if N < 1024 or start == "sync" else max(5, a.reps // (20 if F < 512 else 60))
             for rep in range(reps + 5):
                 t0 = time.perf_counter()
                 benor.launchNetwork(N, F, init, faulty)
