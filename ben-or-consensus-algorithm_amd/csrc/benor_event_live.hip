@@ -62,8 +62,10 @@ __device__ __forceinline__ uint64_t smix(uint64_t z) {
   return z ^ (z >> 31);
 }
 
-// LDS hash slots per batch: at least twice the batch (load <= 1/2)
-constexpr uint32_t hash_slots(int W) { return 64u * (uint32_t)W <= 64u ? 128u : (64u * (uint32_t)W <= 256u ? 512u : (64u * (uint32_t)W <= 512u ? 1024u : 2048u)); }
+// LDS hash slots per batch (a power of two, KParams::ev_hs): four times the
+// batch where LDS allows, else twice -- a wave's slowest lane probes about
+// twice as far at load 1/2 as at 1/4, one LDS round trip per probe
+constexpr uint32_t pow2_ceil(uint32_t v) { uint32_t r = 1u; while (r < v) r <<= 1; return r; }
 
 // The control block: the round state the control wave publishes for the next
 // batch, and the batch's reduction words (double-buffered by batch parity:
@@ -87,6 +89,14 @@ struct Ctl {
 };
 
 __device__ __forceinline__ uint32_t hslot(uint32_t key, uint32_t mask) { return (key * 0x9E3779B1u >> 11) & mask; }
+
+// A wave-uniform value read from LDS or global memory: the compiler cannot see
+// that every lane read the same word, and left to itself turns the round
+// state and everything it controls into exec-masked vector code.
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  return (uint64_t)uni((uint32_t)v) | ((uint64_t)uni((uint32_t)(v >> 32)) << 32);
+}
 
 }  // namespace
 
@@ -115,7 +125,7 @@ __device__ __forceinline__ uint32_t hslot(uint32_t key, uint32_t mask) { return 
 template <int W, bool LP>
 __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p) {
   constexpr uint32_t T = 64u * (uint32_t)W;        // event lanes
-  constexpr uint32_t HS = hash_slots(W);
+  const uint32_t HS = p.ev_hs;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const bool ctl = tid < 64u;                      // the control wave
@@ -285,7 +295,7 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
       }
     };
 
-    // The batch loop, as two loops that meet at the same barriers (H [H2] B C
+    // The batch loop, as two loops that meet at the same barriers (H B C
     // D [E F G] per batch): the control wave's and the event waves'.  Kept
     // apart so that the control wave's in-flight mailbox poll is never waited
     // for by an s_waitcnt the event code needs.
@@ -304,7 +314,7 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
         }
       };
       uint32_t next = 0;
-      uint64_t next_key = kr ? rstops_min() : (p.ev_nstops ? p.ev_stops[0] : ~0ull);
+      uint64_t next_key = uni64(kr ? rstops_min() : (p.ev_nstops ? p.ev_stops[0] : ~0ull));
       uint64_t e = 0, rng;
       {
         const uint4 o = philox4x32_10<false>(k0, k1, make_uint4(tlo, thi, 0u, kStreamOrder << 24));
@@ -326,10 +336,10 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
           if (kr) {
             for (uint32_t j = lane; j < kr; j += 64u)
               if (rstops[j] == next_key) rstops[j] = ~0ull;
-            next_key = rstops_min();
+            next_key = uni64(rstops_min());
           } else {
             ++next;
-            next_key = next < p.ev_nstops ? p.ev_stops[next] : ~0ull;
+            next_key = uni64(next < p.ev_nstops ? p.ev_stops[next] : ~0ull);
           }
         }
         uint32_t snap = 0u;
@@ -401,9 +411,8 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
       for (;;) {
         stamp(5);
         __syncthreads();                           // ---- H: the batch is published
-        if (body != 0xFFFFFFFFu) __syncthreads();  // ---- H2: the broadcast is in the pool
-        snap = C.snap;
-        const uint32_t B = C.B;
+        snap = uni(C.snap);
+        const uint32_t B = uni(C.B);
         if (halted) break;
         stamp(11);
         __syncthreads();                           // ---- B: picks and loads
@@ -412,14 +421,14 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
           __hip_atomic_store(box + kSnapSeq, snap, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         __syncthreads();                           // ---- C: resolution
         stamp(7);
-        const uint32_t used0 = C.conf[par];
+        const uint32_t used0 = uni(C.conf[par]);
         __syncthreads();                           // ---- D: deliveries
         stamp(8);
         uint32_t used = used0;
-        if (C.ncross[par]) {
+        if (uni(C.ncross[par])) {
           __syncthreads();                         // ---- E
           __syncthreads();                         // ---- F
-          used = C.trig[par] + 1u;
+          used = uni(C.trig[par]) + 1u;
           __syncthreads();                         // ---- G
           stamp(9);
           st[14] += 1u;
@@ -431,15 +440,15 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
           st[4] += used0 < B ? 1u : 0u;
           st[15] += snap ? 1u : 0u;
         }
-        const uint32_t tr = C.trig[par];
+        const uint32_t tr = uni(C.trig[par]);
         body = 0xFFFFFFFFu;
         if (tr != 0xFFFFFFFFu) {
           // ---- the trigger (node.ts:52-80 R-phase, :88-157 P-phase)
           st[3] += 1u;
-          const uint32_t tmsg = C.tmsg;
+          const uint32_t tmsg = uni(C.tmsg);
           const uint32_t to = tmsg & 4095u, ph = (tmsg >> 12) & 1u;
           const uint32_t k = cur + (((tmsg >> 15) - cur) & 3u);
-          const uint64_t tbox = ibox[2u * to + ph];
+          const uint64_t tbox = uni64(ibox[2u * to + ph]);
           __builtin_amdgcn_wave_barrier();
           if (lane == 0u) ibox[2u * to + ph] = 0ull;   // every message of the phase arrived: the slot is free
           const uint32_t c0 = (uint32_t)(tbox & kF13), c1 = (uint32_t)((tbox >> 13) & kF13);
@@ -456,9 +465,9 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
               if (c0 + c1 > 0u && c0 > c1) nx = 0;
               else if (c0 + c1 > 0u && c0 < c1) nx = 1;
               else {
-                const uint32_t c = cidx[to];       // the coin of compact node c in round k (node.ts:111)
+                const uint32_t c = uni(cidx[to]);  // the coin of compact node c in round k (node.ts:111)
                 const uint4 rr = coin_block<false>(k0, k1, tlo, thi, c, k);
-                nx = (int8_t)((coin_word(rr, k) >> (c & 31u)) & 1u);
+                nx = (int8_t)uni((coin_word(rr, k) >> (c & 31u)) & 1u);
               }
             }
             if (lane == 0u) {
@@ -503,17 +512,21 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
       }
     } else {
       uint32_t par = 0u;
+      // diagnostics (BENOR_EVENT_STATS): the first event wave's phase 1 split
+      // into its own work and the wait for its pool words, and its phase 4
+      unsigned long long *const stats = tid == 64u ? p.ev_stats : nullptr;
+      uint64_t s_work = 0ull, s_wait = 0ull, s_write = 0ull;
       for (;;) {
         __syncthreads();                           // ---- H
-        const uint32_t body = C.body;
-        if (body != 0xFFFFFFFFu) {                 // the last trigger's broadcast (node.ts:72-80, :149-157)
-          const uint32_t bpos = C.bpos;
+        // the last trigger's broadcast (node.ts:72-80, :149-157) goes to [bpos,
+        // len): stored now, drained with this batch's loads; this batch itself
+        // reads that region's words as they are, d | body for position bpos + d
+        const uint32_t body = uni(C.body), bpos = uni(C.bpos);
+        const bool fresh = body != 0xFFFFFFFFu;
+        if (fresh)
           for (uint32_t d = ei; d < N; d += T) pool[bpos + d] = d | body;
-          vm_drain();
-          __syncthreads();                         // ---- H2
-        }
-        const uint32_t halted = C.halted, B = C.B, len = C.len, cur = C.cur, snap = C.snap;
-        const uint64_t rng = C.rng;
+        const uint32_t halted = uni(C.halted), B = uni(C.B), len = uni(C.len), cur = uni(C.cur), snap = uni(C.snap);
+        const uint64_t rng = uni64(C.rng);
         if (halted) break;
         if (snap) {
           // GET /getState (node.ts:197-199) mid-run: every node's state as of
@@ -534,12 +547,13 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
         // the word at t_i = len - 1 - i there (swap-remove)
         uint32_t qi = 0u, ti = 0u, pv = 0u, tv = 0u, hs = 0u;
         const bool act = ei < B;
+        const uint64_t t1 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
         if (act) {
           const uint64_t z = smix(rng + (uint64_t)(ei + 1u) * kGm);
           qi = (uint32_t)(((uint64_t)(uint32_t)(z >> 32) * (uint64_t)(len - ei)) >> 32);
           ti = len - 1u - ei;
-          pv = load(qi);
-          tv = load(ti);
+          pv = fresh && qi >= bpos ? (qi - bpos) | body : load(qi);
+          tv = fresh && ti >= bpos ? (ti - bpos) | body : load(ti);
           // the batch's pickers of qi: count and first (event index)
           const uint64_t key = (uint64_t)(qi + 1u) << 32;
           hs = hslot(qi, HS - 1u);
@@ -560,8 +574,15 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
           }
           // a pick of a tail position overwrites the word a later event moves
           if (qi >= len - B && qi != ti) atomicMax(&bmax[len - 1u - qi], ei + 1u);
+          if (stats) {
+            const uint64_t t2 = __builtin_amdgcn_s_memtime();
+            s_work += t2 - t1;
+            __builtin_amdgcn_s_waitcnt(0x0F70);
+            s_wait += __builtin_amdgcn_s_memtime() - t2;
+          }
           tvs[ei] = tv;
         }
+        vm_drain();                                // the broadcast's stores too, before any phase-4 store
         __syncthreads();                           // ---- B
         // ================= 2. resolution, one level deep
         uint32_t msg = pv, moved = tv;
@@ -588,7 +609,7 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
           if (cut) atomicMin(&C.conf[par], ei);
         }
         __syncthreads();                           // ---- C
-        const uint32_t used0 = C.conf[par];
+        const uint32_t used0 = uni(C.conf[par]);
         // ================= 3. POST /message (node.ts:45-158): the prefix's deliveries at once
         uint64_t inc = 0ull;
         uint32_t slot = 0u;
@@ -608,7 +629,7 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
         }
         __syncthreads();                           // ---- D
         uint32_t used = used0;
-        if (C.ncross[par]) {
+        if (uni(C.ncross[par])) {
           // a crossed slot triggers at the last batch event into it; the batch
           // ends after the earliest such event
           bool mine = false;
@@ -620,7 +641,7 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
           __syncthreads();                         // ---- E
           if (mine) atomicMin(&C.trig[par], smax[slot] - 1u);
           __syncthreads();                         // ---- F
-          const uint32_t tr = C.trig[par];
+          const uint32_t tr = uni(C.trig[par]);
           if (mine) smax[slot] = 0u;
           if (inc && ei > tr)
             __hip_atomic_fetch_add(reinterpret_cast<unsigned long long *>(&ibox[slot]), 0ull - inc,
@@ -631,6 +652,7 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
         }
         // ================= 4. pool writes: a position's last writer among the
         // used events stores its moved word, unless the position was popped
+        const uint64_t t4 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
         if (act) {
           const uint32_t nx = nxt[ei];
           if (ei < used && (nx == 0u || nx - 1u >= used) && qi < len - used) pool[qi] = moved;
@@ -639,7 +661,13 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
           nxt[ei] = 0u;
         }
         vm_drain();
+        if (stats) s_write += __builtin_amdgcn_s_memtime() - t4;
         par ^= 1u;
+      }
+      if (stats) {
+        atomicAdd(&stats[16], (unsigned long long)s_work);
+        atomicAdd(&stats[17], (unsigned long long)s_wait);
+        atomicAdd(&stats[18], (unsigned long long)s_write);
       }
     }
     // ---- outcome over the nodes still running
@@ -681,6 +709,264 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
   if (ctl && box && poll_out) __builtin_amdgcn_s_waitcnt(0x0F70);
 }
 
+// ---------------------------------------------------------------------------
+// Small networks (N <= kEventSerialMaxN): one wave runs the events one at a
+// time.  A batch of the workgroup kernel is cut by pick conflicts after
+// ~sqrt(len) events, and at N = 10 the pool holds ~50 messages: its batches
+// carried ~5 events for ~6k cycles (tools/live_profile.py).  Here an event is
+// a few scalar instructions around one LDS round trip: the pool (4N^2 + 64
+// words) is in LDS, and everything else in the wave's registers -- lane i
+// holds node i's x, k and compact index and its two inbox slots {c0, c1, len}
+// (8-bit fields, bit 31 killed), read and written with v_readlane /
+// v_writelane at a wave-uniform index; the node sets are 64-bit scalars.
+// The same definition as oracle (iii) event_trial() and the workgroup kernel.
+constexpr uint32_t kSerialKill = 1u << 31;
+
+__global__ void __launch_bounds__(64) benor_event_serial_kernel(KParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t pool[];   // [ev_cap] messages, then comp[4] u64
+  const uint32_t lane = threadIdx.x;
+  const uint32_t N = p.N, F = p.F, quorum = p.N - p.F, m = p.m, kmax = p.k_max;
+  uint64_t *comp = reinterpret_cast<uint64_t *>(pool + ((p.ev_cap + 1u) & ~1u));
+  const uint64_t all = N >= 64u ? ~0ull : (1ull << N) - 1ull;
+  const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
+  uint32_t *box = p.live_box;
+  unsigned long long *const stats = p.ev_stats;
+  // the mailbox poll, issued and consumed >= kPollTicks apart (as the
+  // workgroup kernel's control wave): the wave waits for no PCIe round trip
+  constexpr long long kPollTicks = 500;
+  uint64_t pv_req = 0ull;
+  uint32_t pv_word = 0u, snap_served = 0u, seq_seen = 0u;
+  bool apply_next = false;
+  long long polled = 0;
+  auto poll_issue = [&]() {
+    if (lane == 0u) pv_req = __hip_atomic_load(reinterpret_cast<uint64_t *>(box + kLiveReq), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lane == 1u) pv_word = __hip_atomic_load(box, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lane == 2u) pv_word = __hip_atomic_load(box + kSnapReq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    polled = wall_clock64();
+  };
+  if (box) poll_issue();
+  auto rl = [](uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); };
+  auto wl = [lane](uint32_t v, uint32_t val, uint32_t l) { return lane == l ? val : v; };   // lane l of v := val
+
+  for (uint64_t t = blockIdx.x; t < p.trial_count; t += gridDim.x) {
+    const uint64_t trial = p.trial_begin + t;
+    const uint32_t tlo = (uint32_t)trial, thi = (uint32_t)(trial >> 32);
+    const uint64_t t_start = stats ? __builtin_amdgcn_s_memtime() : 0ull;
+    const uint64_t w_start = stats ? (uint64_t)wall_clock64() : 0ull;
+    // ---- node.ts:21-26 (lane = node): faulty nodes killed with x = k = null
+    const uint32_t myid = lane < m ? p.live_ids[lane] : 0xFFFFFFFFu;   // compact lane c -> node id
+    uint64_t live = 0ull;
+    for (uint32_t c = 0; c < m; ++c) live |= 1ull << rl(myid, c);
+    uint64_t killed = all & ~live, decided = 0ull;
+    uint32_t X = 0xFFFFFFFFu, K = 0xFFFFFFFFu, CI = 0u, IBR = kSerialKill, IBP = kSerialKill;
+    for (uint32_t c = 0; c < m; ++c) CI = lane == rl(myid, c) ? c : CI;
+    if ((live >> lane) & 1ull) {
+      int32_t v;
+      if (p.init_mode == BO_INIT_RANDOM) {        // oracle_random_init
+        if (m <= 32u) {
+          v = (int32_t)((init_word_small(k0, k1, trial) >> CI) & 1u);
+        } else {
+          const uint4 ir = philox4x32_10<false>(k0, k1, make_uint4(tlo, thi, CI >> 7, kStreamInit << 24));
+          v = (int32_t)((coin_word_v(ir, ((CI >> 5) & 3u) + 1u) >> (CI & 31u)) & 1u);
+        }
+      } else {
+        v = p.init_x[lane];
+      }
+      X = (uint32_t)v;
+      K = 1u;                                      // /start: k = 1 (node.ts:172)
+      IBR = IBP = 0u;
+    }
+    if (lane < 4u) comp[lane] = 0ull;
+    // ---- /start (node.ts:167-188): every live node broadcasts its x, in node order
+    for (uint32_t c = 0; c < m; ++c) {
+      const uint32_t body = ((rl(X, rl(myid, c)) & 3u) << 13) | (1u << 15);
+      if (lane < N) pool[c * N + lane] = lane | body;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    uint64_t rng;
+    {
+      const uint4 o = philox4x32_10<false>(k0, k1, make_uint4(tlo, thi, 0u, kStreamOrder << 24));
+      rng = (((uint64_t)o.x << 32) | o.y) ^ 0xD1B54A32D192ED03ull;
+    }
+    uint32_t next = 0;
+    uint64_t next_key = uni64(p.ev_nstops ? p.ev_stops[0] : ~0ull);
+    uint32_t len = m * N, cur = 1u, R = 0u, halted = 0u, overflow = 0u, j = 64u, ZH = 0u;
+    uint64_t e = 0;
+    auto advance = [&]() {                         // node.ts:116-145 as DESIGN §2
+      for (;;) {
+        const uint64_t cw = uni64(comp[cur & 3u]);
+        if ((cw | killed) != all) return;
+        if ((decided | killed) == all) { halted = 1u; R = cur; return; }
+        if (cur >= kmax) { halted = 2u; R = cur; return; }
+        if (lane == 0u) comp[cur & 3u] = 0ull;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        ++cur;
+      }
+    };
+    auto kill = [&](uint32_t i) {                  // GET /stop (node.ts:191-194): drops every later message
+      killed |= 1ull << i;
+      if (lane == i) {
+        IBR |= kSerialKill;
+        IBP |= kSerialKill;
+      }
+    };
+    while (!halted) {
+      // ---- scheduled GET /stop before delivery e
+      bool crashed = false;
+      while ((next_key >> 12) == e) {
+        kill((uint32_t)(next_key & 4095u));
+        crashed = true;
+        ++next;
+        next_key = uni64(next < p.ev_nstops ? p.ev_stops[next] : ~0ull);
+      }
+      if (j == 64u) {
+        // the picks of the next 64 events (splitmix64 is a counter), and the mailbox
+        const uint64_t z = smix(rng + (uint64_t)(lane + 1u) * kGm);
+        ZH = (uint32_t)(z >> 32);
+        rng += 64ull * kGm;
+        j = 0u;
+        if (box && wall_clock64() - polled >= kPollTicks) {
+          const uint64_t req = apply_next ? uni64(pv_req) : 0ull;
+          const uint32_t seq = rl(pv_word, 1u), sreq = rl(pv_word, 2u);
+          apply_next = seq != seq_seen;
+          seq_seen = seq;
+          uint64_t fresh = req & all & ~killed;
+          for (uint64_t f = fresh; f; f &= f - 1ull) {
+            const uint32_t i = (uint32_t)__builtin_ctzll(f);
+            kill(i);
+            if (lane == 0u)
+              __hip_atomic_store(box + kLiveEv + i, e < 0xFFFFFFFFull ? (uint32_t)e : 0xFFFFFFFEu,
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+          crashed = crashed || fresh != 0ull;
+          if (sreq != snap_served) {
+            // GET /getState (node.ts:197-199) mid-run: every node's state before delivery e
+            snap_served = sreq;
+            if (lane < N) {
+              const bool f = (int32_t)K < 0 && (int32_t)X < 0;
+              const uint32_t kl = (uint32_t)((killed >> lane) & 1ull) | ((X & 0xFFu) << 8) |
+                                  ((f ? 0xFFu : (uint32_t)((decided >> lane) & 1ull)) << 16);
+              __hip_atomic_store(box + kSnapSt + 2u * lane, kl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              __hip_atomic_store(box + kSnapSt + 2u * lane + 1u, K, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            if (lane == 0u) {
+              __hip_atomic_store(box + kSnapE, (uint32_t)e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              __hip_atomic_store(box + kSnapE + 1u, (uint32_t)(e >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            __builtin_amdgcn_s_waitcnt(0x0F70);    // vmcnt(0): the states reached the host
+            if (lane == 0u) __hip_atomic_store(box + kSnapSeq, sreq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+          poll_issue();
+        }
+      }
+      if (crashed) {
+        if (killed == all) { halted = 3u; break; }
+        advance();
+        if (halted) break;
+      }
+      if (len == 0u) { halted = 3u; break; }
+      // ---- delivery e: uniform pick, swap-remove (oracle (iii))
+      const uint32_t qp = (uint32_t)(((uint64_t)rl(ZH, j) * (uint64_t)len) >> 32);
+      const uint32_t msg = uni(pool[qp]), tl = uni(pool[len - 1u]);
+      if (lane == 0u) pool[qp] = tl;
+      --len;
+      ++e;
+      ++j;
+      // ---- POST /message (node.ts:45-158)
+      const uint32_t to = msg & 4095u, ph = (msg >> 12) & 1u, xv = (msg >> 13) & 3u;
+      const uint32_t k = cur + (((msg >> 15) - cur) & 3u);
+      if (k >= kmax + 3u) continue;                // beyond the oracle's round window: dropped
+      uint32_t v = ph ? rl(IBP, to) : rl(IBR, to);
+      if (v & kSerialKill) continue;               // node.ts:45
+      v += (1u << 16) + (xv == 0u ? 1u : (xv == 1u ? 1u << 8 : 0u));
+      uint32_t body = 0xFFFFFFFFu;
+      if (((v >> 16) & 0xFFu) == quorum) {          // node.ts:52, :88: every message of the phase arrived
+        const uint32_t c0 = v & 0xFFu, c1 = (v >> 8) & 0xFFu;
+        v = 0u;                                    // the slot is free
+        if (ph == 0u) {                            // node.ts:53-80
+          const uint32_t pv = c0 > c1 ? 0u : (c1 > c0 ? 1u : 2u);
+          body = (1u << 12) | (pv << 13) | ((k & 3u) << 15);
+        } else {                                   // node.ts:89-157
+          uint32_t nx;
+          bool dec = true;
+          if (c0 > F) nx = 0u;
+          else if (c1 > F) nx = 1u;
+          else {
+            dec = false;
+            if (c0 + c1 > 0u && c0 > c1) nx = 0u;
+            else if (c0 + c1 > 0u && c0 < c1) nx = 1u;
+            else {
+              const uint32_t c = rl(CI, to);       // the coin of compact node c in round k (node.ts:111)
+              const uint4 rr = coin_block<false>(k0, k1, tlo, thi, c, k);
+              nx = uni((coin_word(rr, k) >> (c & 31u)) & 1u);
+            }
+          }
+          X = wl(X, nx, to);
+          K = wl(K, k + 1u, to);
+          if (dec) decided |= 1ull << to;
+          if (lane == 0u) comp[k & 3u] |= 1ull << to;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+          advance();
+          if (!halted) body = (nx << 13) | (((k + 1u) & 3u) << 15);
+        }
+      }
+      if (ph) IBP = wl(IBP, v, to);
+      else IBR = wl(IBR, v, to);
+      if (body != 0xFFFFFFFFu) {                   // the broadcast to all N nodes
+        if (len + N > p.ev_cap) {
+          overflow = 1u;
+          halted = 3u;
+          break;
+        }
+        if (lane < N) pool[len + lane] = lane | body;
+        len += N;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      }
+    }
+    // ---- outcome over the nodes still running
+    const bool run = lane < N && !((killed >> lane) & 1ull);
+    const bool g0 = __any(run && X == 0u), g1 = __any(run && X == 1u), gq = __any(run && X != 0u && X != 1u);
+    const bool gl = __any(run);
+    const uint32_t vv = (!gl || gq || (g0 && g1)) ? 2u : (g1 ? 1u : 0u);
+    if (lane == 0u) {
+      atomicAdd(&p.hist[halted == 1u ? (R * 3u + vv) : vv], 1ull);
+      if (halted == 1u && vv == 2u) atomicAdd(&p.hist[p.hist_len - 1u], 1ull);
+      if (overflow && p.rounds_out) atomicOr(p.rounds_out, 0x80000000u);
+      if (overflow && p.overflow) atomicOr(p.overflow, 2u);
+      if (p.node_out && p.rounds_out) atomicOr(p.rounds_out, halted == 1u ? R : 0u);
+      if (stats) {
+        atomicAdd(&stats[1], (unsigned long long)e);
+        atomicAdd(&stats[0], (unsigned long long)e);          // one event per step
+        atomicAdd(&stats[12], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_start));
+        atomicAdd(&stats[13], (unsigned long long)((uint64_t)wall_clock64() - w_start));
+      }
+    }
+    if (p.node_out && lane < N) {
+      bo_node_state ns;
+      const bool f = (int32_t)K < 0 && (int32_t)X < 0;   // faulty from launch (never ran)
+      ns.killed = (int8_t)((killed >> lane) & 1ull);
+      ns.x = (int8_t)X;
+      ns.decided = f ? (int8_t)-1 : (int8_t)((decided >> lane) & 1ull);
+      ns.pad = 0;
+      ns.k = (int32_t)K;
+      p.node_out[lane] = ns;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
+  if (box) __builtin_amdgcn_s_waitcnt(0x0F70);     // the last poll lands before the wave ends
+}
+
 uint32_t event_wg_waves(const KParams &p) {
   const uint32_t forced = knob_u32("BENOR_LIVE_WAVES", 0u);
   if (forced == 1u || forced == 3u || forced == 7u || forced == 15u) return forced;
@@ -692,9 +978,8 @@ uint32_t event_wg_waves(const KParams &p) {
 
 bool event_wg_lds_pool(const KParams &p) { return (uint64_t)p.ev_cap * 4u <= kEventBigLdsPool; }
 
-uint32_t event_wg_lds_bytes(const KParams &p, uint32_t W) {
+static uint32_t wg_lds_bytes(const KParams &p, uint32_t W, uint32_t HS) {
   const uint32_t N = p.N;
-  const uint32_t HS = W == 1u ? hash_slots(1) : W == 3u ? hash_slots(3) : W == 7u ? hash_slots(7) : hash_slots(15);
   uint32_t b = ((uint32_t)sizeof(Ctl) + 15u) & ~15u;
   b += 16u * N + 8u * 64u * 6u + 8u * HS + 8u * 64u + 8u * p.ev_rstops;   // ibox, killed/decided/comp, hash, Floyd set, keys
   b += 8u * N + 3u * 4u * 64u * W;                                        // smax; bmax, nxt, tvs
@@ -703,8 +988,16 @@ uint32_t event_wg_lds_bytes(const KParams &p, uint32_t W) {
   return b;
 }
 
+uint32_t event_wg_hash_slots(const KParams &p, uint32_t W) {
+  const uint32_t big = pow2_ceil(4u * 64u * W), small = pow2_ceil(2u * 64u * W);
+  return wg_lds_bytes(p, W, big) <= 150u * 1024u ? big : small;
+}
+
+uint32_t event_wg_lds_bytes(const KParams &p, uint32_t W) { return wg_lds_bytes(p, W, event_wg_hash_slots(p, W)); }
+
 template <int W, bool LP>
-static hipError_t launch_wg(const KParams &p, int grid, hipStream_t s) {
+static hipError_t launch_wg(KParams p, int grid, hipStream_t s) {
+  p.ev_hs = event_wg_hash_slots(p, (uint32_t)W);
   const uint32_t lds = event_wg_lds_bytes(p, (uint32_t)W);
   if (lds > 64u * 1024u) {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&benor_event_wg_kernel<W, LP>),
@@ -715,7 +1008,26 @@ static hipError_t launch_wg(const KParams &p, int grid, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Small networks run on the serial kernel, unless a random /stop schedule
+// (drawn by the workgroup kernel's control wave) or a forced wave count asks
+// for the workgroup kernel.
+bool event_serial(const KParams &p) {
+  return p.N <= kEventSerialMaxN && p.ev_rstops == 0u && knob_u32("BENOR_LIVE_WAVES", 0u) == 0u;
+}
+
+uint32_t event_serial_lds_bytes(const KParams &p) { return 4u * ((p.ev_cap + 1u) & ~1u) + 4u * 8u; }
+
 hipError_t launch_event_wg(const KParams &p, int grid, hipStream_t s) {
+  if (event_serial(p)) {
+    const uint32_t lds = event_serial_lds_bytes(p);
+    if (lds > 64u * 1024u) {
+      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&benor_event_serial_kernel),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(benor_event_serial_kernel, dim3(grid), dim3(64), lds, s, p);
+    return hipGetLastError();
+  }
   const uint32_t W = event_wg_waves(p);
   const bool lp = event_wg_lds_pool(p);
   if (W == 1u) return lp ? launch_wg<1, true>(p, grid, s) : launch_wg<1, false>(p, grid, s);

@@ -109,8 +109,9 @@ struct KParams {
   // live runs, and batch plans under BENOR_EVENT_FORM=wg
   uint32_t ev_wg;
   // diagnostics (BENOR_EVENT_STATS): that kernel's per-batch counters and
-  // cycle split, 16 u64 (device) or nullptr
+  // cycle split, 24 u64 (device) or nullptr
   unsigned long long *ev_stats;
+  uint32_t ev_hs;                  // its LDS hash slots per batch (a power of two; set at launch)
   // W kernel trial-list mode: run the trials trial_begin + trial_list[i],
   // i < min(*trial_list_len, trial_count), instead of a contiguous range
   const uint32_t *trial_list, *trial_list_len;
@@ -173,6 +174,12 @@ hipError_t launch_event_big(const KParams &p, int grid_blocks, hipStream_t strea
 // workgroup of a control wave and 1, 3, 7 or 15 event waves; live runs (mailbox
 // /stop, /getState snapshots) and single-trial network runs.
 uint32_t event_wg_waves(const KParams &p);
+// ... and for N <= kEventSerialMaxN (no random /stop schedule, no forced wave
+// count) the serial one-wave form of it: the pool in LDS, inboxes and node
+// state in lane registers, one event per step.
+constexpr uint32_t kEventSerialMaxN = 64;
+bool event_serial(const KParams &p);
+uint32_t event_serial_lds_bytes(const KParams &p);
 bool event_wg_lds_pool(const KParams &p);
 uint32_t event_wg_lds_bytes(const KParams &p, uint32_t waves);
 hipError_t launch_event_wg(const KParams &p, int grid_blocks, hipStream_t stream);

@@ -171,7 +171,7 @@ std::vector<LiveSlot *> g_free_slots;
 // Where the run's results sit in the slot's buffer.
 struct WgRun {
   size_t o_st = 0, o_r = 0;            // states [N], round word (the head read back ends after it)
-  size_t o_stats = 0;                  // BENOR_EVENT_STATS counters (16 u64, after the round word)
+  size_t o_stats = 0;                  // BENOR_EVENT_STATS counters (24 u64, after the round word)
   uint32_t N = 0, F = 0;
 };
 }  // namespace
@@ -1083,7 +1083,7 @@ int wg_launch(LiveSlot *sl, const bo_trials_cfg *cfg, bool live, WgRun &run) {
   std::sort(stops.begin(), stops.end());
   const size_t o_st = 16u, o_h = align_up(o_st + sizeof(bo_node_state) * N, 16u);
   const size_t o_r = o_h + sizeof(uint64_t) * H, o_stats = align_up(o_r + 4u, 16u);
-  const size_t o_live = o_stats + 16u * sizeof(uint64_t);
+  const size_t o_live = o_stats + 24u * sizeof(uint64_t);
   const size_t o_ix = align_up(o_live + sizeof(uint32_t) * m, 16u);
   const size_t o_stops = align_up(o_ix + N, 16u);
   const size_t o_pool = align_up(o_stops + sizeof(uint64_t) * stops.size(), 256u);
@@ -1136,16 +1136,16 @@ int wg_launch(LiveSlot *sl, const bo_trials_cfg *cfg, bool live, WgRun &run) {
 // The run's head (flag | states | hist | rounds), read back on the slot's stream.
 int wg_read(LiveSlot *sl, const WgRun &run, uint32_t N, std::vector<bo_node_state> &states) {
   if (const char *path = benor::knob("BENOR_EVENT_STATS")) {   // diagnostics: one JSON line per run
-    unsigned long long s[16] = {};
+    unsigned long long s[24] = {};
     if (hipMemcpyAsync(s, sl->d + run.o_stats, sizeof s, hipMemcpyDeviceToHost, sl->s) == hipSuccess &&
         hipStreamSynchronize(sl->s) == hipSuccess)
       if (FILE *f = std::fopen(path, "a")) {
-        static const char *names[16] = {"batches", "events", "batch_slots", "trigger_batches", "conflict_cut",
+        static const char *names[19] = {"batches", "events", "batch_slots", "trigger_batches", "conflict_cut",
                                         "cyc_top", "cyc_picks", "cyc_lookup", "cyc_deliver", "cyc_cross",
                                         "cyc_writes_trigger", "cyc_bcast", "cycles", "wall_ticks", "cross_batches",
-                                        "snapshots"};
+                                        "snapshots", "ev_work", "ev_wait", "ev_write"};
         std::fprintf(f, "{\"N\": %u, \"F\": %u", run.N, run.F);
-        for (int i = 0; i < 16; ++i) std::fprintf(f, ", \"%s\": %llu", names[i], s[i]);
+        for (int i = 0; i < 19; ++i) std::fprintf(f, ", \"%s\": %llu", names[i], s[i]);
         std::fprintf(f, "}\n");
         std::fclose(f);
       }
