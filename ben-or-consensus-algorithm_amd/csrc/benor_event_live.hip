@@ -46,6 +46,7 @@
 // 4N^2 + 64 words fit kEventBigLdsPool (N <= 78) -- in LDS.
 #include "benor_device.h"
 
+#include <type_traits>
 #include <utility>
 
 namespace benor {
@@ -710,23 +711,36 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
 }
 
 // ---------------------------------------------------------------------------
-// Small networks (N <= kEventSerialMaxN): one wave runs the events one at a
-// time.  A batch of the workgroup kernel is cut by pick conflicts after
-// ~sqrt(len) events, and at N = 10 the pool holds ~50 messages: its batches
-// carried ~5 events for ~6k cycles (tools/live_profile.py).  Here an event is
-// a few scalar instructions around one LDS round trip: the pool (4N^2 + 64
-// words) is in LDS, and everything else in the wave's registers -- lane i
-// holds node i's x, k and compact index and its two inbox slots {c0, c1, len}
-// (8-bit fields, bit 31 killed), read and written with v_readlane /
-// v_writelane at a wave-uniform index; the node sets are 64-bit scalars.
+// Small networks (N <= kEventWaveMaxN): one wave, no barriers.  A batch of
+// the workgroup kernel is cut by pick conflicts after ~sqrt(len) events, and
+// at N = 10 the pool holds ~50 messages: its batches carried ~5 events for
+// ~6k cycles, and a one-event-per-step loop costs ~700 cycles per event (one
+// wave issues an instruction every ~10 cycles, tools/live_profile.py).  Here
+// the wave takes micro-batches of up to 64 events, lane i = event e + i:
+//   * picks as the workgroup kernel (they depend on e and len only), the pool
+//     (4N^2 + 64 words) in LDS;
+//   * no conflict cuts: the word event i takes is followed back through the
+//     batch's earlier moves (position p before event i holds what the last
+//     earlier event j with q_j = p moved there from t_j, before j; an LDS
+//     table of 64-bit lane masks by position hash finds j), so a batch runs
+//     to its first trigger;
+//   * the batch is delivered at once (64-bit LDS adds of {len, c0 | c1} to
+//     the inbox slots; a slot reaching its quorum triggers at its last batch
+//     event, found by one ballot per crossed slot), later adds undone;
+//   * each position the batch wrote and the pool keeps gets its last
+//     writer's word, followed back the same way;
+//   * the trigger (node.ts:52-80, :88-157), the stops, the mailbox and the
+//     snapshots are scalar code, node state in lane registers (lane = node).
 // The same definition as oracle (iii) event_trial() and the workgroup kernel.
-constexpr uint32_t kSerialKill = 1u << 31;
-
-__global__ void __launch_bounds__(64) benor_event_serial_kernel(KParams p) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t pool[];   // [ev_cap] messages, then comp[4] u64
+__global__ void __launch_bounds__(64) benor_event_wave_kernel(KParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t pool[];   // [cap] messages | picks | writers | ibox | comp
   const uint32_t lane = threadIdx.x;
-  const uint32_t N = p.N, F = p.F, quorum = p.N - p.F, m = p.m, kmax = p.k_max;
-  uint64_t *comp = reinterpret_cast<uint64_t *>(pool + ((p.ev_cap + 1u) & ~1u));
+  const uint32_t N = p.N, F = p.F, quorum = p.N - p.F, m = p.m, kmax = p.k_max, cap = p.ev_cap;
+  const uint32_t capa = (cap + 1u) & ~1u;
+  uint32_t *qarr = pool + capa;                                      // [64] the batch's picks
+  uint64_t *wm = reinterpret_cast<uint64_t *>(qarr + 64);            // [256] batch lanes writing a position, by hash
+  uint64_t *ibox = wm + 256;                                         // [2N] {c0, c1, len}, bit 63 killed
+  uint64_t *comp = ibox + 128;                                       // [4] round k complete at k & 3
   const uint64_t all = N >= 64u ? ~0ull : (1ull << N) - 1ull;
   const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
   uint32_t *box = p.live_box;
@@ -748,6 +762,12 @@ __global__ void __launch_bounds__(64) benor_event_serial_kernel(KParams p) {
   if (box) poll_issue();
   auto rl = [](uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); };
   auto wl = [lane](uint32_t v, uint32_t val, uint32_t l) { return lane == l ? val : v; };   // lane l of v := val
+  auto lds_order = []() {                          // one wave's LDS operations are in order: compiler ordering only
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+  };
+  for (uint32_t i = lane; i < 256u; i += 64u) wm[i] = 0ull;
+  uint64_t cyc[5] = {0ull, 0ull, 0ull, 0ull, 0ull};
 
   for (uint64_t t = blockIdx.x; t < p.trial_count; t += gridDim.x) {
     const uint64_t trial = p.trial_begin + t;
@@ -759,7 +779,7 @@ __global__ void __launch_bounds__(64) benor_event_serial_kernel(KParams p) {
     uint64_t live = 0ull;
     for (uint32_t c = 0; c < m; ++c) live |= 1ull << rl(myid, c);
     uint64_t killed = all & ~live, decided = 0ull;
-    uint32_t X = 0xFFFFFFFFu, K = 0xFFFFFFFFu, CI = 0u, IBR = kSerialKill, IBP = kSerialKill;
+    uint32_t X = 0xFFFFFFFFu, K = 0xFFFFFFFFu, CI = 0u;
     for (uint32_t c = 0; c < m; ++c) CI = lane == rl(myid, c) ? c : CI;
     if ((live >> lane) & 1ull) {
       int32_t v;
@@ -775,17 +795,15 @@ __global__ void __launch_bounds__(64) benor_event_serial_kernel(KParams p) {
       }
       X = (uint32_t)v;
       K = 1u;                                      // /start: k = 1 (node.ts:172)
-      IBR = IBP = 0u;
     }
+    for (uint32_t s = lane; s < 128u; s += 64u) ibox[s] = s < 2u * N && ((live >> (s >> 1)) & 1ull) ? 0ull : kDead;
     if (lane < 4u) comp[lane] = 0ull;
     // ---- /start (node.ts:167-188): every live node broadcasts its x, in node order
     for (uint32_t c = 0; c < m; ++c) {
       const uint32_t body = ((rl(X, rl(myid, c)) & 3u) << 13) | (1u << 15);
       if (lane < N) pool[c * N + lane] = lane | body;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    lds_order();
     uint64_t rng;
     {
       const uint4 o = philox4x32_10<false>(k0, k1, make_uint4(tlo, thi, 0u, kStreamOrder << 24));
@@ -793,8 +811,8 @@ __global__ void __launch_bounds__(64) benor_event_serial_kernel(KParams p) {
     }
     uint32_t next = 0;
     uint64_t next_key = uni64(p.ev_nstops ? p.ev_stops[0] : ~0ull);
-    uint32_t len = m * N, cur = 1u, R = 0u, halted = 0u, overflow = 0u, j = 64u, ZH = 0u;
-    uint64_t e = 0;
+    uint32_t len = m * N, cur = 1u, R = 0u, halted = 0u, overflow = 0u;
+    uint64_t e = 0, batches = 0, trig = 0, c_z = stats ? __builtin_amdgcn_s_memtime() : 0ull;
     auto advance = [&]() {                         // node.ts:116-145 as DESIGN §2
       for (;;) {
         const uint64_t cw = uni64(comp[cur & 3u]);
@@ -802,18 +820,14 @@ __global__ void __launch_bounds__(64) benor_event_serial_kernel(KParams p) {
         if ((decided | killed) == all) { halted = 1u; R = cur; return; }
         if (cur >= kmax) { halted = 2u; R = cur; return; }
         if (lane == 0u) comp[cur & 3u] = 0ull;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        lds_order();
         ++cur;
       }
     };
     auto kill = [&](uint32_t i) {                  // GET /stop (node.ts:191-194): drops every later message
       killed |= 1ull << i;
-      if (lane == i) {
-        IBR |= kSerialKill;
-        IBP |= kSerialKill;
-      }
+      if (lane < 2u && i < N) ibox[2u * i + lane] |= kDead;
+      lds_order();
     };
     while (!halted) {
       // ---- scheduled GET /stop before delivery e
@@ -824,24 +838,376 @@ __global__ void __launch_bounds__(64) benor_event_serial_kernel(KParams p) {
         ++next;
         next_key = uni64(next < p.ev_nstops ? p.ev_stops[next] : ~0ull);
       }
-      if (j == 64u) {
-        // the picks of the next 64 events (splitmix64 is a counter), and the mailbox
+      if (box && wall_clock64() - polled >= kPollTicks) {
+        // live GET /stop requests (applied one poll after their sequence word,
+        // so a burst lands together) and GET /getState snapshot requests
+        const uint64_t req = apply_next ? uni64(pv_req) : 0ull;
+        const uint32_t seq = rl(pv_word, 1u), sreq = rl(pv_word, 2u);
+        apply_next = seq != seq_seen;
+        seq_seen = seq;
+        const uint64_t fresh = req & all & ~killed;
+        for (uint64_t f = fresh; f; f &= f - 1ull) {
+          const uint32_t i = (uint32_t)__builtin_ctzll(f);
+          kill(i);
+          if (lane == 0u)
+            __hip_atomic_store(box + kLiveEv + i, e < 0xFFFFFFFFull ? (uint32_t)e : 0xFFFFFFFEu, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        crashed = crashed || fresh != 0ull;
+        if (crashed) {
+          if (killed == all) { halted = 3u; break; }
+          advance();
+          if (halted) break;
+          crashed = false;
+        }
+        if (sreq != snap_served) {
+          // GET /getState (node.ts:197-199) mid-run: every node's state before delivery e
+          snap_served = sreq;
+          if (lane < N) {
+            const bool f = (int32_t)K < 0 && (int32_t)X < 0;
+            const uint32_t kl = (uint32_t)((killed >> lane) & 1ull) | ((X & 0xFFu) << 8) |
+                                ((f ? 0xFFu : (uint32_t)((decided >> lane) & 1ull)) << 16);
+            __hip_atomic_store(box + kSnapSt + 2u * lane, kl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(box + kSnapSt + 2u * lane + 1u, K, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+          if (lane == 0u) {
+            __hip_atomic_store(box + kSnapE, (uint32_t)e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(box + kSnapE + 1u, (uint32_t)(e >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+          __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0): the states reached the host
+          if (lane == 0u) __hip_atomic_store(box + kSnapSeq, sreq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        poll_issue();
+      }
+      if (crashed) {
+        if (killed == all) { halted = 3u; break; }
+        advance();
+        if (halted) break;
+      }
+      if (len == 0u) { halted = 3u; break; }
+      // ---- a micro-batch of events e .. e + B - 1 (lane i: event e + i)
+      const uint64_t c_a = stats ? __builtin_amdgcn_s_memtime() : 0ull;
+      uint32_t B = len < 64u ? len : 64u;
+      if (next_key != ~0ull && (next_key >> 12) - e < B) B = (uint32_t)((next_key >> 12) - e);
+      const bool act = lane < B;
+      uint32_t qi = 0u, ti = 0u;
+      bool wr = false;
+      if (act) {
         const uint64_t z = smix(rng + (uint64_t)(lane + 1u) * kGm);
-        ZH = (uint32_t)(z >> 32);
-        rng += 64ull * kGm;
-        j = 0u;
-        if (box && wall_clock64() - polled >= kPollTicks) {
+        qi = (uint32_t)(((uint64_t)(uint32_t)(z >> 32) * (uint64_t)(len - lane)) >> 32);
+        ti = len - 1u - lane;
+        wr = qi != ti;                             // event i moves the tail word t_i to q_i
+        qarr[lane] = qi;
+        if (wr) atomicOr(reinterpret_cast<unsigned long long *>(&wm[qi & 255u]), 1ull << lane);
+      }
+      lds_order();
+      // the word at position pp before event ii: the word event j (the last
+      // earlier writer of pp) moved there from t_j = len - 1 - j, before j;
+      // pp never was a tail (pp < len - ii), so the chain ends in the pool
+      auto word_at = [&](uint32_t pp, uint32_t ii) {
+        for (;;) {
+          uint64_t mm = wm[pp & 255u] & ((1ull << ii) - 1ull);
+          uint32_t j = 64u;
+          while (mm) {
+            const uint32_t c = 63u - (uint32_t)__builtin_clzll(mm);
+            if (qarr[c] == pp) { j = c; break; }
+            mm &= ~(1ull << c);
+          }
+          if (j == 64u) return pool[pp];
+          pp = len - 1u - j;
+          ii = j;
+        }
+      };
+      const uint32_t pv = act ? word_at(qi, lane) : 0u;
+      const uint64_t c_b = stats ? __builtin_amdgcn_s_memtime() : 0ull;
+      // ---- POST /message (node.ts:45-158): the batch's deliveries at once
+      uint64_t inc = 0ull;
+      uint32_t slot = 0u;
+      if (act) {
+        const uint32_t to = pv & 4095u, ph = (pv >> 12) & 1u, xv = (pv >> 13) & 3u;
+        const uint32_t k = cur + (((pv >> 15) - cur) & 3u);
+        slot = 2u * to + ph;
+        if (k < kmax + 3u)                         // beyond the oracle's round window: dropped
+          inc = (1ull << 26) + (xv == 0u ? 1ull : (xv == 1u ? 1ull << 13 : 0ull));
+      }
+      bool cross = false;
+      if (inc) {
+        const uint64_t old = __hip_atomic_fetch_add(reinterpret_cast<unsigned long long *>(&ibox[slot]), inc,
+                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        // killed receivers drop the message (node.ts:45): their slot counts
+        // on, never tested; a live slot crosses its quorum (node.ts:52, :88)
+        cross = !(old & kDead) && ((old >> 26) & kF13) + 1u == quorum;
+      }
+      uint32_t tr = 0xFFFFFFFFu;
+      for (uint64_t xm = __ballot(cross); xm; xm &= xm - 1ull) {
+        // a crossed slot triggers at the last batch event into it
+        const uint32_t s = rl(slot, (uint32_t)__builtin_ctzll(xm));
+        const uint64_t into = __ballot(inc != 0ull && slot == s);
+        const uint32_t last = 63u - (uint32_t)__builtin_clzll(into);
+        tr = last < tr ? last : tr;
+      }
+      uint32_t used = B;
+      if (tr != 0xFFFFFFFFu) {
+        if (inc && lane > tr)                      // the batch ends at its first trigger: later adds undone
+          __hip_atomic_fetch_add(reinterpret_cast<unsigned long long *>(&ibox[slot]), 0ull - inc, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+        used = tr + 1u;
+      }
+      const uint64_t c_c = stats ? __builtin_amdgcn_s_memtime() : 0ull;
+      // ---- the pool after the batch: each position below the new length that
+      // the batch wrote keeps its last writer's word
+      bool last = false;
+      if (lane < used && wr && qi < len - used) {
+        const uint64_t below = used >= 64u ? ~0ull : (1ull << used) - 1ull;
+        uint64_t mm = wm[qi & 255u] & below & ~((2ull << lane) - 1ull);
+        last = true;
+        while (mm) {
+          const uint32_t c = (uint32_t)__builtin_ctzll(mm);
+          if (qarr[c] == qi) { last = false; break; }
+          mm &= mm - 1ull;
+        }
+      }
+      const uint32_t wv = last ? word_at(ti, lane) : 0u;
+      lds_order();
+      if (last) pool[qi] = wv;
+      if (wr) wm[qi & 255u] = 0ull;
+      lds_order();
+      len -= used;
+      e += used;
+      rng += (uint64_t)used * kGm;
+      ++batches;
+      if (stats) {
+        const uint64_t c_d = __builtin_amdgcn_s_memtime();
+        cyc[0] += c_a - c_z;
+        cyc[1] += c_b - c_a;
+        cyc[2] += c_c - c_b;
+        cyc[3] += c_d - c_c;
+        c_z = c_d;
+      }
+      if (tr == 0xFFFFFFFFu) continue;
+      // ---- the trigger (node.ts:52-80 R-phase, :88-157 P-phase)
+      const uint32_t msg = rl(pv, tr), ts = rl(slot, tr);
+      const uint32_t to = msg & 4095u, ph = (msg >> 12) & 1u;
+      const uint32_t k = cur + (((msg >> 15) - cur) & 3u);
+      const uint64_t v = uni64(ibox[ts]);
+      if (lane == 0u) ibox[ts] = 0ull;             // every message of the phase arrived: the slot is free
+      lds_order();
+      const uint32_t c0 = (uint32_t)(v & kF13), c1 = (uint32_t)((v >> 13) & kF13);
+      uint32_t body = 0xFFFFFFFFu;
+      if (ph == 0u) {
+        const uint32_t pr = c0 > c1 ? 0u : (c1 > c0 ? 1u : 2u);
+        body = (1u << 12) | (pr << 13) | ((k & 3u) << 15);
+      } else {
+        uint32_t nx;
+        bool dec = true;
+        if (c0 > F) nx = 0u;
+        else if (c1 > F) nx = 1u;
+        else {
+          dec = false;
+          if (c0 + c1 > 0u && c0 > c1) nx = 0u;
+          else if (c0 + c1 > 0u && c0 < c1) nx = 1u;
+          else {
+            const uint32_t c = rl(CI, to);         // the coin of compact node c in round k (node.ts:111)
+            const uint4 rr = coin_block<false>(k0, k1, tlo, thi, c, k);
+            nx = uni((coin_word(rr, k) >> (c & 31u)) & 1u);
+          }
+        }
+        X = wl(X, nx, to);
+        K = wl(K, k + 1u, to);
+        if (dec) decided |= 1ull << to;
+        if (lane == 0u) comp[k & 3u] |= 1ull << to;
+        lds_order();
+        advance();
+        if (!halted) body = (nx << 13) | (((k + 1u) & 3u) << 15);
+      }
+      if (body != 0xFFFFFFFFu) {                   // the broadcast to all N nodes
+        if (len + N > cap) {
+          overflow = 1u;
+          halted = 3u;
+          break;
+        }
+        if (lane < N) pool[len + lane] = lane | body;
+        len += N;
+        lds_order();
+      }
+      ++trig;
+      if (stats) {
+        const uint64_t c_d = __builtin_amdgcn_s_memtime();
+        cyc[4] += c_d - c_z;
+        c_z = c_d;
+      }
+    }
+    // ---- outcome over the nodes still running
+    const bool run = lane < N && !((killed >> lane) & 1ull);
+    const bool g0 = __any(run && X == 0u), g1 = __any(run && X == 1u), gq = __any(run && X != 0u && X != 1u);
+    const bool gl = __any(run);
+    const uint32_t vv = (!gl || gq || (g0 && g1)) ? 2u : (g1 ? 1u : 0u);
+    if (lane == 0u) {
+      atomicAdd(&p.hist[halted == 1u ? (R * 3u + vv) : vv], 1ull);
+      if (halted == 1u && vv == 2u) atomicAdd(&p.hist[p.hist_len - 1u], 1ull);
+      if (overflow && p.rounds_out) atomicOr(p.rounds_out, 0x80000000u);
+      if (overflow && p.overflow) atomicOr(p.overflow, 2u);
+      if (p.node_out && p.rounds_out) atomicOr(p.rounds_out, halted == 1u ? R : 0u);
+      if (stats) {
+        atomicAdd(&stats[0], (unsigned long long)batches);
+        atomicAdd(&stats[1], (unsigned long long)e);
+        atomicAdd(&stats[3], (unsigned long long)trig);
+        atomicAdd(&stats[5], (unsigned long long)cyc[0]);
+        atomicAdd(&stats[6], (unsigned long long)cyc[1]);
+        atomicAdd(&stats[8], (unsigned long long)cyc[2]);
+        atomicAdd(&stats[10], (unsigned long long)cyc[3]);
+        atomicAdd(&stats[11], (unsigned long long)cyc[4]);
+        atomicAdd(&stats[12], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_start));
+        atomicAdd(&stats[13], (unsigned long long)((uint64_t)wall_clock64() - w_start));
+      }
+    }
+    if (p.node_out && lane < N) {
+      bo_node_state ns;
+      const bool f = (int32_t)K < 0 && (int32_t)X < 0;   // faulty from launch (never ran)
+      ns.killed = (int8_t)((killed >> lane) & 1ull);
+      ns.x = (int8_t)X;
+      ns.decided = f ? (int8_t)-1 : (int8_t)((decided >> lane) & 1ull);
+      ns.pad = 0;
+      ns.k = (int32_t)K;
+      p.node_out[lane] = ns;
+    }
+    lds_order();
+  }
+  if (box) __builtin_amdgcn_s_waitcnt(0x0F70);     // the last poll lands before the wave ends
+}
+
+// ---------------------------------------------------------------------------
+// The smallest networks (N <= kEventRegMaxN): one wave, one event per step,
+// no memory.  At N = 10 a batch of the wave kernel above carries ~10 events
+// (it ends at its first trigger, and every ~10th delivery is one) for ~730
+// instructions and ~30 LDS round trips (tools/live_profile.py, PMC).  Here
+// the whole round state lives in registers:
+//   * the pool in R VGPRs, position p in lane p & 63 of register p >> 6
+//     (R * 64 >= 4N^2 + 64); a step reads its two words with v_readlane
+//     through a uniform register index (s_set_gpr_idx) and writes the moved
+//     word back with one lane select -- about 15 instructions, no waits;
+//   * the inbox slots in one VGPR, slot s = 2 * to + ph in lane s, packed
+//     {len << 24 | c1 << 16 | c0 << 8}: a pool word carries its slot, k & 3
+//     and the increment its delivery adds, so a delivery is one read-add-select;
+//   * 64 picks per block (lane i: the pick word of event e + i, splitmix64
+//     is a counter), one readlane per event;
+//   * the trigger, the stops, the mailbox and the snapshots as the wave
+//     kernel, node state in lane registers and SGPR masks.
+// Words: slot | (k & 3) << 6 | {1 << 24 | (x == 0) << 8 | (x == 1) << 16}.
+template <int R>
+__global__ void __launch_bounds__(64) benor_event_reg_kernel(KParams p) {
+  const uint32_t lane = threadIdx.x;
+  const uint32_t N = p.N, F = p.F, quorum = p.N - p.F, m = p.m, kmax = p.k_max, cap = p.ev_cap;
+  const uint64_t all = (1ull << N) - 1ull;                           // N <= kEventRegMaxN
+  const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
+  uint32_t *box = p.live_box;
+  unsigned long long *const stats = p.ev_stats;
+  constexpr long long kPollTicks = 500;                              // as the wave kernel
+  uint64_t pv_req = 0ull;
+  uint32_t pv_word = 0u, snap_served = 0u, seq_seen = 0u;
+  bool apply_next = false;
+  long long polled = 0;
+  auto poll_issue = [&]() {
+    if (lane == 0u) pv_req = __hip_atomic_load(reinterpret_cast<uint64_t *>(box + kLiveReq), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lane == 1u) pv_word = __hip_atomic_load(box, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lane == 2u) pv_word = __hip_atomic_load(box + kSnapReq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    polled = wall_clock64();
+  };
+  if (box) poll_issue();
+  auto rl = [](uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); };
+  auto wl = [lane](uint32_t v, uint32_t val, uint32_t l) { return lane == l ? val : v; };   // lane l of v := val
+  auto inc_of = [](uint32_t x) { return (1u << 24) | (x == 0u ? 1u << 8 : (x == 1u ? 1u << 16 : 0u)); };
+  uint32_t P[R];
+
+  for (uint64_t t = blockIdx.x; t < p.trial_count; t += gridDim.x) {
+    const uint64_t trial = p.trial_begin + t;
+    const uint32_t tlo = (uint32_t)trial, thi = (uint32_t)(trial >> 32);
+    uint64_t t_start = stats ? __builtin_amdgcn_s_memtime() : 0ull;
+    uint64_t w_start = stats ? (uint64_t)wall_clock64() : 0ull;
+    asm volatile("" : "+v"(t_start), "+v"(w_start));   // cold: kept out of the SGPR file
+    // ---- node.ts:21-26 (lane = node): faulty nodes killed with x = k = null
+    const uint32_t myid = lane < m ? p.live_ids[lane] : 0xFFFFFFFFu;   // compact lane c -> node id
+    uint64_t live = 0ull;
+    for (uint32_t c = 0; c < m; ++c) live |= 1ull << rl(myid, c);
+    uint64_t killed = all & ~live, decided = 0ull;
+    uint32_t X = 0xFFFFFFFFu, K = 0xFFFFFFFFu, CI = 0u;
+    for (uint32_t c = 0; c < m; ++c) CI = lane == rl(myid, c) ? c : CI;
+    if ((live >> lane) & 1ull) {
+      int32_t v;
+      if (p.init_mode == BO_INIT_RANDOM) {        // oracle_random_init (m <= 32)
+        v = (int32_t)((init_word_small(k0, k1, trial) >> CI) & 1u);
+      } else {
+        v = p.init_x[lane];
+      }
+      X = (uint32_t)v;
+      K = 1u;                                      // /start: k = 1 (node.ts:172)
+    }
+    // ---- /start (node.ts:167-188): every live node broadcasts its x, in node order
+    const uint32_t XC = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(myid << 2), (int)X);   // x of compact node c
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint32_t pos = (uint32_t)r * 64u + lane, c = pos / N, n = pos - c * N;
+      const uint32_t xc = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(c << 2), (int)XC);
+      P[r] = c < m ? (2u * n) | (1u << 6) | inc_of(xc & 3u) : 0u;
+    }
+    // inbox slots; bit 7: the receiver is killed
+    uint32_t CNT = lane < 2u * N && !((live >> (lane >> 1)) & 1ull) ? 0x80u : 0u;
+    // round k complete at k & 3, in lane k & 3 (the SGPR file is full)
+    uint64_t CPV = 0ull;
+    auto comp_get = [&](uint32_t i) {
+      return ((uint64_t)rl((uint32_t)(CPV >> 32), i) << 32) | rl((uint32_t)CPV, i);
+    };
+    auto comp_set = [&](uint32_t i, uint64_t v) { CPV = lane == i ? v : CPV; };
+    uint64_t rngb;
+    {
+      const uint4 o = philox4x32_10<false>(k0, k1, make_uint4(tlo, thi, 0u, kStreamOrder << 24));
+      rngb = (((uint64_t)o.x << 32) | o.y) ^ 0xD1B54A32D192ED03ull;
+    }
+    uint32_t next = 0;
+    uint64_t next_key = uni64(p.ev_nstops ? p.ev_stops[0] : ~0ull);
+    uint32_t len = m * N, cur = 1u, Rr = 0u, halted = 0u, overflow = 0u;
+    uint64_t e = 0, trig = 0, cyc_steps = 0;
+    uint32_t H = 0u, hi = 64u;                     // the block's picks, the next one's lane
+    auto advance = [&]() {                         // node.ts:116-145 as DESIGN §2
+      for (;;) {
+        const uint64_t cw = comp_get(cur & 3u);
+        if ((cw | killed) != all) return;
+        if ((decided | killed) == all) { halted = 1u; Rr = cur; return; }
+        if (cur >= kmax) { halted = 2u; Rr = cur; return; }
+        comp_set(cur & 3u, 0ull);
+        ++cur;
+      }
+    };
+    auto kill = [&](uint32_t i) {                  // GET /stop (node.ts:191-194): drops every later message
+      killed |= 1ull << i;
+      CNT |= (lane >> 1) == i ? 0x80u : 0u;
+    };
+    auto pread = [&](uint32_t pos) { return rl(P[pos >> 6], pos & 63u); };
+    while (!halted) {
+      // ---- scheduled GET /stop before delivery e
+      bool crashed = false;
+      while ((next_key >> 12) == e) {
+        kill((uint32_t)(next_key & 4095u));
+        crashed = true;
+        ++next;
+        next_key = uni64(next < p.ev_nstops ? p.ev_stops[next] : ~0ull);
+      }
+      if (box && hi == 64u) {                      // the clock is read once per 64 events
+        if (wall_clock64() - polled >= kPollTicks) {
+          // live GET /stop requests (applied one poll after their sequence
+          // word) and GET /getState snapshot requests, as the wave kernel
           const uint64_t req = apply_next ? uni64(pv_req) : 0ull;
           const uint32_t seq = rl(pv_word, 1u), sreq = rl(pv_word, 2u);
           apply_next = seq != seq_seen;
           seq_seen = seq;
-          uint64_t fresh = req & all & ~killed;
+          const uint64_t fresh = req & all & ~killed;
           for (uint64_t f = fresh; f; f &= f - 1ull) {
             const uint32_t i = (uint32_t)__builtin_ctzll(f);
             kill(i);
             if (lane == 0u)
-              __hip_atomic_store(box + kLiveEv + i, e < 0xFFFFFFFFull ? (uint32_t)e : 0xFFFFFFFEu,
-                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              __hip_atomic_store(box + kLiveEv + i, e < 0xFFFFFFFFull ? (uint32_t)e : 0xFFFFFFFEu, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_SYSTEM);
           }
           crashed = crashed || fresh != 0ull;
           if (sreq != snap_served) {
@@ -870,66 +1236,130 @@ __global__ void __launch_bounds__(64) benor_event_serial_kernel(KParams p) {
         if (halted) break;
       }
       if (len == 0u) { halted = 3u; break; }
-      // ---- delivery e: uniform pick, swap-remove (oracle (iii))
-      const uint32_t qp = (uint32_t)(((uint64_t)rl(ZH, j) * (uint64_t)len) >> 32);
-      const uint32_t msg = uni(pool[qp]), tl = uni(pool[len - 1u]);
-      if (lane == 0u) pool[qp] = tl;
-      --len;
-      ++e;
-      ++j;
-      // ---- POST /message (node.ts:45-158)
-      const uint32_t to = msg & 4095u, ph = (msg >> 12) & 1u, xv = (msg >> 13) & 3u;
-      const uint32_t k = cur + (((msg >> 15) - cur) & 3u);
-      if (k >= kmax + 3u) continue;                // beyond the oracle's round window: dropped
-      uint32_t v = ph ? rl(IBP, to) : rl(IBR, to);
-      if (v & kSerialKill) continue;               // node.ts:45
-      v += (1u << 16) + (xv == 0u ? 1u : (xv == 1u ? 1u << 8 : 0u));
-      uint32_t body = 0xFFFFFFFFu;
-      if (((v >> 16) & 0xFFu) == quorum) {          // node.ts:52, :88: every message of the phase arrived
-        const uint32_t c0 = v & 0xFFu, c1 = (v >> 8) & 0xFFu;
-        v = 0u;                                    // the slot is free
-        if (ph == 0u) {                            // node.ts:53-80
-          const uint32_t pv = c0 > c1 ? 0u : (c1 > c0 ? 1u : 2u);
-          body = (1u << 12) | (pv << 13) | ((k & 3u) << 15);
-        } else {                                   // node.ts:89-157
-          uint32_t nx;
-          bool dec = true;
-          if (c0 > F) nx = 0u;
-          else if (c1 > F) nx = 1u;
-          else {
-            dec = false;
-            if (c0 + c1 > 0u && c0 > c1) nx = 0u;
-            else if (c0 + c1 > 0u && c0 < c1) nx = 1u;
-            else {
-              const uint32_t c = rl(CI, to);       // the coin of compact node c in round k (node.ts:111)
-              const uint4 rr = coin_block<false>(k0, k1, tlo, thi, c, k);
-              nx = uni((coin_word(rr, k) >> (c & 31u)) & 1u);
-            }
-          }
-          X = wl(X, nx, to);
-          K = wl(K, k + 1u, to);
-          if (dec) decided |= 1ull << to;
-          if (lane == 0u) comp[k & 3u] |= 1ull << to;
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-          advance();
-          if (!halted) body = (nx << 13) | (((k + 1u) & 3u) << 15);
-        }
+      if (hi == 64u) {                             // the next 64 picks (event e + i in lane i)
+        const uint64_t z = smix(rngb + (uint64_t)(lane + 1u) * kGm);
+        H = (uint32_t)(z >> 32);
+        rngb += 64ull * kGm;
+        hi = 0u;
       }
-      if (ph) IBP = wl(IBP, v, to);
-      else IBR = wl(IBR, v, to);
-      if (body != 0xFFFFFFFFu) {                   // the broadcast to all N nodes
-        if (len + N > p.ev_cap) {
+      // ---- POST /message (node.ts:45-158), one delivery per step up to the
+      // block's end, the next stop or the first trigger
+      uint32_t seg = 64u - hi;
+      if (seg > len) seg = len;
+      if (next_key != ~0ull && (next_key >> 12) - e < seg) seg = (uint32_t)((next_key >> 12) - e);
+      uint32_t j = 0u, tw = 0u, tc = 0u;
+      bool fired = false;
+      seg = uni(seg);
+      const uint32_t qmark = quorum << 24;
+      // one delivery: false when its slot reaches the quorum (the trigger)
+      auto deliver = [&](uint32_t w, auto late) {  // late: messages of round >= k_max + 3 are dropped
+        if (decltype(late)::value && cur + (((w >> 6) - cur) & 3u) >= kmax + 3u) return true;
+        const uint32_t s = w & 63u;
+        const uint32_t c = rl(CNT, s) + (w & 0xFFFFFF00u);
+        CNT = wl(CNT, c, s);
+        // killed receivers drop the message (node.ts:45): their slots count
+        // on (wrapping), never tested; a live slot reaches its quorum
+        if ((c & 0xFF000080u) != qmark) return true;
+        tw = w;
+        tc = c;
+        fired = true;
+        return false;
+      };
+      auto steps = [&](auto late) {
+        if (len <= 64u) {                          // the whole pool in lane p of one register
+          uint32_t P0 = P[0];
+          while (j < seg) {
+            j = uni(j);
+            len = uni(len);
+            const uint32_t q = uni((uint32_t)(((uint64_t)rl(H, hi + j) * len) >> 32));
+            const uint32_t w = rl(P0, q);
+            --len;
+            const uint32_t tv = rl(P0, len);
+            P0 = lane == q ? tv : P0;              // the tail word moves to q
+            ++j;
+            if (!deliver(w, late)) break;
+          }
+          P[0] = P0;
+          return;
+        }
+        while (j < seg) {
+          j = uni(j);
+          len = uni(len);
+          const uint32_t q = uni((uint32_t)(((uint64_t)rl(H, hi + j) * len) >> 32));
+          const uint32_t w = pread(q);
+          --len;
+          {                                        // the tail word moves to q (no-op when q is the tail)
+            const uint32_t tv = pread(len);
+            uint32_t reg = P[q >> 6];
+            reg = wl(reg, tv, q & 63u);
+            P[q >> 6] = reg;
+          }
+          ++j;
+          if (!deliver(w, late)) break;
+        }
+      };
+      const uint64_t c_a = stats ? __builtin_amdgcn_s_memtime() : 0ull;
+      if (cur >= kmax) steps(std::true_type{});
+      else steps(std::false_type{});
+      if (stats) cyc_steps += __builtin_amdgcn_s_memtime() - c_a;
+      e += j;
+      hi += j;
+      if (!fired) continue;
+      ++trig;
+      // ---- the trigger (node.ts:52-80 R-phase, :88-157 P-phase)
+      const uint32_t s = tw & 63u, to = s >> 1, ph = s & 1u;
+      const uint32_t k = cur + (((tw >> 6) - cur) & 3u);
+      CNT = wl(CNT, 0u, s);                        // every message of the phase arrived: the slot is free
+      const uint32_t c0 = (tc >> 8) & 0xFFu, c1 = (tc >> 16) & 0xFFu;
+      uint32_t base = 0xFFFFFFFFu;
+      if (ph == 0u) {
+        const uint32_t pr = c0 > c1 ? 0u : (c1 > c0 ? 1u : 2u);
+        base = 1u | ((k & 3u) << 6) | inc_of(pr);
+      } else {
+        uint32_t nx;
+        bool dec = true;
+        if (c0 > F) nx = 0u;
+        else if (c1 > F) nx = 1u;
+        else {
+          dec = false;
+          if (c0 + c1 > 0u && c0 > c1) nx = 0u;
+          else if (c0 + c1 > 0u && c0 < c1) nx = 1u;
+          else {
+            const uint32_t c = rl(CI, to);         // the coin of compact node c in round k (node.ts:111)
+            const uint4 rr = coin_block<false>(k0, k1, tlo, thi, c, k);
+            nx = uni((coin_word(rr, k) >> (c & 31u)) & 1u);
+          }
+        }
+        X = wl(X, nx, to);
+        K = wl(K, k + 1u, to);
+        if (dec) decided |= 1ull << to;
+        comp_set(k & 3u, comp_get(k & 3u) | (1ull << to));
+        advance();
+        if (!halted) base = ((((k + 1u) & 3u) << 6)) | inc_of(nx);
+      }
+      if (base != 0xFFFFFFFFu) {                   // the broadcast to all N nodes: positions len .. len + N - 1
+        if (len + N > cap) {
           overflow = 1u;
           halted = 3u;
           break;
         }
-        if (lane < N) pool[len + lane] = lane | body;
+        const uint32_t r0 = len >> 6, r1 = (len + N - 1u) >> 6;
+        if (r1 == 0u) {                            // within register 0
+          const uint32_t d = lane - len;
+          P[0] = d < N ? 2u * d + base : P[0];
+        } else {
+          const uint32_t d = r0 * 64u + lane - len;
+          uint32_t reg = P[r0];
+          reg = d < N ? 2u * d + base : reg;
+          P[r0] = reg;
+        }
+        if (r1 != r0) {
+          const uint32_t d = r1 * 64u + lane - len;
+          uint32_t reg = P[r1];
+          reg = d < N ? 2u * d + base : reg;
+          P[r1] = reg;
+        }
         len += N;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
       }
     }
     // ---- outcome over the nodes still running
@@ -938,14 +1368,16 @@ __global__ void __launch_bounds__(64) benor_event_serial_kernel(KParams p) {
     const bool gl = __any(run);
     const uint32_t vv = (!gl || gq || (g0 && g1)) ? 2u : (g1 ? 1u : 0u);
     if (lane == 0u) {
-      atomicAdd(&p.hist[halted == 1u ? (R * 3u + vv) : vv], 1ull);
+      atomicAdd(&p.hist[halted == 1u ? (Rr * 3u + vv) : vv], 1ull);
       if (halted == 1u && vv == 2u) atomicAdd(&p.hist[p.hist_len - 1u], 1ull);
       if (overflow && p.rounds_out) atomicOr(p.rounds_out, 0x80000000u);
       if (overflow && p.overflow) atomicOr(p.overflow, 2u);
-      if (p.node_out && p.rounds_out) atomicOr(p.rounds_out, halted == 1u ? R : 0u);
+      if (p.node_out && p.rounds_out) atomicOr(p.rounds_out, halted == 1u ? Rr : 0u);
       if (stats) {
+        atomicAdd(&stats[0], (unsigned long long)trig);
         atomicAdd(&stats[1], (unsigned long long)e);
-        atomicAdd(&stats[0], (unsigned long long)e);          // one event per step
+        atomicAdd(&stats[3], (unsigned long long)trig);
+        atomicAdd(&stats[6], (unsigned long long)cyc_steps);
         atomicAdd(&stats[12], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_start));
         atomicAdd(&stats[13], (unsigned long long)((uint64_t)wall_clock64() - w_start));
       }
@@ -960,9 +1392,6 @@ __global__ void __launch_bounds__(64) benor_event_serial_kernel(KParams p) {
       ns.k = (int32_t)K;
       p.node_out[lane] = ns;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   }
   if (box) __builtin_amdgcn_s_waitcnt(0x0F70);     // the last poll lands before the wave ends
 }
@@ -1008,24 +1437,39 @@ static hipError_t launch_wg(KParams p, int grid, hipStream_t s) {
   return hipGetLastError();
 }
 
-// Small networks run on the serial kernel, unless a random /stop schedule
+// Small networks run on a one-wave kernel, unless a random /stop schedule
 // (drawn by the workgroup kernel's control wave) or a forced wave count asks
 // for the workgroup kernel.
-bool event_serial(const KParams &p) {
-  return p.N <= kEventSerialMaxN && p.ev_rstops == 0u && knob_u32("BENOR_LIVE_WAVES", 0u) == 0u;
+static bool event_one_wave(const KParams &p) {
+  return p.ev_rstops == 0u && knob_u32("BENOR_LIVE_WAVES", 0u) == 0u;
 }
 
-uint32_t event_serial_lds_bytes(const KParams &p) { return 4u * ((p.ev_cap + 1u) & ~1u) + 4u * 8u; }
+uint32_t event_reg_regs(const KParams &p) {
+  if (p.N > kEventRegMaxN || !event_one_wave(p) || knob_is("BENOR_EVENT_FORM", "wave")) return 0u;
+  const uint32_t need = (p.ev_cap + 63u) / 64u;
+  return need <= 16u ? 16u : (need <= 32u ? 32u : 0u);
+}
+
+bool event_wave_form(const KParams &p) { return p.N <= kEventWaveMaxN && event_one_wave(p) && !event_reg_regs(p); }
+
+uint32_t event_wave_lds_bytes(const KParams &p) {
+  return 4u * ((p.ev_cap + 1u) & ~1u) + 4u * 64u + 8u * 256u + 8u * 128u + 8u * 4u;
+}
 
 hipError_t launch_event_wg(const KParams &p, int grid, hipStream_t s) {
-  if (event_serial(p)) {
-    const uint32_t lds = event_serial_lds_bytes(p);
+  if (const uint32_t regs = event_reg_regs(p)) {
+    if (regs == 16u) hipLaunchKernelGGL(benor_event_reg_kernel<16>, dim3(grid), dim3(64), 0, s, p);
+    else hipLaunchKernelGGL(benor_event_reg_kernel<32>, dim3(grid), dim3(64), 0, s, p);
+    return hipGetLastError();
+  }
+  if (event_wave_form(p)) {
+    const uint32_t lds = event_wave_lds_bytes(p);
     if (lds > 64u * 1024u) {
-      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&benor_event_serial_kernel),
+      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&benor_event_wave_kernel),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(benor_event_serial_kernel, dim3(grid), dim3(64), lds, s, p);
+    hipLaunchKernelGGL(benor_event_wave_kernel, dim3(grid), dim3(64), lds, s, p);
     return hipGetLastError();
   }
   const uint32_t W = event_wg_waves(p);

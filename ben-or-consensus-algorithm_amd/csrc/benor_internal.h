@@ -174,12 +174,16 @@ hipError_t launch_event_big(const KParams &p, int grid_blocks, hipStream_t strea
 // workgroup of a control wave and 1, 3, 7 or 15 event waves; live runs (mailbox
 // /stop, /getState snapshots) and single-trial network runs.
 uint32_t event_wg_waves(const KParams &p);
-// ... and for N <= kEventSerialMaxN (no random /stop schedule, no forced wave
-// count) the serial one-wave form of it: the pool in LDS, inboxes and node
-// state in lane registers, one event per step.
-constexpr uint32_t kEventSerialMaxN = 64;
-bool event_serial(const KParams &p);
-uint32_t event_serial_lds_bytes(const KParams &p);
+// ... and, with no random /stop schedule and no forced wave count, its
+// one-wave forms: for N <= kEventRegMaxN the pool, inboxes and node state in
+// registers, one event per step (event_reg_regs: pool VGPRs, 0 = not this
+// form); for N <= kEventWaveMaxN micro-batches of up to 64 events, the pool
+// in LDS (BENOR_EVENT_FORM=wave: this form below kEventRegMaxN too).
+constexpr uint32_t kEventRegMaxN = 16;            // the LDS micro-batch form is faster from N ~ 20
+constexpr uint32_t kEventWaveMaxN = 64;
+uint32_t event_reg_regs(const KParams &p);
+bool event_wave_form(const KParams &p);
+uint32_t event_wave_lds_bytes(const KParams &p);
 bool event_wg_lds_pool(const KParams &p);
 uint32_t event_wg_lds_bytes(const KParams &p, uint32_t waves);
 hipError_t launch_event_wg(const KParams &p, int grid_blocks, hipStream_t stream);

@@ -591,8 +591,9 @@ void plan_geometry(KParams &p) {
   p.hist_len = (p.k_max + 1u) * 3u + 1u;
   p.hist_bytes = (((p.hist_len * 4u) + 15u) & ~15u) + kParamBytes;   // histogram + parameter block
   // one wave per trial (benor_event_big.hip), or one workgroup per trial
-  // (benor_event_live.hip: live runs; batch plans under BENOR_EVENT_FORM=wg)
-  const bool wg = p.mode == BO_MODE_EVENT && (p.live || knob_is("BENOR_EVENT_FORM", "wg"));
+  // (benor_event_live.hip: live runs; batch plans under BENOR_EVENT_FORM=wg or wave)
+  const bool wg = p.mode == BO_MODE_EVENT &&
+                  (p.live || knob_is("BENOR_EVENT_FORM", "wg") || knob_is("BENOR_EVENT_FORM", "wave"));
   if (p.mode == BO_MODE_EVENT && (p.N > kMaxEventN || wg)) {
     p.G = 1;
     p.nblocks = 1;

@@ -9,7 +9,9 @@ pick conflict and at its first quorum (node.ts:52, :88).  Checked here:
 * histograms of many trials against the oracle (BENOR_EVENT_FORM=wg routes
   batch event plans to it), with no stop, explicit and random /stop
   schedules, at N from 1 to 1024, every wave count, both pool forms (LDS for
-  N <= 78, HBM above);
+  N <= 78, HBM above), and its one-wave forms (the register kernel at
+  N <= 16, the LDS micro-batch kernel at N <= 64; BENOR_EVENT_FORM=wave
+  puts the small N on the latter);
 * live runs' GET /getState snapshots (bo_get_states): each equals oracle (iii)
   truncated at the delivery count the snapshot reports, with the killed flag
   of every /stop already posted (node.ts:191-194);
@@ -31,8 +33,8 @@ def first_f(N, F):
 
 
 def wg_hist(monkeypatch, N, F, *, waves=None, seed, trials, k_max=16, init=None, crash_at=None, crash_count=0,
-            crash_window=0):
-    monkeypatch.setenv("BENOR_EVENT_FORM", "wg")
+            crash_window=0, form="wg"):
+    monkeypatch.setenv("BENOR_EVENT_FORM", form)
     if waves:
         monkeypatch.setenv("BENOR_LIVE_WAVES", str(waves))
     plan = benor.TrialsPlan(N, F, first_f(N, F), seed=seed, k_max=k_max, initial_values=init,
@@ -97,6 +99,21 @@ def test_random_stop_schedules(monkeypatch, N, F, count, window, trials):
     got = wg_hist(monkeypatch, N, F, seed=seed, trials=trials, crash_count=count, crash_window=window)
     np.testing.assert_array_equal(got, ref_hist(N, F, seed=seed, trials=trials, crash_count=count,
                                                 crash_window=window))
+
+
+@pytest.mark.parametrize("N,F,stops", [
+    (1, 0, {}), (3, 1, {}), (10, 4, {4: 0, 7: 13}), (10, 5, {}), (16, 5, {3: 200}), (15, 7, {}), (16, 8, {0: 50}),
+])
+def test_wave_form_below_the_register_form(monkeypatch, N, F, stops):
+    """N <= 16 runs on the register kernel (the pool in VGPRs, one event per
+    step); BENOR_EVENT_FORM=wave runs the same plans on the LDS micro-batch
+    kernel that N = 23 .. 64 use.  Both against the oracle."""
+    crash = [stops.get(i) for i in range(N)] if stops else None
+    seed, trials = 0x3B + N, 120
+    want = ref_hist(N, F, seed=seed, trials=trials, crash_at=crash)
+    for form in ("wg", "wave"):
+        got = wg_hist(monkeypatch, N, F, seed=seed, trials=trials, crash_at=crash, form=form)
+        np.testing.assert_array_equal(got, want, err_msg=form)
 
 
 def test_fixed_ties_and_question_marks(monkeypatch):

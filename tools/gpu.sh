@@ -30,6 +30,7 @@
 #   c5trace         the same under rocprofv3 --kernel-trace --stats
 #   matrix          tools/perf_matrix.py over its built-in shape list
 #   liveprof        tools/live_profile.py (LIVEPROF_ARGS): a live run's batch counters and cycle split
+#   livepmc         PMC passes (PMC_GROUPS) over tools/live_profile.py (LIVEPROF_ARGS)
 #   netlat          tools/net_latency.py (NETLAT_ARGS): the reference's launch + start + final states
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R" || exit 1
@@ -86,6 +87,15 @@ for step in "$@"; do
         (cd /tmp && timeout -s KILL 90 rocprofv3 --pmc $grp --output-format csv -d "$OUT/pmc_$tag/p$i" -o pmc -- \
           python3 "$R/tools/perf_matrix.py" --shapes "$shape" > "$OUT/pmc_$tag/p$i.log" 2>&1)
         chk $? "pmc $key pass $i ($grp)"
+      done;;
+    livepmc)
+      i=0; mkdir -p "$OUT/livepmc"
+      IFS='|' read -r -a GRPS <<< "$PMC_GROUPS"
+      for grp in "${GRPS[@]}"; do
+        i=$((i+1))
+        (cd /tmp && timeout -s KILL 90 rocprofv3 --pmc $grp --output-format csv -d "$OUT/livepmc/p$i" -o pmc -- \
+          python3 "$R/tools/live_profile.py" $LIVEPROF_ARGS > "$OUT/livepmc/p$i.log" 2>&1)
+        chk $? "livepmc pass $i ($grp)"
       done;;
     ab)
       for rep in 1 2; do
