@@ -19,6 +19,7 @@ from __future__ import annotations
 import ctypes
 import os
 import secrets
+import struct
 from typing import Sequence
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -117,8 +118,9 @@ def lib() -> ctypes.CDLL:
         raise RuntimeError(f"libbenor.so not built at {LIB_PATH}: run __graft_entry__.build()")
     L = ctypes.CDLL(LIB_PATH)
     P = ctypes.POINTER
-    L.bo_network_create.argtypes = [ctypes.c_uint32, ctypes.c_uint32, P(ctypes.c_int8), ctypes.c_uint32,
-                                    P(ctypes.c_uint8), ctypes.c_uint32, P(ctypes.c_void_p)]
+    # int8 initial values and uint8 faulty flags, passed as bytes
+    L.bo_network_create.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32,
+                                    ctypes.c_char_p, ctypes.c_uint32, P(ctypes.c_void_p)]
     L.bo_consensus_start.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32]
     L.bo_consensus_start_sched.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, P(ctypes.c_uint32),
                                            ctypes.c_uint32]
@@ -189,14 +191,34 @@ def _state_dict(s: NodeStateC) -> dict:
             "k": None if s.k < 0 else int(s.k)}
 
 
+_REC = struct.Struct("bbbbi")                     # bo_node_state
+
+
+def _state_dicts(arr, n: int) -> list[dict]:
+    """n NodeState dicts from a bo_node_state array: a network's states repeat
+    (a few distinct records at any N), so each distinct 8-byte record is
+    decoded once and copied."""
+    raw = memoryview(arr).cast("B").cast("Q")[:n]
+    tab = {}
+    for v in set(raw):
+        kl, x, dec, _, k = _REC.unpack(v.to_bytes(8, "little"))
+        tab[v] = {"killed": kl != 0, "x": _UNVAL[x], "decided": None if dec < 0 else dec != 0,
+                  "k": None if k < 0 else k}
+    return [tab[v].copy() for v in raw]
+
+
 class Node:
     """Stands in for one of the `http.Server` objects launchNetwork returns:
     the caller may close() it (benorconsensus.test.ts:14-29); the node's
     routes are getState() / status()."""
+    __slots__ = ("_net", "node_id")
 
     def __init__(self, net: "Network", node_id: int):
         self._net, self.node_id = net, node_id
-        self.port = BASE_NODE_PORT + node_id
+
+    @property
+    def port(self) -> int:
+        return BASE_NODE_PORT + self.node_id
 
     def close(self, cb=None):
         if cb is not None:
@@ -218,8 +240,8 @@ class Network:
     def __init__(self, N: int, F: int, initialValues: Sequence, faultyList: Sequence[bool]):
         L = lib()
         n_init, n_f = len(initialValues), len(faultyList)
-        init = (ctypes.c_int8 * max(1, n_init))(*[_VAL.get(v, -2) for v in initialValues])
-        fl = (ctypes.c_uint8 * max(1, n_f))(*[1 if v is True else 0 for v in faultyList])
+        init = bytes(_VAL.get(v, -2) & 0xFF for v in initialValues) or b"\0"     # int8 values
+        fl = bytes(v is True for v in faultyList) or b"\0"
         h = ctypes.c_void_p()
         _check(L.bo_network_create(N, F, init, n_init, fl, n_f, ctypes.byref(h)))
         self._h = h
@@ -297,7 +319,7 @@ class Network:
         st = (NodeStateC * max(1, self.N))()
         ev = ctypes.c_uint64(0)
         _check(lib().bo_get_states(self._h, st, self.N, ctypes.byref(ev)))
-        return [_state_dict(st[i]) for i in range(self.N)], (None if ev.value == 2 ** 64 - 1 else int(ev.value))
+        return _state_dicts(st, self.N), (None if ev.value == 2 ** 64 - 1 else int(ev.value))
 
     def get_states(self) -> list[dict]:
         return self.get_states_at()[0]

@@ -35,7 +35,7 @@
 //   * the control wave issues no pool access: it owns the round state in LDS,
 //     applies scheduled /stop (delivery counts) and live /stop requests, and
 //     polls the host-mapped mailbox with an uncached load that it consumes
-//     ~5 us later (so the PCIe round trip is never waited for), and serves
+//     ~20 us later (so the PCIe round trip is never waited for), and serves
 //     GET /getState snapshots: on request, the event waves write every node's
 //     {killed, x, decided, k} at a batch boundary to host memory with the
 //     delivery count it reflects, so a snapshot is oracle (iii) truncated at
@@ -88,6 +88,16 @@ struct Ctl {
   uint32_t ncross[2];  // inbox slots that reached their quorum in the batch
   uint32_t trig[2];    // the batch's first trigger event (~0: none)
 };
+
+// The mailbox poll's clock: shader cycles.  A poll is consumed >= 20 us
+// after it was issued (its PCIe round trip is long done, so no wait): 48000
+// cycles at 2.4 GHz, a slower clock only spaces the polls further.  Each
+// consumed poll costs the batch loop ~500 cycles: at 5 us it was ~7 % of a live
+// run at N = 1024 (10.6 against 9.85 ms with polls 1 ms apart,
+// tools/live_profile.py); a GET /stop or /getState waits at most ~20 us more
+// for the kernel, against the reference's HTTP round trip per request.
+constexpr long long kPollCycles = 48000;
+__device__ __forceinline__ long long poll_clock() { return (long long)__builtin_amdgcn_s_memtime(); }
 
 __device__ __forceinline__ uint32_t hslot(uint32_t key, uint32_t mask) { return (key * 0x9E3779B1u >> 11) & mask; }
 
@@ -185,11 +195,10 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
 
   // the control wave's mailbox poll: lane l < NWd reads request bits 64l ..
   // 64l + 63, lane 0 also the request sequence word and lane 1 the snapshot
-  // request; issued at `polled`, consumed >= kPollTicks later.  The host sets a
+  // request; issued at `polled`, consumed >= kPollCycles later.  The host sets a
   // burst's bits (stopConsensus: every node) and then bumps the sequence word,
   // so the bits of the poll AFTER the one that saw the new sequence hold the
   // whole burst, which then lands at one delivery count.
-  constexpr long long kPollTicks = 500;            // 5 us of the 100 MHz wall clock
   uint64_t pv_req = 0ull;
   uint32_t pv_word = 0u, snap_served = 0u, seq_seen = 0u;
   bool apply_next = false;
@@ -201,7 +210,7 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
                                  __HIP_MEMORY_SCOPE_SYSTEM);
     if (lane == 0u) pv_word = __hip_atomic_load(box, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (lane == 1u) pv_word = __hip_atomic_load(box + kSnapReq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    polled = wall_clock64();
+    polled = poll_clock();
     poll_out = true;
   };
   if (ctl && box) poll_issue();
@@ -304,7 +313,7 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
       // diagnostics (BENOR_EVENT_STATS): batch counters and the shader cycles
       // between the control wave's barriers, accumulated per trial
       unsigned long long *const stats = p.ev_stats;
-      uint64_t st[16] = {};
+      uint64_t st[24] = {};
       uint64_t t_prev = stats ? __builtin_amdgcn_s_memtime() : 0ull;
       const uint64_t t_start = t_prev, w_start = stats ? (uint64_t)wall_clock64() : 0ull;
       auto stamp = [&](int slot) {
@@ -344,11 +353,11 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
           }
         }
         uint32_t snap = 0u;
-        if (box && poll_out && wall_clock64() - polled >= kPollTicks) {
+        if (box && poll_out && poll_clock() - polled >= kPollCycles) {
           // live GET /stop requests and /getState snapshot requests: the poll
-          // issued >= 5 us ago (its PCIe round trip is long done)
+          // issued >= 20 us ago (its PCIe round trip is long done)
           const uint64_t req = apply_next ? pv_req : 0ull;   // a burst is complete one poll after its sequence
-          const uint32_t seq = __shfl(pv_word, 0), sreq = __shfl(pv_word, 1);
+          const uint32_t seq = uni(__shfl(pv_word, 0)), sreq = uni(__shfl(pv_word, 1));   // uniform: keeps the loop scalar
           apply_next = seq != seq_seen;
           seq_seen = seq;
           uint64_t fresh = 0ull;
@@ -410,6 +419,22 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
       }
       uint32_t snap = 0u;
       for (;;) {
+        // the loop-carried round state is wave-uniform; said so, the loop stays
+        // scalar code (the compiler cannot prove it through the LDS reads)
+        e = uni64(e);
+        rng = uni64(rng);
+        next_key = uni64(next_key);
+        len = uni(len);
+        cur = uni(cur);
+        halted = uni(halted);
+        body = uni(body);
+        par = uni(par);
+        next = uni(next);
+        polled = (long long)uni64((uint64_t)polled);
+        seq_seen = uni(seq_seen);
+        snap_served = uni(snap_served);
+        apply_next = uni(apply_next ? 1u : 0u) != 0u;
+        poll_out = uni(poll_out ? 1u : 0u) != 0u;
         stamp(5);
         __syncthreads();                           // ---- H: the batch is published
         snap = uni(C.snap);
@@ -488,6 +513,7 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
             overflow = 1u;
           }
         }
+        stamp(21);
         const uint32_t bpos = len - used;
         len = bpos + (body != 0xFFFFFFFFu ? N : 0u);
         e += used;
@@ -499,6 +525,7 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
           nB = bs.first;
           nsnap = bs.second;
         }
+        stamp(22);
         publish(nB, nsnap, bpos);
         stamp(10);
       }
@@ -510,15 +537,18 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
         st[12] = __builtin_amdgcn_s_memtime() - t_start;
         st[13] = (uint64_t)wall_clock64() - w_start;
         for (int i = 0; i < 16; ++i) atomicAdd(&stats[i], (unsigned long long)st[i]);
+        atomicAdd(&stats[21], (unsigned long long)st[21]);
+        atomicAdd(&stats[22], (unsigned long long)st[22]);
       }
     } else {
       uint32_t par = 0u;
       // diagnostics (BENOR_EVENT_STATS): the first event wave's phase 1 split
       // into its own work and the wait for its pool words, and its phase 4
       unsigned long long *const stats = tid == 64u ? p.ev_stats : nullptr;
-      uint64_t s_work = 0ull, s_wait = 0ull, s_write = 0ull;
+      uint64_t s_work = 0ull, s_wait = 0ull, s_write = 0ull, s_pre = 0ull, s_drain = 0ull;
       for (;;) {
         __syncthreads();                           // ---- H
+        const uint64_t t0 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
         // the last trigger's broadcast (node.ts:72-80, :149-157) goes to [bpos,
         // len): stored now, drained with this batch's loads; this batch itself
         // reads that region's words as they are, d | body for position bpos + d
@@ -549,6 +579,7 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
         uint32_t qi = 0u, ti = 0u, pv = 0u, tv = 0u, hs = 0u;
         const bool act = ei < B;
         const uint64_t t1 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
+        if (stats) s_pre += t1 - t0;
         if (act) {
           const uint64_t z = smix(rng + (uint64_t)(ei + 1u) * kGm);
           qi = (uint32_t)(((uint64_t)(uint32_t)(z >> 32) * (uint64_t)(len - ei)) >> 32);
@@ -583,7 +614,9 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
           }
           tvs[ei] = tv;
         }
+        const uint64_t t3 = stats ? __builtin_amdgcn_s_memtime() : 0ull;
         vm_drain();                                // the broadcast's stores too, before any phase-4 store
+        if (stats) s_drain += __builtin_amdgcn_s_memtime() - t3;
         __syncthreads();                           // ---- B
         // ================= 2. resolution, one level deep
         uint32_t msg = pv, moved = tv;
@@ -669,6 +702,8 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
         atomicAdd(&stats[16], (unsigned long long)s_work);
         atomicAdd(&stats[17], (unsigned long long)s_wait);
         atomicAdd(&stats[18], (unsigned long long)s_write);
+        atomicAdd(&stats[19], (unsigned long long)s_pre);
+        atomicAdd(&stats[20], (unsigned long long)s_drain);
       }
     }
     // ---- outcome over the nodes still running
@@ -745,9 +780,8 @@ __global__ void __launch_bounds__(64) benor_event_wave_kernel(KParams p) {
   const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
   uint32_t *box = p.live_box;
   unsigned long long *const stats = p.ev_stats;
-  // the mailbox poll, issued and consumed >= kPollTicks apart (as the
+  // the mailbox poll, issued and consumed >= kPollCycles apart (as the
   // workgroup kernel's control wave): the wave waits for no PCIe round trip
-  constexpr long long kPollTicks = 500;
   uint64_t pv_req = 0ull;
   uint32_t pv_word = 0u, snap_served = 0u, seq_seen = 0u;
   bool apply_next = false;
@@ -757,7 +791,7 @@ __global__ void __launch_bounds__(64) benor_event_wave_kernel(KParams p) {
                                                __HIP_MEMORY_SCOPE_SYSTEM);
     if (lane == 1u) pv_word = __hip_atomic_load(box, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (lane == 2u) pv_word = __hip_atomic_load(box + kSnapReq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    polled = wall_clock64();
+    polled = poll_clock();
   };
   if (box) poll_issue();
   auto rl = [](uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); };
@@ -838,7 +872,7 @@ __global__ void __launch_bounds__(64) benor_event_wave_kernel(KParams p) {
         ++next;
         next_key = uni64(next < p.ev_nstops ? p.ev_stops[next] : ~0ull);
       }
-      if (box && wall_clock64() - polled >= kPollTicks) {
+      if (box && poll_clock() - polled >= kPollCycles) {
         // live GET /stop requests (applied one poll after their sequence word,
         // so a burst lands together) and GET /getState snapshot requests
         const uint64_t req = apply_next ? uni64(pv_req) : 0ull;
@@ -1102,7 +1136,6 @@ __global__ void __launch_bounds__(64) benor_event_reg_kernel(KParams p) {
   const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
   uint32_t *box = p.live_box;
   unsigned long long *const stats = p.ev_stats;
-  constexpr long long kPollTicks = 500;                              // as the wave kernel
   uint64_t pv_req = 0ull;
   uint32_t pv_word = 0u, snap_served = 0u, seq_seen = 0u;
   bool apply_next = false;
@@ -1112,7 +1145,7 @@ __global__ void __launch_bounds__(64) benor_event_reg_kernel(KParams p) {
                                                __HIP_MEMORY_SCOPE_SYSTEM);
     if (lane == 1u) pv_word = __hip_atomic_load(box, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (lane == 2u) pv_word = __hip_atomic_load(box + kSnapReq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    polled = wall_clock64();
+    polled = poll_clock();
   };
   if (box) poll_issue();
   auto rl = [](uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); };
@@ -1194,7 +1227,7 @@ __global__ void __launch_bounds__(64) benor_event_reg_kernel(KParams p) {
         next_key = uni64(next < p.ev_nstops ? p.ev_stops[next] : ~0ull);
       }
       if (box && hi == 64u) {                      // the clock is read once per 64 events
-        if (wall_clock64() - polled >= kPollTicks) {
+        if (poll_clock() - polled >= kPollCycles) {
           // live GET /stop requests (applied one poll after their sequence
           // word) and GET /getState snapshot requests, as the wave kernel
           const uint64_t req = apply_next ? uni64(pv_req) : 0ull;

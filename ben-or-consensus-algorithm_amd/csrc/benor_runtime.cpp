@@ -1140,12 +1140,13 @@ int wg_read(LiveSlot *sl, const WgRun &run, uint32_t N, std::vector<bo_node_stat
     if (hipMemcpyAsync(s, sl->d + run.o_stats, sizeof s, hipMemcpyDeviceToHost, sl->s) == hipSuccess &&
         hipStreamSynchronize(sl->s) == hipSuccess)
       if (FILE *f = std::fopen(path, "a")) {
-        static const char *names[19] = {"batches", "events", "batch_slots", "trigger_batches", "conflict_cut",
+        static const char *names[23] = {"batches", "events", "batch_slots", "trigger_batches", "conflict_cut",
                                         "cyc_top", "cyc_picks", "cyc_lookup", "cyc_deliver", "cyc_cross",
                                         "cyc_writes_trigger", "cyc_bcast", "cycles", "wall_ticks", "cross_batches",
-                                        "snapshots", "ev_work", "ev_wait", "ev_write"};
+                                        "snapshots", "ev_work", "ev_wait", "ev_write", "ev_pre", "ev_drain",
+                                        "cyc_trigger", "cyc_prepare"};
         std::fprintf(f, "{\"N\": %u, \"F\": %u", run.N, run.F);
-        for (int i = 0; i < 19; ++i) std::fprintf(f, ", \"%s\": %llu", names[i], s[i]);
+        for (int i = 0; i < 23; ++i) std::fprintf(f, ", \"%s\": %llu", names[i], s[i]);
         std::fprintf(f, "}\n");
         std::fclose(f);
       }

@@ -126,7 +126,7 @@ int bo_consensus_start_sched(bo_network *net, uint64_t seed, uint32_t k_max,
  * N <= BO_MAX_N; one workgroup of 1-15 event waves and a control wave) on its
  * own HIP stream and returns.  While it runs:
  *   - bo_node_stop / bo_consensus_stop also post to a host-mapped mailbox the
- *     kernel polls (every ~5 us): a request is applied before the next
+ *     kernel polls (every ~20 us): a request is applied before the next
  *     delivery, and that delivery count is recorded (bo_live_stop_events);
  *   - bo_get_state / bo_get_states answer at once from a snapshot the kernel
  *     writes at its next batch boundary (tens of microseconds): every node's

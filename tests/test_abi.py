@@ -80,6 +80,21 @@ def test_initial_state_before_start():
     assert not benor.reachedFinality(st)
 
 
+def test_state_records_decode_as_single_reads():
+    """getNodesState decodes each distinct bo_node_state record once
+    (benor._state_dicts); every dict equals the per-record decoding and is a
+    separate object."""
+    recs = [(0, 1, 1, 0, 3), (1, -1, -1, 0, -1), (0, 2, 0, 0, 7), (1, 0, 1, 0, 12), (0, 1, 1, 0, 3)]
+    arr = (benor.NodeStateC * len(recs))()
+    for r, (kl, x, d, pad, k) in zip(arr, recs):
+        r.killed, r.x, r.decided, r.pad, r.k = kl, x, d, pad, k
+    got = benor._state_dicts(arr, len(recs))
+    assert got == [benor._state_dict(arr[i]) for i in range(len(recs))]
+    assert got[0] is not got[4]
+    got[0]["k"] = 99
+    assert got[4]["k"] == 3
+
+
 def test_reference_accepts_what_it_accepts():
     # F > N/2, '?' initial values, F == N are all accepted (launchNodes.ts:10-13
     # is the only validation; start.ts:25-29 rejects F > N/2 only in the demo).

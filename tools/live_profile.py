@@ -74,7 +74,7 @@ def main():
                        "cross_batches": s["cross_batches"], "cycles_per_batch": s["cycles"] / b,
                        "ns_per_event": s["wall_ticks"] * 10.0 / max(1, s["events"]),
                        "split_cycles_per_batch": {k[4:]: round(s[k] / b, 1) for k in s if k.startswith("cyc_")},
-                       "event_wave_per_batch": {k[3:]: round(s.get(k, 0) / b, 1) for k in ("ev_work", "ev_wait", "ev_write")}}
+                       "event_wave_per_batch": {k[3:]: round(s.get(k, 0) / b, 1) for k in ("ev_pre", "ev_work", "ev_wait", "ev_drain", "ev_write")}}
                 print(json.dumps(out), flush=True)
     os.environ.pop("BENOR_EVENT_STATS", None)
     os.unlink(path)

@@ -5,7 +5,10 @@ Prints one JSON line per (N, start) with the median and p90 wall time in ms:
 the default start (resolves at launch; waitConsensus, then getNodesState's
 final states) and the sync one.
 
-    python tools/net_latency.py [--reps 200] [--max-n 1024]
+    python tools/net_latency.py [--reps 200] [--max-n 1024] [--min-n 1]
+
+Each line also carries the median of each call (launchNetwork, startConsensus,
+waitConsensus, getNodesState).
 """
 import argparse
 import json
@@ -21,30 +24,37 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=200)
     ap.add_argument("--max-n", type=int, default=1024)
+    ap.add_argument("--min-n", type=int, default=1)
     a = ap.parse_args()
     import benor
 
     for N, F in [(5, 1), (10, 4), (10, 5), (100, 33), (1024, 341), (1024, 512)]:
-        if N > a.max_n:
+        if N > a.max_n or N < a.min_n:
             continue
         faulty = [i < F for i in range(N)]
         init = [(i * 7 + 3) % 2 for i in range(N)]
         for start, kw in (("default", {}), ("sync", {"sync": True})):
-            times = []
+            times, phases = [], []
             reps = a.reps if N < 1024 or start == "sync" else max(5, a.reps // (20 if F < 512 else 60))
             for rep in range(reps + 5):
                 t0 = time.perf_counter()
                 benor.launchNetwork(N, F, init, faulty)
+                t1 = time.perf_counter()
                 benor.startConsensus(N, seed=rep, **kw)
+                t2 = time.perf_counter()
                 benor.waitConsensus(N)
+                t3 = time.perf_counter()
                 states = benor.getNodesState(N)
-                dt = time.perf_counter() - t0
+                t4 = time.perf_counter()
                 if rep >= 5:
-                    times.append(dt * 1e3)
+                    times.append((t4 - t0) * 1e3)
+                    phases.append(((t1 - t0) * 1e3, (t2 - t1) * 1e3, (t3 - t2) * 1e3, (t4 - t3) * 1e3))
             times.sort()
+            med = [sorted(p[i] for p in phases)[len(phases) // 2] for i in range(4)]
             decided = sum(1 for s in states if s["decided"])
             print(json.dumps({"N": N, "F": F, "start": start, "reps": reps, "median_ms": times[len(times) // 2],
-                              "p90_ms": times[int(len(times) * 0.9)], "last_decided_nodes": decided}), flush=True)
+                              "p90_ms": times[int(len(times) * 0.9)], "last_decided_nodes": decided,
+                              "phase_median_ms": dict(zip(("launch", "start", "wait", "states"), med))}), flush=True)
 
 
 if __name__ == "__main__":
