@@ -74,6 +74,7 @@ constexpr uint32_t pow2_ceil(uint32_t v) { uint32_t r = 1u; while (r < v) r <<= 
 // batch n's).
 struct Ctl {
   uint64_t rng;        // splitmix64 state at the batch's first delivery
+  uint64_t tbox;       // the first trigger's inbox slot {c0, c1, len} (its slot is then cleared)
   uint32_t len;        // pending messages
   uint32_t B;          // the batch's events
   uint32_t cur;        // completion round (decodes a message's k & 3)
@@ -466,17 +467,17 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
           st[4] += used0 < B ? 1u : 0u;
           st[15] += snap ? 1u : 0u;
         }
-        const uint32_t tr = uni(C.trig[par]);
+        // read together: the trigger's message and slot (written by its event lane)
+        const uint32_t tr = uni(C.trig[par]), tmsg_w = C.tmsg;
+        const uint64_t tbox_w = C.tbox;
         body = 0xFFFFFFFFu;
         if (tr != 0xFFFFFFFFu) {
           // ---- the trigger (node.ts:52-80 R-phase, :88-157 P-phase)
           st[3] += 1u;
-          const uint32_t tmsg = uni(C.tmsg);
+          const uint32_t tmsg = uni(tmsg_w);
           const uint32_t to = tmsg & 4095u, ph = (tmsg >> 12) & 1u;
           const uint32_t k = cur + (((tmsg >> 15) - cur) & 3u);
-          const uint64_t tbox = uni64(ibox[2u * to + ph]);
-          __builtin_amdgcn_wave_barrier();
-          if (lane == 0u) ibox[2u * to + ph] = 0ull;   // every message of the phase arrived: the slot is free
+          const uint64_t tbox = uni64(tbox_w);
           const uint32_t c0 = (uint32_t)(tbox & kF13), c1 = (uint32_t)((tbox >> 13) & kF13);
           if (ph == 0u) {
             const uint32_t v = c0 > c1 ? 0u : (c1 > c0 ? 1u : 2u);
@@ -514,6 +515,9 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
           }
         }
         stamp(21);
+        body = uni(body);                          // uniform (see the loop head)
+        halted = uni(halted);
+        cur = uni(cur);
         const uint32_t bpos = len - used;
         len = bpos + (body != 0xFFFFFFFFu ? N : 0u);
         e += used;
@@ -680,7 +684,14 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
           if (inc && ei > tr)
             __hip_atomic_fetch_add(reinterpret_cast<unsigned long long *>(&ibox[slot]), 0ull - inc,
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          if (act && ei == tr) C.tmsg = msg;
+          if (act && ei == tr) {
+            // the trigger's slot is final (no later batch event goes there):
+            // its counts to the control wave, and every message of the phase
+            // arrived, so the slot is free
+            C.tmsg = msg;
+            C.tbox = ibox[slot];
+            ibox[slot] = 0ull;
+          }
           used = tr + 1u;
           __syncthreads();                         // ---- G
         }
@@ -1451,8 +1462,11 @@ static uint32_t wg_lds_bytes(const KParams &p, uint32_t W, uint32_t HS) {
 }
 
 uint32_t event_wg_hash_slots(const KParams &p, uint32_t W) {
-  const uint32_t big = pow2_ceil(4u * 64u * W), small = pow2_ceil(2u * 64u * W);
-  return wg_lds_bytes(p, W, big) <= 150u * 1024u ? big : small;
+  for (uint32_t f = 8u; f > 2u; f >>= 1) {
+    const uint32_t hs = pow2_ceil(f * 64u * W);
+    if (wg_lds_bytes(p, W, hs) <= 150u * 1024u) return hs;
+  }
+  return pow2_ceil(2u * 64u * W);
 }
 
 uint32_t event_wg_lds_bytes(const KParams &p, uint32_t W) { return wg_lds_bytes(p, W, event_wg_hash_slots(p, W)); }
