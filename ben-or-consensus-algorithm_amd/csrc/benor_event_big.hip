@@ -38,13 +38,9 @@
 //     delivery at a time up to that trigger).  A trigger ends the batch: the
 //     used events' writes go back, the triggered broadcast is appended, and
 //     the next batch starts after it.  Batches also end before a scheduled stop.
-//   * a live run (bo_consensus_start_live, any N) reads a host-mapped mailbox
-//     for GET /stop requests served while the run goes on: with the pool in
-//     LDS a second wave polls it (one PCIe round trip every ~2 us) and mirrors
-//     it in LDS for wave 0, else wave 0 reads it between batches every ~10 us
-//     of wall clock.  A request is applied before the next
-//     delivery e, exactly like a scheduled stop at e, and e is written back so
-//     the host can replay the run as a schedule (bo_live_stop_events).
+//   * r04-r05 live runs also ran here (a host-mapped mailbox polled between
+//     batches); since r06 they run on csrc/benor_event_live.hip, and this
+//     kernel serves batch event plans (many trials) only.
 #include "benor_device.h"
 
 namespace benor {
@@ -83,9 +79,8 @@ __device__ __forceinline__ uint32_t below_mask(uint32_t a, uint32_t b) {
   return r;
 }
 
-// Wave 0's LDS ordering point: a live run's workgroup also holds the polling
-// wave, which never joins a barrier, so wave 0 orders its LDS traffic with a
-// fence and a wave barrier instead of __syncthreads.
+// The wave's LDS ordering point (one wave per workgroup: a fence and a wave
+// barrier).
 __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_wave_barrier();
@@ -109,46 +104,17 @@ struct BigState {
 }  // namespace
 
 template <bool LP>
-__global__ void __launch_bounds__(128) benor_event_big_kernel(KParams p) {
+__global__ void __launch_bounds__(64) benor_event_big_kernel(KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t lane = threadIdx.x & 63u;
   uint32_t *lhist = reinterpret_cast<uint32_t *>(smem);
-  // live runs: the host mailbox's mirror -- [0] request sequence, [1] wave 0
-  // done, [2 ..) requested-stop bits -- written by the polling wave
-  uint32_t *mb = reinterpret_cast<uint32_t *>(smem + p.hist_bytes);
   const uint32_t N = p.N, F = p.F, quorum = p.N - p.F, m = p.m;
   const uint32_t NWd = (N + 63u) >> 6;                       // bitset words (<= 64: one per lane)
-  if (threadIdx.x < 64u) {
-    for (uint32_t i = lane; i < p.hist_len; i += 64u) lhist[i] = 0u;
-    for (uint32_t i = lane; i < kEvMailboxWords; i += 64u) mb[i] = 0u;
-  }
-  __syncthreads();   // the only workgroup barrier: below, wave 0 syncs with itself (wsync)
-  if (LP && threadIdx.x >= 64u) {
-    // ---- the polling wave of a live LP run (launched with 128 threads): it reads
-    // the host-mapped mailbox (a PCIe round trip) so that wave 0 only reads
-    // its LDS mirror between batches, and ends when wave 0 is done
-    uint32_t seen = 0u;
-    for (;;) {
-      if (__hip_atomic_load(&mb[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
-      uint32_t seq = 0u;
-      if (lane == 0u) seq = __hip_atomic_load(p.live_box, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-      seq = rl(seq, 0u);
-      if (seq != seen) {
-        seen = seq;
-        for (uint32_t w = lane; w < 2u * NWd; w += 64u) {
-          const uint32_t v = __hip_atomic_load(p.live_box + kLiveReq + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          if (v) __hip_atomic_fetch_or(&mb[2u + w], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if (lane == 0u) __hip_atomic_store(&mb[0], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-      __builtin_amdgcn_s_sleep(8);
-    }
-    return;
-  }
+  for (uint32_t i = lane; i < p.hist_len; i += 64u) lhist[i] = 0u;
+  __syncthreads();   // the only workgroup barrier: below, the wave syncs with itself (wsync)
 
   BigState S;
-  unsigned char *q = smem + p.hist_bytes + 4u * kEvMailboxWords;
+  unsigned char *q = smem + p.hist_bytes;
   S.ibox = reinterpret_cast<uint64_t *>(q);
   S.killed = S.ibox + 2u * N;
   S.decided = S.killed + 64;
@@ -264,8 +230,7 @@ __global__ void __launch_bounds__(128) benor_event_big_kernel(KParams p) {
     uint32_t next = 0;
     uint64_t next_key = kr ? rstops_min() : (p.ev_nstops ? p.ev_stops[0] : ~0ull);
     __threadfence_block();
-    uint32_t cur = 1, R = 0, halted = 0, seen = 0;
-    long long polled = wall_clock64() - (long long)kLivePollTicks;   // !LP: the first batch polls
+    uint32_t cur = 1, R = 0, halted = 0;
     // the next batch's picks and pool words, loaded while this batch resolves
     // (valid when it starts at pf_e with pf_len messages and pf_b events)
     uint32_t pf_pk = 0u, pf_pv = 0u, pf_tv = 0u, pf_len = 0u, wq = 0xFFFFFFFFu;
@@ -299,49 +264,6 @@ __global__ void __launch_bounds__(128) benor_event_big_kernel(KParams p) {
         } else {
           ++next;
           next_key = next < p.ev_nstops ? p.ev_stops[next] : ~0ull;
-        }
-      }
-      // ---- live GET /stop requests (bo_consensus_start_live).  With the pool in
-      // LDS (LP) a second wave polls the host mailbox and mirrors it in LDS, so
-      // this wave reads the mirror between batches; otherwise this wave reads
-      // the mailbox itself every ~10 us of wall clock (a polling wave there
-      // slowed the run's HBM pool traffic: N=1024 +16 %,
-      // profiles/r05-m_live_poll_wave_net_latency.jsonl).  A new request lands
-      // before delivery e, and e goes back to the host so the run can be
-      // replayed as a schedule.
-      if (p.live_box && (LP || (uint64_t)(wall_clock64() - polled) >= kLivePollTicks)) {
-        uint32_t seq;
-        if constexpr (LP) {
-          seq = __hip_atomic_load(&mb[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        } else {
-          polled = wall_clock64();
-          seq = 0u;
-          if (lane == 0u) seq = __hip_atomic_load(p.live_box, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-          seq = rl(seq, 0u);
-        }
-        if (seq != seen) {
-          seen = seq;
-          uint64_t fresh = 0ull;
-          if (lane < NWd) {
-            uint32_t lo, hi;
-            if constexpr (LP) {
-              lo = __hip_atomic_load(&mb[2u + 2u * lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-              hi = __hip_atomic_load(&mb[3u + 2u * lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            } else {
-              const uint32_t *rq = p.live_box + kLiveReq + 2u * lane;
-              lo = __hip_atomic_load(rq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-              hi = __hip_atomic_load(rq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
-            fresh = ((uint64_t)hi << 32 | lo) & allw & ~S.killed[lane];
-            S.killed[lane] |= fresh;
-          }
-          for (uint64_t f = fresh; f; f &= f - 1ull) {
-            const uint32_t i = 64u * lane + (uint32_t)__builtin_ctzll(f);
-            S.ibox[2u * i] |= kKilled;
-            S.ibox[2u * i + 1u] |= kKilled;
-            __hip_atomic_store(p.live_box + kLiveEv + i, e < 0xFFFFFFFFull ? (uint32_t)e : 0xFFFFFFFEu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          }
-          crashed = crashed || __any(fresh != 0ull);
         }
       }
       if (crashed) {
@@ -600,8 +522,7 @@ __global__ void __launch_bounds__(128) benor_event_big_kernel(KParams p) {
     wsync();
   }
   wsync();
-  if (p.live_box && lane == 0u) __hip_atomic_store(&mb[1], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-  for (uint32_t i = lane; i < p.hist_len; i += 64u) {   // flush_hist over wave 0 only
+  for (uint32_t i = lane; i < p.hist_len; i += 64u) {   // flush_hist
     const uint32_t c = lhist[i];
     if (c) atomicAdd(&p.hist[i], (unsigned long long)c);
   }
@@ -611,7 +532,7 @@ bool event_big_lds_pool(const KParams &p) { return (uint64_t)p.ev_cap * 4u <= kE
 
 uint32_t event_big_lds_bytes(const KParams &p) {
   const uint32_t N = p.N;
-  return p.hist_bytes + 4u * kEvMailboxWords + 16u * N + 8u * 64u * 6u + 2u * ((N + 3u) & ~3u) * 2u + ((N + 15u) & ~15u) + 2u * 2048u * 4u +
+  return p.hist_bytes + 16u * N + 8u * 64u * 6u + 2u * ((N + 3u) & ~3u) * 2u + ((N + 15u) & ~15u) + 2u * 2048u * 4u +
          8u * 64u + 8u * p.ev_rstops +   // random /stop schedule: Floyd set, keys
          (event_big_lds_pool(p) ? 4u * p.ev_cap : 0u);   // the message pool, when it fits
 }
@@ -624,12 +545,12 @@ static hipError_t launch_event_big_lp(const KParams &p, int grid, hipStream_t s)
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  // a live run with the pool in LDS adds the polling wave (threads 64..127)
-  hipLaunchKernelGGL(benor_event_big_kernel<LP>, dim3(grid), dim3(LP && p.live_box ? 128 : 64), lds, s, p);
+  hipLaunchKernelGGL(benor_event_big_kernel<LP>, dim3(grid), dim3(64), lds, s, p);
   return hipGetLastError();
 }
 
 hipError_t launch_event_big(const KParams &p, int grid, hipStream_t s) {
+  if (p.live_box) return hipErrorInvalidValue;      // live runs are benor_event_live.hip's
   return event_big_lds_pool(p) ? launch_event_big_lp<true>(p, grid, s) : launch_event_big_lp<false>(p, grid, s);
 }
 

@@ -135,8 +135,6 @@ constexpr uint32_t kSnapSeq = kSnapReq + 1u;     // the last request served (dev
 constexpr uint32_t kSnapE = kSnapSeq + 1u;       // u64: the delivery count the snapshot reflects
 constexpr uint32_t kSnapSt = kSnapE + 4u;        // [BO_MAX_N] {killed | x << 8 | decided << 16, k}: the snapshot
 constexpr uint32_t kLiveBoxWords = kSnapSt + 2u * BO_MAX_N;
-constexpr uint64_t kLivePollTicks = 1000;        // wall-clock ticks (100 MHz) between wave 0's own mailbox polls
-constexpr uint32_t kEvMailboxWords = 4u + 128u;  // the event kernel's LDS mirror of it: seq, done, request bits, pad
 
 constexpr uint32_t kMfmaContRounds = 3;       // matrix-core passes up to round 3, then the popcount kernel
 // The deferral buffer's 64-word length block: pass r's list length at 16 (r - 1).

@@ -327,8 +327,9 @@ def event_network(benor, N=1024, F=341, stop_node=500, stop_after=300_000, seed=
     """SURVEY §8f #2 at BASELINE configs[3]'s size: one network through the
     reference's calls -- launchNetwork, startConsensus with a mid-run GET /stop
     of one node after `stop_after` deliveries (node.ts:191-194) -- on the
-    event-level kernel for N > 256 (one wave per trial, benor_event_big.hip).
-    Wall time of startConsensus and the deliveries it simulated."""
+    workgroup-batched event kernel (benor_event_live.hip), as the default
+    (live) start runs.  Wall time of startConsensus and the deliveries it
+    simulated."""
     m = N - F
     init = [0] * F + [1] * (m // 2) + [0] * (m // 2) + ["?"] * (m % 2)
     faulty = [i < F for i in range(N)]

@@ -9,10 +9,11 @@ Python, startConsensus(N, {stopAfter}) in js/index.js): the network API runs
 the event-level kernel for one trial and serves its final per-node states.
 
 GPU: per-node states equal oracle (iii) event_trial (oracle/benor_oracle.c,
-trial 0 of the same seed and schedule) at N = 5, 10, 256 (one lane per
-trial, benor_event_kernel) and N = 1024, 4096 (one wave per trial,
-benor_event_big.hip), with stops inside round 1 and inside round 2, through
-the C ABI and through the N-API addon.  CPU: the schedule's validation.
+trial 0 of the same seed and schedule) at N = 5, 10, 256, 1024 and 4096
+(a network start with a schedule runs the live-run kernels of
+benor_event_live.hip: registers at N <= 16, one wave at N <= 64, a workgroup
+above), with stops inside round 1 and inside round 2, through the C ABI and
+through the N-API addon.  CPU: the schedule's validation.
 """
 import json
 import os
@@ -71,8 +72,8 @@ def cases():
 
 
 def big_cases():
-    """Networks above the one-lane event kernel's N <= 256 (benor_event_big.hip,
-    VERDICT r03 #2): BASELINE configs[3]'s N = 1024, F = 341 and configs[4]'s
+    """Networks above the one-lane event kernel's N <= 256 (VERDICT r03 #2;
+    the workgroup form of benor_event_live.hip since r06): BASELINE configs[3]'s N = 1024, F = 341 and configs[4]'s
     N = 4096, F = 1365.  m is odd there, so a random start decides in round 1;
     as many 1s as 0s plus one "?" make every R-phase tie (node.ts:63-69) and
     every node take its coin, so the run reaches round 2.  Round 1 spans
