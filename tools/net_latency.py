@@ -35,7 +35,7 @@ def main():
         init = [(i * 7 + 3) % 2 for i in range(N)]
         for start, kw in (("default", {}), ("sync", {"sync": True})):
             times, phases = [], []
-            reps = a.reps if N < 1024 or start == "sync" else max(5, a.reps // (20 if F < 512 else 60))
+            reps = a.reps if N < 1024 or start == "sync" else max(5, a.reps // (5 if F < 512 else 60))
             for rep in range(reps + 5):
                 t0 = time.perf_counter()
                 benor.launchNetwork(N, F, init, faulty)
