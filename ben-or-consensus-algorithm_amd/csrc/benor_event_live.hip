@@ -1,49 +1,52 @@
-// benor_event_live.hip -- the workgroup-batched event kernel (r06): live runs
-// (bo_consensus_start_live, the default startConsensus) at every N <= 4096.
+// benor_event_live.hip -- the event kernels of live runs (r06): the default
+// startConsensus (bo_consensus_start_live) and network starts with a /stop
+// schedule, at every N <= 4096.
 //
 // The reference's GET /start answers before consensus finishes
 // (consensus.ts:3-8, node.ts:167-188): its round loop is the POST /message
 // handler (node.ts:43-163) firing message by message, and a GET /stop
 // (node.ts:191-194) or GET /getState (node.ts:197-199) may arrive at any
-// moment.  This kernel runs the message-granular model of oracle (iii),
+// moment.  These kernels run the message-granular model of oracle (iii),
 // oracle/benor_oracle.c event_trial() -- one delivery per event in the seeded
 // order (uniform pick from the pending pool, swap-remove), scheduled and live
-// stops applied before their delivery count -- for ONE trial per workgroup.
-// r05 ran a live trial on one wave (benor_event_big.hip: 64 events per batch,
-// every step on one SIMD); here a trial gets a workgroup of up to 15 event
-// waves plus one control wave:
+// stops applied before their delivery count -- for ONE trial per workgroup,
+// in one of three forms by N (launch_event_wg):
 //
-//   * the event waves take a batch of B <= 64 W consecutive events: lane i
-//     draws the pick of event e + i assuming no trigger (splitmix64 is a
-//     counter), loads the two pool words its swap-remove touches, and inserts
-//     its pick into an LDS hash table that keeps, per position, the first
-//     event of the batch that picks it;
-//   * a batch is exact up to its first *conflict* -- an event that picks a
-//     position an earlier event of the batch picked, or whose tail word an
-//     earlier event overwrote -- so the batch is cut there (the conflict-free
-//     prefix reads the pool's own words: no chains to resolve);
-//   * its deliveries are applied at once with 64-bit LDS adds of
+//   * N > 64 (benor_event_wg_kernel): a control wave and up to 15 event
+//     waves.  The event waves take a batch of B <= 64 W consecutive events:
+//     lane i draws the pick of event e + i assuming no trigger (splitmix64 is
+//     a counter), loads the two pool words its swap-remove touches, and
+//     inserts its pick into an LDS hash table {position, pickers, first
+//     picker}.  A word one earlier event of the batch moved is forwarded; a
+//     second level, or a third picker of one position, cuts the batch there.
+//     The deliveries are applied at once with 64-bit LDS adds of
 //     {len, c0 | c1} to the receivers' inbox slots.  With exactly F faulty
 //     every slot receives exactly N - F messages per round (each trigger fires
 //     once), so a slot that reaches its quorum inside the batch
-//     triggers at the LAST batch event into it; the batch is cut after the
-//     earliest such event and the later events' adds are undone;
-//   * the conflict-free prefix then writes its moved words back, the control
-//     wave runs the trigger (node.ts:53-80 R-phase, :89-157 P-phase: decide,
-//     adopt, coin, all-decided halting) and the event waves append its
-//     broadcast of N messages;
-//   * the control wave issues no pool access: it owns the round state in LDS,
-//     applies scheduled /stop (delivery counts) and live /stop requests, and
-//     polls the host-mapped mailbox with an uncached load that it consumes
-//     ~20 us later (so the PCIe round trip is never waited for), and serves
-//     GET /getState snapshots: on request, the event waves write every node's
-//     {killed, x, decided, k} at a batch boundary to host memory with the
-//     delivery count it reflects, so a snapshot is oracle (iii) truncated at
-//     that count.
+//     triggers at the LAST batch event into it; the batch ends after the
+//     earliest such event and the later events' adds are undone.  The used
+//     events write their moved words back, the control wave runs the trigger
+//     (node.ts:53-80 R-phase, :89-157 P-phase: decide, adopt, coin,
+//     all-decided halting) and the event waves append its broadcast of N
+//     messages.  The control wave issues no pool access: it owns the round
+//     state, applies scheduled and live /stop requests, and polls the
+//     host-mapped mailbox with an uncached load that it consumes ~20 us later
+//     (so the PCIe round trip is never waited for);
+//   * 16 < N <= 64 (benor_event_wave_kernel): one wave, micro-batches of up to
+//     64 events with the pool in LDS, every chain of the batch's moves
+//     followed back, so a batch runs to its first trigger;
+//   * N <= 16 (benor_event_reg_kernel): one wave, one event per step, the
+//     pool, the inbox slots and the node state in registers.
 //
-// Pool: `to | ph << 12 | x << 13 | (k & 3) << 15` (k decoded against the
-// completion round `cur`, as benor_event_big.hip), in HBM scratch or -- when
-// 4N^2 + 64 words fit kEventBigLdsPool (N <= 78) -- in LDS.
+// All three serve GET /getState snapshots: on request they write every node's
+// {killed, x, decided, k} at a batch boundary to host memory with the
+// delivery count it reflects, so a snapshot is oracle (iii) truncated at
+// that count.
+//
+// Pool words (workgroup and LDS-wave forms): `to | ph << 12 | x << 13 |
+// (k & 3) << 15` (k decoded against the completion round `cur`, as
+// benor_event_big.hip), in HBM scratch or -- when 4N^2 + 64 words fit
+// kEventBigLdsPool (N <= 78) -- in LDS.
 #include "benor_device.h"
 
 #include <type_traits>
