@@ -19,6 +19,8 @@
  *   networkStop(handle) / nodeStop(handle, i)       consensus.ts:10-15, node.ts:191-194
  *   getState(handle, i) -> {killed, x, decided, k}  node.ts:197-199 (at once: a snapshot
  *       of a live run in flight)
+ *   networkCreateTyped(N, F, Int8Array, Uint8Array) -> handle   the same, values encoded in JS
+ *   getStatesRaw(handle) -> {buf, events}          the same records as an ArrayBuffer (decoded in JS)
  *   getStates(handle) -> {states, events}          every node at once (bo_get_states):
  *       events = the deliveries a live run's snapshot reflects, null otherwise
  *   consensusPoll(handle) -> boolean               a live run is in flight (bo_consensus_poll)
@@ -137,6 +139,44 @@ static napi_value network_create(napi_env env, napi_callback_info info) {
     int rc = bo_network_create(N, F, init, ni, fl, nf, &net);
     free(init);
     free(fl);
+    if (rc) { throw_bo(env, rc); return NULL; }
+    napi_value ext;
+    NAPI_CALL(env, napi_create_external(env, net, finalize_net, NULL, &ext));
+    return ext;
+}
+
+/* networkCreate with the values already encoded by the JS wrapper (js/index.js
+ * encodeValues: Int8Array 0 / 1 / 2 = "?" / -2 invalid, Uint8Array 1 = faulty):
+ * the same bo_network_create, no per-element N-API calls. */
+static int typed_bytes(napi_env env, napi_value v, napi_typedarray_type want, void **data, uint32_t *len) {
+    bool is = false;
+    napi_is_typedarray(env, v, &is);
+    if (!is) return 0;
+    napi_typedarray_type t;
+    size_t n = 0, off = 0;
+    napi_value ab;
+    if (napi_get_typedarray_info(env, v, &t, &n, data, &ab, &off) != napi_ok || t != want) return 0;
+    *len = (uint32_t)n;
+    return 1;
+}
+
+static napi_value network_create_typed(napi_env env, napi_callback_info info) {
+    size_t argc = 4;
+    napi_value argv[4];
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    int ok = argc == 4;
+    uint32_t N = ok ? get_u32(env, argv[0], &ok) : 0, F = ok ? get_u32(env, argv[1], &ok) : 0;
+    void *init = NULL, *fl = NULL;
+    uint32_t ni = 0, nf = 0;
+    if (!ok || !typed_bytes(env, argv[2], napi_int8_array, &init, &ni) ||
+        !typed_bytes(env, argv[3], napi_uint8_array, &fl, &nf)) {
+        napi_throw_type_error(env, NULL, "networkCreateTyped(N, F, Int8Array, Uint8Array)");
+        return NULL;
+    }
+    static const uint8_t none = 0;
+    bo_network *net = NULL;
+    int rc = bo_network_create(N, F, ni ? (const int8_t *)init : (const int8_t *)&none, ni,
+                               nf ? (const uint8_t *)fl : &none, nf, &net);
     if (rc) { throw_bo(env, rc); return NULL; }
     napi_value ext;
     NAPI_CALL(env, napi_create_external(env, net, finalize_net, NULL, &ext));
@@ -407,6 +447,30 @@ static napi_value get_states(napi_env env, napi_callback_info info) {
     return o;
 }
 
+/* getStates as raw bo_node_state records (8 bytes each: int8 killed, x,
+ * decided, pad; int32 k) in an ArrayBuffer, decoded by js/index.js: one N-API
+ * allocation instead of five calls per node. */
+static napi_value get_states_raw(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1];
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    bo_network *net = get_net(env, argv[0]);
+    if (!net) return NULL;
+    const uint32_t N = bo_network_size(net);
+    void *data = NULL;
+    napi_value ab, o, v;
+    NAPI_CALL(env, napi_create_arraybuffer(env, sizeof(bo_node_state) * (N ? N : 1), &data, &ab));
+    uint64_t ev = 0;
+    int rc = bo_get_states(net, (bo_node_state *)data, N, &ev);
+    if (rc) { throw_bo(env, rc); return NULL; }
+    napi_create_object(env, &o);
+    napi_set_named_property(env, o, "buf", ab);
+    if (ev == UINT64_MAX) napi_get_null(env, &v);
+    else napi_create_double(env, (double)ev, &v);
+    napi_set_named_property(env, o, "events", v);
+    return o;
+}
+
 static napi_value consensus_poll(napi_env env, napi_callback_info info) {
     size_t argc = 1;
     napi_value argv[1];
@@ -603,6 +667,8 @@ static napi_value init_module(napi_env env, napi_value exports) {
         {"nodeStop", NULL, node_stop, NULL, NULL, NULL, napi_default, NULL},
         {"getState", NULL, get_state, NULL, NULL, NULL, napi_default, NULL},
         {"getStates", NULL, get_states, NULL, NULL, NULL, napi_default, NULL},
+        {"getStatesRaw", NULL, get_states_raw, NULL, NULL, NULL, napi_default, NULL},
+        {"networkCreateTyped", NULL, network_create_typed, NULL, NULL, NULL, napi_default, NULL},
         {"consensusPoll", NULL, consensus_poll, NULL, NULL, NULL, napi_default, NULL},
         {"status", NULL, status, NULL, NULL, NULL, napi_default, NULL},
         {"runTrials", NULL, run_trials, NULL, NULL, NULL, napi_default, NULL},

@@ -41,8 +41,29 @@ function stopSchedule(N, stopAfter) {
   return sched;
 }
 
+// The Value encoding of bo_network_create (0, 1, 2 = "?", anything else -2:
+// rejected there) and launchNodes.ts:12's `el === true` for faulty nodes, done
+// here so that the addon takes two typed arrays instead of 2N elements.
+function encodeValues(initialValues) {
+  const out = new Int8Array(initialValues.length);
+  for (let i = 0; i < out.length; i++) {
+    const v = initialValues[i];
+    out[i] = v === 0 ? 0 : v === 1 ? 1 : v === '?' ? 2 : -2;
+  }
+  return out;
+}
+
+function encodeFaulty(faultyList) {
+  const out = new Uint8Array(faultyList.length);
+  for (let i = 0; i < out.length; i++) out[i] = faultyList[i] === true ? 1 : 0;
+  return out;
+}
+
 async function launchNetwork(N, F, initialValues, faultyList) {
-  const handle = addon.networkCreate(N, F, initialValues, faultyList);   // throws the reference's Errors
+  // throws the reference's Errors (bo_network_create validates, in its order)
+  const handle = Array.isArray(initialValues) && Array.isArray(faultyList)
+    ? addon.networkCreateTyped(N, F, encodeValues(initialValues), encodeFaulty(faultyList))
+    : addon.networkCreate(N, F, initialValues, faultyList);
   current = { handle, N, running: null };
   const servers = [];
   for (let i = 0; i < N; i++) servers.push(new NodeServer(i));
@@ -141,15 +162,30 @@ async function getNodeState(nodeId) {
   return addon.getState(net().handle, nodeId);
 }
 
+// bo_node_state records (8 bytes: int8 killed, x, decided, pad; int32 k) ->
+// NodeState objects (src/types.ts:1-8), as the addon's getState builds them.
+function decodeStates(buf) {
+  const b = new Int8Array(buf), k = new Int32Array(buf), n = b.length >> 3, out = new Array(n);
+  for (let i = 0; i < n; i++) {
+    const x = b[8 * i + 1], d = b[8 * i + 2], kk = k[2 * i + 1];
+    out[i] = { killed: b[8 * i] !== 0, x: x < 0 ? null : x === 2 ? '?' : x, decided: d < 0 ? null : d !== 0,
+               k: kk < 0 ? null : kk };
+  }
+  return out;
+}
+
 // __test__/tests/utils.ts:14-20: every node's state, from one snapshot.
 async function getNodesState(N) {
-  return addon.getStates(net(N).handle).states;
+  const cur = net(N);
+  return decodeStates(addon.getStatesRaw(cur.handle).buf).slice(0, cur.N);
 }
 
 // The same with the delivery count a live run's snapshot reflects (null when
 // no run is in flight): oracle (iii) truncated there gives the states.
 async function getNodesStateAt(N) {
-  return addon.getStates(net(N).handle);
+  const cur = net(N);
+  const r = addon.getStatesRaw(cur.handle);
+  return { states: decodeStates(r.buf).slice(0, cur.N), events: r.events };
 }
 
 // GET /status: { status: 500, body: "faulty" } | { status: 200, body: "live" }

@@ -31,6 +31,7 @@
 #   matrix          tools/perf_matrix.py over its built-in shape list
 #   liveprof        tools/live_profile.py (LIVEPROF_ARGS): a live run's batch counters and cycle split
 #   livepmc         PMC passes (PMC_GROUPS) over tools/live_profile.py (LIVEPROF_ARGS)
+#   jslat           tools/js_latency.js (JSLAT_REPS): the same through the N-API addon (the JS drop-in)
 #   netlat          tools/net_latency.py (NETLAT_ARGS): the reference's launch + start + final states
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R" || exit 1
@@ -164,6 +165,9 @@ for step in "$@"; do
     netlat)
       timeout -k 10 400 python -u tools/net_latency.py ${NETLAT_ARGS:---reps 60} > "$OUT/net_latency.jsonl" 2> "$OUT/net_latency.err"
       chk $? netlat; cat "$OUT/net_latency.jsonl";;
+    jslat)
+      timeout -k 10 300 node tools/js_latency.js ${JSLAT_REPS:-60} > "$OUT/js_latency.jsonl" 2> "$OUT/js_latency.err"
+      chk $? jslat; cat "$OUT/js_latency.jsonl";;
     *)
       echo "unknown step $step"; exit 2;;
   esac
