@@ -171,8 +171,9 @@ int bo_get_state(const bo_network *net, uint32_t node, bo_node_state *out);
  * n == N.  During a live run: one snapshot of the running kernel, taken at a
  * batch boundary after *events_out POST /message deliveries -- exactly oracle
  * (iii) truncated there, plus the killed flags of /stop requests served but
- * not yet applied; otherwise the network's states and *events_out =
- * UINT64_MAX.  events_out may be NULL. */
+ * not yet applied; a snapshot taken within the last 500 us answers later
+ * requests too (N concurrent GET /getState cost one).  Otherwise the
+ * network's states and *events_out = UINT64_MAX.  events_out may be NULL. */
 int bo_get_states(const bo_network *net, bo_node_state *out, uint32_t n, uint64_t *events_out);
 
 /* GET /status (node.ts:33-39): returns 500 ("faulty") or 200 ("live"), or a
