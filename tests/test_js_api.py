@@ -34,6 +34,17 @@ def test_js_reference_suite():
     _run("all")
 
 
+@needs_node
+def test_js_typed_paths_agree_with_the_addon():
+    """js/index.js encodes launchNetwork's arrays itself and decodes raw state
+    records; the same errors and NodeState objects as the addon's per-element
+    paths (tests/js/typed_paths.test.js, pre-run states: no GPU)."""
+    p = subprocess.run(["node", os.path.join(ROOT, "tests", "js", "typed_paths.test.js")], capture_output=True,
+                       text=True, timeout=120)
+    print(p.stdout, p.stderr)
+    assert p.returncode == 0, p.stdout + p.stderr
+
+
 HTTP_SCRIPT = os.path.join(ROOT, "tests", "js", "http_facade.test.js")
 
 
