@@ -1139,14 +1139,24 @@ __global__ void __launch_bounds__(64) benor_event_wave_kernel(KParams p) {
 //     and the increment its delivery adds, so a delivery is one read-add-select;
 //   * 64 picks per block (lane i: the pick word of event e + i, splitmix64
 //     is a counter), one readlane per event;
+//   * while the pool holds <= 64 words (at N = 10, F = 5 it never holds more
+//     than ~50) it lives in one VGPR alone, and the array form starts at the
+//     first broadcast past 64 (no register-array copies around a trigger);
 //   * the trigger, the stops, the mailbox and the snapshots as the wave
-//     kernel, node state in lane registers and SGPR masks.
+//     kernel, node state in lane registers and 32-bit SGPR masks, the four
+//     open rounds' completion masks packed in one 64-bit scalar.
 // Words: slot | (k & 3) << 6 | {1 << 24 | (x == 0) << 8 | (x == 1) << 16}.
-template <int R>
+// At N = 10, F = 5 a batch (~10 deliveries and a trigger) takes ~3200 shader
+// cycles (r06-F: 3600): ~2150 the deliveries (~215 each: three v_readlane ->
+// SALU hops), ~330 the loop head and ~720 the trigger (phase stamps in
+// r06-G5, since dropped: their SGPRs cost 6 %).  A/Bs of each change on one
+// box: profiles/r06-G_reg_kernel_ab.jsonl.
+template <int R, bool SM>
 __global__ void __launch_bounds__(64) benor_event_reg_kernel(KParams p) {
+  using M = uint32_t;                                                 // node masks (N <= 16)
   const uint32_t lane = threadIdx.x;
   const uint32_t N = p.N, F = p.F, quorum = p.N - p.F, m = p.m, kmax = p.k_max, cap = p.ev_cap;
-  const uint64_t all = (1ull << N) - 1ull;                           // N <= kEventRegMaxN
+  const M all = (M(1) << N) - M(1);                                   // N <= kEventRegMaxN
   const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
   uint32_t *box = p.live_box;
   unsigned long long *const stats = p.ev_stats;
@@ -1175,12 +1185,12 @@ __global__ void __launch_bounds__(64) benor_event_reg_kernel(KParams p) {
     asm volatile("" : "+v"(t_start), "+v"(w_start));   // cold: kept out of the SGPR file
     // ---- node.ts:21-26 (lane = node): faulty nodes killed with x = k = null
     const uint32_t myid = lane < m ? p.live_ids[lane] : 0xFFFFFFFFu;   // compact lane c -> node id
-    uint64_t live = 0ull;
-    for (uint32_t c = 0; c < m; ++c) live |= 1ull << rl(myid, c);
-    uint64_t killed = all & ~live, decided = 0ull;
+    M live = 0;
+    for (uint32_t c = 0; c < m; ++c) live |= M(1) << rl(myid, c);
+    M killed = all & ~live, decided = 0;
     uint32_t X = 0xFFFFFFFFu, K = 0xFFFFFFFFu, CI = 0u;
     for (uint32_t c = 0; c < m; ++c) CI = lane == rl(myid, c) ? c : CI;
-    if ((live >> lane) & 1ull) {
+    if (lane < N && ((live >> lane) & 1u)) {
       int32_t v;
       if (p.init_mode == BO_INIT_RANDOM) {        // oracle_random_init (m <= 32)
         v = (int32_t)((init_word_small(k0, k1, trial) >> CI) & 1u);
@@ -1199,13 +1209,11 @@ __global__ void __launch_bounds__(64) benor_event_reg_kernel(KParams p) {
       P[r] = c < m ? (2u * n) | (1u << 6) | inc_of(xc & 3u) : 0u;
     }
     // inbox slots; bit 7: the receiver is killed
-    uint32_t CNT = lane < 2u * N && !((live >> (lane >> 1)) & 1ull) ? 0x80u : 0u;
-    // round k complete at k & 3, in lane k & 3 (the SGPR file is full)
+    uint32_t CNT = lane < 2u * N && !((live >> (lane >> 1)) & 1u) ? 0x80u : 0u;
+    // round k complete: the nodes done with it in bits 16 (k & 3) .. + 15 of one scalar
     uint64_t CPV = 0ull;
-    auto comp_get = [&](uint32_t i) {
-      return ((uint64_t)rl((uint32_t)(CPV >> 32), i) << 32) | rl((uint32_t)CPV, i);
-    };
-    auto comp_set = [&](uint32_t i, uint64_t v) { CPV = lane == i ? v : CPV; };
+    auto comp_get = [&](uint32_t i) -> M { return (M)((CPV >> (16u * i)) & 0xFFFFull); };
+    auto comp_set = [&](uint32_t i, M v) { CPV = (CPV & ~(0xFFFFull << (16u * i))) | ((uint64_t)v << (16u * i)); };
     uint64_t rngb;
     {
       const uint4 o = philox4x32_10<false>(k0, k1, make_uint4(tlo, thi, 0u, kStreamOrder << 24));
@@ -1218,20 +1226,26 @@ __global__ void __launch_bounds__(64) benor_event_reg_kernel(KParams p) {
     uint32_t H = 0u, hi = 64u;                     // the block's picks, the next one's lane
     auto advance = [&]() {                         // node.ts:116-145 as DESIGN §2
       for (;;) {
-        const uint64_t cw = comp_get(cur & 3u);
+        const M cw = comp_get(cur & 3u);
         if ((cw | killed) != all) return;
         if ((decided | killed) == all) { halted = 1u; Rr = cur; return; }
         if (cur >= kmax) { halted = 2u; Rr = cur; return; }
-        comp_set(cur & 3u, 0ull);
+        comp_set(cur & 3u, 0);
         ++cur;
       }
     };
     auto kill = [&](uint32_t i) {                  // GET /stop (node.ts:191-194): drops every later message
-      killed |= 1ull << i;
+      killed |= M(1) << i;
       CNT |= (lane >> 1) == i ? 0x80u : 0u;
     };
     auto pread = [&](uint32_t pos) { return rl(P[pos >> 6], pos & 63u); };
-    while (!halted) {
+    // While the pool fits one register (len <= 64; at N = 10, F = 5 it
+    // never holds more than ~50 words) it lives in P0 alone and the array P
+    // is untouched; the batch that outgrows P0 writes it back to P[0] and
+    // the run goes on in the array form.  One batch: 0 go on, 1 the run
+    // ended, 2 the pool left P0.
+    uint32_t P0 = P[0];
+    auto batch = [&](auto small) -> uint32_t {
       // ---- scheduled GET /stop before delivery e
       bool crashed = false;
       while ((next_key >> 12) == e) {
@@ -1248,9 +1262,9 @@ __global__ void __launch_bounds__(64) benor_event_reg_kernel(KParams p) {
           const uint32_t seq = rl(pv_word, 1u), sreq = rl(pv_word, 2u);
           apply_next = seq != seq_seen;
           seq_seen = seq;
-          const uint64_t fresh = req & all & ~killed;
-          for (uint64_t f = fresh; f; f &= f - 1ull) {
-            const uint32_t i = (uint32_t)__builtin_ctzll(f);
+          const M fresh = (M)req & all & ~killed;
+          for (M f = fresh; f; f &= f - 1) {
+            const uint32_t i = (uint32_t)__builtin_ctzll((uint64_t)f);
             kill(i);
             if (lane == 0u)
               __hip_atomic_store(box + kLiveEv + i, e < 0xFFFFFFFFull ? (uint32_t)e : 0xFFFFFFFEu, __ATOMIC_RELAXED,
@@ -1262,8 +1276,8 @@ __global__ void __launch_bounds__(64) benor_event_reg_kernel(KParams p) {
             snap_served = sreq;
             if (lane < N) {
               const bool f = (int32_t)K < 0 && (int32_t)X < 0;
-              const uint32_t kl = (uint32_t)((killed >> lane) & 1ull) | ((X & 0xFFu) << 8) |
-                                  ((f ? 0xFFu : (uint32_t)((decided >> lane) & 1ull)) << 16);
+              const uint32_t kl = (uint32_t)((killed >> lane) & 1u) | ((X & 0xFFu) << 8) |
+                                  ((f ? 0xFFu : (uint32_t)((decided >> lane) & 1u)) << 16);
               __hip_atomic_store(box + kSnapSt + 2u * lane, kl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
               __hip_atomic_store(box + kSnapSt + 2u * lane + 1u, K, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
@@ -1278,11 +1292,11 @@ __global__ void __launch_bounds__(64) benor_event_reg_kernel(KParams p) {
         }
       }
       if (crashed) {
-        if (killed == all) { halted = 3u; break; }
+        if (killed == all) { halted = 3u; return 1u; }
         advance();
-        if (halted) break;
+        if (halted) return 1u;
       }
-      if (len == 0u) { halted = 3u; break; }
+      if (len == 0u) { halted = 3u; return 1u; }
       if (hi == 64u) {                             // the next 64 picks (event e + i in lane i)
         const uint64_t z = smix(rngb + (uint64_t)(lane + 1u) * kGm);
         H = (uint32_t)(z >> 32);
@@ -1301,7 +1315,11 @@ __global__ void __launch_bounds__(64) benor_event_reg_kernel(KParams p) {
       // one delivery: false when its slot reaches the quorum (the trigger)
       auto deliver = [&](uint32_t w, auto late) {  // late: messages of round >= k_max + 3 are dropped
         if (decltype(late)::value && cur + (((w >> 6) - cur) & 3u) >= kmax + 3u) return true;
-        const uint32_t s = w & 63u;
+        // one register: the slot through the SALU (a v_readlane lane select
+        // written by the previous v_readlane stalls longer; r06-G5, 4 % per
+        // event at N = 10; in the array form it costs, r06-G7)
+        uint32_t s = w & 63u;
+        if constexpr (decltype(small)::value) asm volatile("s_and_b32 %0, %1, 63" : "=s"(s) : "s"(w));
         const uint32_t c = rl(CNT, s) + (w & 0xFFFFFF00u);
         CNT = wl(CNT, c, s);
         // killed receivers drop the message (node.ts:45): their slots count
@@ -1313,20 +1331,51 @@ __global__ void __launch_bounds__(64) benor_event_reg_kernel(KParams p) {
         return false;
       };
       auto steps = [&](auto late) {
-        if (len <= 64u) {                          // the whole pool in lane p of one register
-          uint32_t P0 = P[0];
+        if constexpr (decltype(small)::value && !decltype(late)::value) {
+          // the common case, one register and no late drops: one exit test
+          // per delivery (the segment's end or a quorum)
+          uint32_t Q0 = P0, rem = seg, w = 0u, c = 0u;
+          if (rem) {
+            for (;;) {
+              len = uni(len);
+              const uint32_t q = uni((uint32_t)(((uint64_t)rl(H, hi + j) * len) >> 32));
+              w = rl(Q0, q);
+              --len;
+              const uint32_t tv = rl(Q0, len);
+              Q0 = lane == q ? tv : Q0;            // the tail word moves to q
+              ++j;
+              --rem;
+              uint32_t s;
+              asm volatile("s_and_b32 %0, %1, 63" : "=s"(s) : "s"(w));
+              c = rl(CNT, s) + (w & 0xFFFFFF00u);
+              CNT = wl(CNT, c, s);
+              const uint32_t x = (c & 0xFF000080u) ^ qmark;   // 0: a live slot reached its quorum
+              if (uni(x < rem ? x : rem) == 0u) break;
+            }
+            if ((c & 0xFF000080u) == qmark) {
+              tw = w;
+              tc = c;
+              fired = true;
+            }
+          }
+          P0 = Q0;
+          return;
+        }
+        if (decltype(small)::value || len <= 64u) {   // the whole pool in lane p of one register
+          uint32_t Q0 = decltype(small)::value ? P0 : P[0];
           while (j < seg) {
             j = uni(j);
             len = uni(len);
             const uint32_t q = uni((uint32_t)(((uint64_t)rl(H, hi + j) * len) >> 32));
-            const uint32_t w = rl(P0, q);
+            const uint32_t w = rl(Q0, q);
             --len;
-            const uint32_t tv = rl(P0, len);
-            P0 = lane == q ? tv : P0;              // the tail word moves to q
+            const uint32_t tv = rl(Q0, len);
+            Q0 = lane == q ? tv : Q0;              // the tail word moves to q
             ++j;
             if (!deliver(w, late)) break;
           }
-          P[0] = P0;
+          if (decltype(small)::value) P0 = Q0;
+          else P[0] = Q0;
           return;
         }
         while (j < seg) {
@@ -1351,7 +1400,7 @@ __global__ void __launch_bounds__(64) benor_event_reg_kernel(KParams p) {
       if (stats) cyc_steps += __builtin_amdgcn_s_memtime() - c_a;
       e += j;
       hi += j;
-      if (!fired) continue;
+      if (!fired) return 0u;
       ++trig;
       // ---- the trigger (node.ts:52-80 R-phase, :88-157 P-phase)
       const uint32_t s = tw & 63u, to = s >> 1, ph = s & 1u;
@@ -1379,8 +1428,8 @@ __global__ void __launch_bounds__(64) benor_event_reg_kernel(KParams p) {
         }
         X = wl(X, nx, to);
         K = wl(K, k + 1u, to);
-        if (dec) decided |= 1ull << to;
-        comp_set(k & 3u, comp_get(k & 3u) | (1ull << to));
+        if (dec) decided |= M(1) << to;
+        comp_set(k & 3u, comp_get(k & 3u) | (M(1) << to));
         advance();
         if (!halted) base = ((((k + 1u) & 3u) << 6)) | inc_of(nx);
       }
@@ -1388,7 +1437,16 @@ __global__ void __launch_bounds__(64) benor_event_reg_kernel(KParams p) {
         if (len + N > cap) {
           overflow = 1u;
           halted = 3u;
-          break;
+          return 1u;
+        }
+        if (decltype(small)::value) {
+          if (len + N <= 64u) {
+            const uint32_t d = lane - len;
+            P0 = d < N ? 2u * d + base : P0;
+            len += N;
+            return 0u;
+          }
+          P[0] = P0;                               // the pool outgrows one register
         }
         const uint32_t r0 = len >> 6, r1 = (len + N - 1u) >> 6;
         if (r1 == 0u) {                            // within register 0
@@ -1407,10 +1465,23 @@ __global__ void __launch_bounds__(64) benor_event_reg_kernel(KParams p) {
           P[r1] = reg;
         }
         len += N;
+        if (decltype(small)::value) return 2u;
+      }
+      return 0u;
+    };
+    if constexpr (SM) {                            // SM: the launch's pool starts in one register
+      bool grown = len > 64u;
+      while (!halted && !grown) {
+        const uint32_t r = batch(std::true_type{});
+        if (r == 1u) break;
+        grown = r == 2u;
       }
     }
+    while (!halted) {
+      if (batch(std::false_type{}) == 1u) break;
+    }
     // ---- outcome over the nodes still running
-    const bool run = lane < N && !((killed >> lane) & 1ull);
+    const bool run = lane < N && !((killed >> lane) & 1u);
     const bool g0 = __any(run && X == 0u), g1 = __any(run && X == 1u), gq = __any(run && X != 0u && X != 1u);
     const bool gl = __any(run);
     const uint32_t vv = (!gl || gq || (g0 && g1)) ? 2u : (g1 ? 1u : 0u);
@@ -1432,9 +1503,9 @@ __global__ void __launch_bounds__(64) benor_event_reg_kernel(KParams p) {
     if (p.node_out && lane < N) {
       bo_node_state ns;
       const bool f = (int32_t)K < 0 && (int32_t)X < 0;   // faulty from launch (never ran)
-      ns.killed = (int8_t)((killed >> lane) & 1ull);
+      ns.killed = (int8_t)((killed >> lane) & 1u);
       ns.x = (int8_t)X;
-      ns.decided = f ? (int8_t)-1 : (int8_t)((decided >> lane) & 1ull);
+      ns.decided = f ? (int8_t)-1 : (int8_t)((decided >> lane) & 1u);
       ns.pad = 0;
       ns.k = (int32_t)K;
       p.node_out[lane] = ns;
@@ -1508,8 +1579,13 @@ uint32_t event_wave_lds_bytes(const KParams &p) {
 
 hipError_t launch_event_wg(const KParams &p, int grid, hipStream_t s) {
   if (const uint32_t regs = event_reg_regs(p)) {
-    if (regs == 16u) hipLaunchKernelGGL(benor_event_reg_kernel<16>, dim3(grid), dim3(64), 0, s, p);
-    else hipLaunchKernelGGL(benor_event_reg_kernel<32>, dim3(grid), dim3(64), 0, s, p);
+    // the one-register pool mode only where the pool starts there (m N <= 64):
+    // compiled in, it slows the array form by 5-8 % (r06-G9, N = 12 and 16)
+    const bool sm = p.m * p.N <= 64u;
+    if (regs == 16u && sm) hipLaunchKernelGGL((benor_event_reg_kernel<16, true>), dim3(grid), dim3(64), 0, s, p);
+    else if (regs == 16u) hipLaunchKernelGGL((benor_event_reg_kernel<16, false>), dim3(grid), dim3(64), 0, s, p);
+    else if (sm) hipLaunchKernelGGL((benor_event_reg_kernel<32, true>), dim3(grid), dim3(64), 0, s, p);
+    else hipLaunchKernelGGL((benor_event_reg_kernel<32, false>), dim3(grid), dim3(64), 0, s, p);
     return hipGetLastError();
   }
   if (event_wave_form(p)) {
