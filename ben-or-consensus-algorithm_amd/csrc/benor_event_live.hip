@@ -1146,11 +1146,13 @@ __global__ void __launch_bounds__(64) benor_event_wave_kernel(KParams p) {
 //     kernel, node state in lane registers and 32-bit SGPR masks, the four
 //     open rounds' completion masks packed in one 64-bit scalar.
 // Words: slot | (k & 3) << 6 | {1 << 24 | (x == 0) << 8 | (x == 1) << 16}.
-// At N = 10, F = 5 a batch (~10 deliveries and a trigger) takes ~3200 shader
-// cycles (r06-F: 3600): ~2150 the deliveries (~215 each: three v_readlane ->
-// SALU hops), ~330 the loop head and ~720 the trigger (phase stamps in
-// r06-G5, since dropped: their SGPRs cost 6 %).  A/Bs of each change on one
-// box: profiles/r06-G_reg_kernel_ab.jsonl.
+// At N = 10, F = 5 a batch (~10 deliveries and a trigger) takes ~3050 shader
+// cycles (r06-F: 3600): ~2070 the deliveries (~207 each: three v_readlane ->
+// SALU hops), ~1000 the loop head and the trigger (~330 / ~720 with phase
+// stamps in r06-G5, since dropped: their SGPRs cost 6 %).  A/Bs of each change
+// on one box: profiles/r06-G_reg_kernel_ab.jsonl (register allocation moves
+// these numbers by several % either way, e.g. dropping the one remaining
+// cycle stamp costs 2-14 %: keep changes here under an A/B).
 template <int R, bool SM>
 __global__ void __launch_bounds__(64) benor_event_reg_kernel(KParams p) {
   using M = uint32_t;                                                 // node masks (N <= 16)
@@ -1160,13 +1162,15 @@ __global__ void __launch_bounds__(64) benor_event_reg_kernel(KParams p) {
   const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
   uint32_t *box = p.live_box;
   unsigned long long *const stats = p.ev_stats;
-  uint64_t pv_req = 0ull;
+  // the request word's low half (N <= 16): a 64-bit load whose high half is
+  // dead lets the register allocator reuse that half, and the reuse waits for
+  // the host-memory load at the next batch end
+  uint32_t pv_req = 0u;
   uint32_t pv_word = 0u, snap_served = 0u, seq_seen = 0u;
   bool apply_next = false;
   long long polled = 0;
   auto poll_issue = [&]() {
-    if (lane == 0u) pv_req = __hip_atomic_load(reinterpret_cast<uint64_t *>(box + kLiveReq), __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lane == 0u) pv_req = __hip_atomic_load(box + kLiveReq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (lane == 1u) pv_word = __hip_atomic_load(box, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (lane == 2u) pv_word = __hip_atomic_load(box + kSnapReq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     polled = poll_clock();
@@ -1221,6 +1225,7 @@ __global__ void __launch_bounds__(64) benor_event_reg_kernel(KParams p) {
     }
     uint32_t next = 0;
     uint64_t next_key = uni64(p.ev_nstops ? p.ev_stops[0] : ~0ull);
+    uint64_t next_e = next_key >> 12;              // the next scheduled stop's delivery (2^52 - 1: none)
     uint32_t len = m * N, cur = 1u, Rr = 0u, halted = 0u, overflow = 0u;
     uint64_t e = 0, trig = 0, cyc_steps = 0;
     uint32_t H = 0u, hi = 64u;                     // the block's picks, the next one's lane
@@ -1248,17 +1253,18 @@ __global__ void __launch_bounds__(64) benor_event_reg_kernel(KParams p) {
     auto batch = [&](auto small) -> uint32_t {
       // ---- scheduled GET /stop before delivery e
       bool crashed = false;
-      while ((next_key >> 12) == e) {
+      while (next_e == e) {
         kill((uint32_t)(next_key & 4095u));
         crashed = true;
         ++next;
         next_key = uni64(next < p.ev_nstops ? p.ev_stops[next] : ~0ull);
+        next_e = next_key >> 12;
       }
       if (box && hi == 64u) {                      // the clock is read once per 64 events
         if (poll_clock() - polled >= kPollCycles) {
           // live GET /stop requests (applied one poll after their sequence
           // word) and GET /getState snapshot requests, as the wave kernel
-          const uint64_t req = apply_next ? uni64(pv_req) : 0ull;
+          const uint32_t req = apply_next ? uni(pv_req) : 0u;
           const uint32_t seq = rl(pv_word, 1u), sreq = rl(pv_word, 2u);
           apply_next = seq != seq_seen;
           seq_seen = seq;
@@ -1307,7 +1313,7 @@ __global__ void __launch_bounds__(64) benor_event_reg_kernel(KParams p) {
       // block's end, the next stop or the first trigger
       uint32_t seg = 64u - hi;
       if (seg > len) seg = len;
-      if (next_key != ~0ull && (next_key >> 12) - e < seg) seg = (uint32_t)((next_key >> 12) - e);
+      if (next_e - e < seg) seg = (uint32_t)(next_e - e);   // e < next_e here
       uint32_t j = 0u, tw = 0u, tc = 0u;
       bool fired = false;
       seg = uni(seg);
@@ -1434,20 +1440,18 @@ __global__ void __launch_bounds__(64) benor_event_reg_kernel(KParams p) {
         if (!halted) base = ((((k + 1u) & 3u) << 6)) | inc_of(nx);
       }
       if (base != 0xFFFFFFFFu) {                   // the broadcast to all N nodes: positions len .. len + N - 1
+        if (decltype(small)::value && len + N <= 64u) {   // (cap >= 4 N^2 + 64 > 64)
+          const uint32_t d = lane - len;
+          P0 = d < N ? 2u * d + base : P0;
+          len += N;
+          return 0u;
+        }
         if (len + N > cap) {
           overflow = 1u;
           halted = 3u;
           return 1u;
         }
-        if (decltype(small)::value) {
-          if (len + N <= 64u) {
-            const uint32_t d = lane - len;
-            P0 = d < N ? 2u * d + base : P0;
-            len += N;
-            return 0u;
-          }
-          P[0] = P0;                               // the pool outgrows one register
-        }
+        if (decltype(small)::value) P[0] = P0;     // the pool outgrows one register
         const uint32_t r0 = len >> 6, r1 = (len + N - 1u) >> 6;
         if (r1 == 0u) {                            // within register 0
           const uint32_t d = lane - len;
