@@ -162,7 +162,11 @@ struct LiveSlot {
   uint32_t *dbox = nullptr;            // its device address
   unsigned char *d = nullptr;          // flag | states | hist | rounds | live ids | init x | stops | pool
   size_t bytes = 0;
-  std::vector<unsigned char> h;        // host staging of the buffer's head
+  // pinned host copy of the buffer's head: the upload reads it, and the
+  // result head (flag | states | hist | rounds) is copied back into it right
+  // behind the kernel, so the end of a run is one stream synchronisation
+  unsigned char *hp = nullptr;
+  size_t hp_bytes = 0;
 };
 constexpr size_t kSlotKeepBytes = 64u << 20;
 std::mutex g_slots_mu;
@@ -1026,6 +1030,7 @@ int bo_run_trial_states(const bo_trials_cfg *cfg, uint64_t trial, bo_node_state 
 namespace {
 void slot_destroy(LiveSlot *sl) {
   if (sl->d) (void)hipFree(sl->d);
+  if (sl->hp) (void)hipHostFree(sl->hp);
   if (sl->box) (void)hipHostFree(sl->box);
   if (sl->s) (void)hipStreamDestroy(sl->s);
   delete sl;
@@ -1101,13 +1106,21 @@ int wg_launch(LiveSlot *sl, const bo_trials_cfg *cfg, bool live, WgRun &run) {
     HIP_TRY(hipMalloc(&sl->d, bytes));
     sl->bytes = bytes;
   }
-  sl->h.assign(o_pool, 0);
+  if (sl->hp_bytes < o_pool) {                  // (the slot's stream is idle: its last run ended)
+    if (sl->hp) (void)hipHostFree(sl->hp);
+    sl->hp = nullptr;
+    sl->hp_bytes = 0;
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&sl->hp), o_pool, hipHostMallocDefault));
+    sl->hp_bytes = o_pool;
+  }
+  unsigned char *const h = sl->hp;
+  std::memset(h, 0, o_pool);
   std::vector<bo_node_state> st;
   initial_states(cfg, st);
-  std::memcpy(sl->h.data() + o_st, st.data(), sizeof(bo_node_state) * N);
-  if (m) std::memcpy(sl->h.data() + o_live, ids.data(), sizeof(uint32_t) * m);
-  std::memcpy(sl->h.data() + o_ix, cfg->init, N);
-  if (!stops.empty()) std::memcpy(sl->h.data() + o_stops, stops.data(), sizeof(uint64_t) * stops.size());
+  std::memcpy(h + o_st, st.data(), sizeof(bo_node_state) * N);
+  if (m) std::memcpy(h + o_live, ids.data(), sizeof(uint32_t) * m);
+  std::memcpy(h + o_ix, cfg->init, N);
+  if (!stops.empty()) std::memcpy(h + o_stops, stops.data(), sizeof(uint64_t) * stops.size());
   if (live) {
     // the mailbox: no request, no stop landed, no snapshot asked (the slot's
     // previous kernel has ended)
@@ -1115,7 +1128,7 @@ int wg_launch(LiveSlot *sl, const bo_trials_cfg *cfg, bool live, WgRun &run) {
     for (uint32_t i = 0; i < N; ++i) sl->box[benor::kLiveEv + i] = 0xFFFFFFFFu;
     std::memset(sl->box + benor::kSnapReq, 0, sizeof(uint32_t) * (benor::kSnapSt - benor::kSnapReq));
   }
-  HIP_TRY(hipMemcpyAsync(sl->d, sl->h.data(), o_pool, hipMemcpyHostToDevice, sl->s));
+  HIP_TRY(hipMemcpyAsync(sl->d, h, o_pool, hipMemcpyHostToDevice, sl->s));
   kp.hist = reinterpret_cast<unsigned long long *>(sl->d + o_h);
   kp.overflow = reinterpret_cast<uint32_t *>(sl->d);
   kp.node_out = reinterpret_cast<bo_node_state *>(sl->d + o_st);
@@ -1136,6 +1149,7 @@ int wg_launch(LiveSlot *sl, const bo_trials_cfg *cfg, bool live, WgRun &run) {
   run.N = N;
   run.F = cfg->F;
   HIP_TRY(benor::launch_event_wg(kp, 1, sl->s));
+  HIP_TRY(hipMemcpyAsync(h, sl->d, o_r + 4u, hipMemcpyDeviceToHost, sl->s));   // read by wg_read
   return BO_OK;
 }
 
@@ -1157,15 +1171,15 @@ int wg_read(LiveSlot *sl, const WgRun &run, uint32_t N, std::vector<bo_node_stat
         std::fclose(f);
       }
   }
-  std::vector<unsigned char> head(run.o_r + 4u);
-  hipError_t e = hipMemcpyAsync(head.data(), sl->d, head.size(), hipMemcpyDeviceToHost, sl->s);
-  if (e == hipSuccess) e = hipStreamSynchronize(sl->s);
+  // the head was copied into the pinned buffer behind the kernel (wg_launch)
+  const hipError_t e = hipStreamSynchronize(sl->s);
   if (e != hipSuccess) return hip_fail(e, "event-level run");
+  const unsigned char *head = sl->hp;
   uint32_t flag = 0, rounds = 0;
-  std::memcpy(&flag, head.data(), 4u);
-  std::memcpy(&rounds, head.data() + run.o_r, 4u);
+  std::memcpy(&flag, head, 4u);
+  std::memcpy(&rounds, head + run.o_r, 4u);
   states.resize(N);
-  std::memcpy(states.data(), head.data() + run.o_st, sizeof(bo_node_state) * N);
+  std::memcpy(states.data(), head + run.o_st, sizeof(bo_node_state) * N);
   int rc = plan_flag_error(flag);
   if (!rc && (rounds & 0x80000000u))
     rc = fail(BO_ERR_INTERNAL, "event-level message pool filled up: the run stopped early");
