@@ -137,7 +137,7 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {
 // Meanwhile the control wave runs the trigger, applies the next batch's
 // scheduled and live stops, serves snapshot requests and publishes the next
 // batch; the event waves then append the trigger's broadcast.
-template <int W, bool LP>
+template <int W, bool LP, bool ST>
 __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p) {
   constexpr uint32_t T = 64u * (uint32_t)W;        // event lanes
   const uint32_t HS = p.ev_hs;
@@ -316,7 +316,7 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
     if (ctl) {
       // diagnostics (BENOR_EVENT_STATS): batch counters and the shader cycles
       // between the control wave's barriers, accumulated per trial
-      unsigned long long *const stats = p.ev_stats;
+      unsigned long long *const stats = ST ? p.ev_stats : nullptr;   // ST: compiled in only for BENOR_EVENT_STATS
       uint64_t st[24] = {};
       uint64_t t_prev = stats ? __builtin_amdgcn_s_memtime() : 0ull;
       const uint64_t t_start = t_prev, w_start = stats ? (uint64_t)wall_clock64() : 0ull;
@@ -551,7 +551,7 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
       uint32_t par = 0u;
       // diagnostics (BENOR_EVENT_STATS): the first event wave's phase 1 split
       // into its own work and the wait for its pool words, and its phase 4
-      unsigned long long *const stats = tid == 64u ? p.ev_stats : nullptr;
+      unsigned long long *const stats = ST && tid == 64u ? p.ev_stats : nullptr;
       uint64_t s_work = 0ull, s_wait = 0ull, s_write = 0ull, s_pre = 0ull, s_drain = 0ull;
       for (;;) {
         __syncthreads();                           // ---- H
@@ -1549,17 +1549,24 @@ uint32_t event_wg_hash_slots(const KParams &p, uint32_t W) {
 
 uint32_t event_wg_lds_bytes(const KParams &p, uint32_t W) { return wg_lds_bytes(p, W, event_wg_hash_slots(p, W)); }
 
-template <int W, bool LP>
-static hipError_t launch_wg(KParams p, int grid, hipStream_t s) {
+template <int W, bool LP, bool ST>
+static hipError_t launch_wg1(KParams p, int grid, hipStream_t s) {
   p.ev_hs = event_wg_hash_slots(p, (uint32_t)W);
   const uint32_t lds = event_wg_lds_bytes(p, (uint32_t)W);
   if (lds > 64u * 1024u) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&benor_event_wg_kernel<W, LP>),
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&benor_event_wg_kernel<W, LP, ST>),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((benor_event_wg_kernel<W, LP>), dim3(grid), dim3(64 * (W + 1)), lds, s, p);
+  hipLaunchKernelGGL((benor_event_wg_kernel<W, LP, ST>), dim3(grid), dim3(64 * (W + 1)), lds, s, p);
   return hipGetLastError();
+}
+
+// the stamps and counters only where BENOR_EVENT_STATS asks for them: their
+// registers slow the control wave otherwise
+template <int W, bool LP>
+static hipError_t launch_wg(KParams p, int grid, hipStream_t s) {
+  return p.ev_stats ? launch_wg1<W, LP, true>(p, grid, s) : launch_wg1<W, LP, false>(p, grid, s);
 }
 
 // Small networks run on a one-wave kernel, unless a random /stop schedule
