@@ -781,6 +781,7 @@ __global__ void __launch_bounds__(64 * (W + 1)) benor_event_wg_kernel(KParams p)
 //   * the trigger (node.ts:52-80, :88-157), the stops, the mailbox and the
 //     snapshots are scalar code, node state in lane registers (lane = node).
 // The same definition as oracle (iii) event_trial() and the workgroup kernel.
+template <bool ST>
 __global__ void __launch_bounds__(64) benor_event_wave_kernel(KParams p) {
   extern __shared__ __attribute__((aligned(16))) uint32_t pool[];   // [cap] messages | picks | writers | ibox | comp
   const uint32_t lane = threadIdx.x;
@@ -793,7 +794,7 @@ __global__ void __launch_bounds__(64) benor_event_wave_kernel(KParams p) {
   const uint64_t all = N >= 64u ? ~0ull : (1ull << N) - 1ull;
   const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
   uint32_t *box = p.live_box;
-  unsigned long long *const stats = p.ev_stats;
+  unsigned long long *const stats = ST ? p.ev_stats : nullptr;   // ST: only for BENOR_EVENT_STATS
   // the mailbox poll, issued and consumed >= kPollCycles apart (as the
   // workgroup kernel's control wave): the wave waits for no PCIe round trip
   uint64_t pv_req = 0ull;
@@ -1601,12 +1602,14 @@ hipError_t launch_event_wg(const KParams &p, int grid, hipStream_t s) {
   }
   if (event_wave_form(p)) {
     const uint32_t lds = event_wave_lds_bytes(p);
+    const void *fn = p.ev_stats ? reinterpret_cast<const void *>(&benor_event_wave_kernel<true>)
+                                : reinterpret_cast<const void *>(&benor_event_wave_kernel<false>);
     if (lds > 64u * 1024u) {
-      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&benor_event_wave_kernel),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(benor_event_wave_kernel, dim3(grid), dim3(64), lds, s, p);
+    if (p.ev_stats) hipLaunchKernelGGL((benor_event_wave_kernel<true>), dim3(grid), dim3(64), lds, s, p);
+    else hipLaunchKernelGGL((benor_event_wave_kernel<false>), dim3(grid), dim3(64), lds, s, p);
     return hipGetLastError();
   }
   const uint32_t W = event_wg_waves(p);
